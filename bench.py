@@ -1,0 +1,208 @@
+"""Benchmark: TransMIL training-step throughput (slides/sec, fwd+bwd) on MI355X.
+
+BASELINE.json metric: "slides/sec (fwd+bwd) at N=8192 patches, d=512; 1/2/4/8 MI355X".
+Workload (configs[1]): TransMIL_feat 2-class, one synthetic bag of N=8192 x 512
+features per GPU per step, bf16 MFMA operands (fp32 softmax / LayerNorm /
+pseudo-inverse / residual stream / master weights).
+
+One step = forward (train mode, dropout 0.7 active) -> CrossEntropy(one-hot)
+-> backward -> gradient all-reduce over ranks (RCCL, N > 1) -> Lookahead(RAdam)
+optimizer step -> zero_grad.  Bags are resident in HBM before timing starts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 8192]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
+
+Prints ONE JSON line on rank 0.  Extra objects:
+  roofline      -- the dominant kernel's achieved rate (algorithmic bytes or flops
+                   per launch / its mean HIP-event duration over the timed steps)
+  cpu_baseline  -- the fp32 CPU oracle (oracle/transmil_ref.py, logits path) on a
+                   bounded sample of the same workload, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFS = 2500.0       # dense bf16 MFMA spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=8192, help="patches per bag")
+    ap.add_argument("--classes", type=int, default=2)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--probe", default="a1_fwd", help="call site timed for the roofline object")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=3)
+    return ap.parse_args()
+
+
+def roofline_model(site, n_patches, dtype_bytes):
+    """Algorithmic bytes / flops of ONE launch of `site`."""
+    import math
+    G = math.ceil(math.sqrt(n_patches))
+    S = G * G + 1
+    n = (S + 255) // 256 * 256
+    heads, dh, m = 8, 64, 256
+    t = dtype_bytes
+    if site == "a1_fwd":
+        # read q, v (conv) [n, 512] T; write merged [n, 512] T + lse [8, n] fp32; landmarks/Y fp32
+        byts = 3 * n * 512 * t + heads * n * 4 + 2 * heads * m * dh * 4
+        flops = 2 * 2 * heads * n * m * dh + 2 * 33 * heads * n * dh
+        return dict(bytes=byts, flops=flops)
+    if site == "qkv_gemm":
+        byts = n * 512 * t + 1536 * 512 * t + 3 * n * 512 * t
+        flops = 2 * n * 512 * 1536
+        return dict(bytes=byts, flops=flops)
+    if site == "a3_fwd":
+        byts = 2 * n * 512 * t + heads * m * dh * 4 * 2
+        flops = 2 * 2 * heads * m * n * dh
+        return dict(bytes=byts, flops=flops)
+    raise ValueError(site)
+
+
+def cpu_baseline(n_patches, ncls, steps):
+    """fp32 CPU oracle, logits path (no unused n'xn' attention product), timed on this host."""
+    from oracle.transmil_ref import TransMIL as RefTransMIL, TransLayer
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    TransLayer.compute_attn = False
+    torch.manual_seed(0)
+    model = RefTransMIL(ncls, 512, 512).train()
+    opt = torch.optim.RAdam(model.parameters(), lr=2e-4)
+    x = torch.rand(1, n_patches, 512)
+    y = torch.tensor([1])
+    lossf = torch.nn.CrossEntropyLoss()
+
+    def step():
+        logits = model(x)
+        loss = lossf(logits, torch.nn.functional.one_hot(y, ncls).float())
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    TransLayer.compute_attn = True
+    return dict(value=steps / dt, unit="slides/sec", cores=threads, kind="port",
+                sample=f"{steps} fwd+bwd+RAdam steps (after 1 warm-up), 1 bag N={n_patches}x512, fp32, "
+                       f"train mode, torch.set_num_threads({threads})")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from transmil_deepgraft_amd.models import TransMIL
+    from transmil_deepgraft_amd.interface import TransMILTask, GradAllReduce
+    from transmil_deepgraft_amd import engine
+
+    torch.manual_seed(1234)  # same random-init weights on every rank
+    model = TransMIL(args.classes, 512, 512).to(dev).train()
+    model.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
+    task = TransMILTask(model)
+    opt = task.configure_optimizers()[0][0]
+    allreduce = GradAllReduce(model.parameters())
+
+    g = torch.Generator(device=dev).manual_seed(2021 + rank)
+    bags = [torch.rand(1, args.n, 512, device=dev, generator=g) for _ in range(4)]
+    labels = [torch.randint(0, args.classes, (1,), device=dev, generator=g) for _ in range(4)]
+
+    def step(i):
+        loss = task.training_step((bags[i % 4], labels[i % 4], None))
+        loss.backward()
+        allreduce()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    for i in range(args.warmup):
+        step(i)
+    engine.probe.target = args.probe
+    engine.probe.events.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+        if (i + 1) % 50 == 0 and rank == 0:
+            print(f"# step {i + 1}/{args.steps}", file=sys.stderr, flush=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    engine.probe.target = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ev = engine.probe.events
+    kernel_ms = sum(s.elapsed_time(e) for s, e in ev) / max(len(ev), 1)
+
+    if rank == 0:
+        slides = args.steps * world
+        tb = 2 if args.dtype == "bf16" else 4
+        rm = roofline_model(args.probe, args.n, tb)
+        sec = kernel_ms / 1e3
+        ach_bw = rm["bytes"] / sec / 1e9
+        ach_fl = rm["flops"] / sec / 1e12
+        peak_fl = BF16_PEAK_TFS if args.dtype == "bf16" else 157.3
+        hbm_bound = rm["flops"] / rm["bytes"] < peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
+        roof = (dict(bound="hbm", achieved=round(ach_bw, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                     frac=round(ach_bw / HBM_PEAK_GBS, 4), traffic=None)
+                if hbm_bound else
+                dict(bound="mfma", achieved=round(ach_fl, 2), peak=peak_fl, unit="TFLOP/s",
+                     frac=round(ach_fl / peak_fl, 4), traffic=None))
+        roof.update(kernel=args.probe, kernel_ms=round(kernel_ms, 5), launches=len(ev),
+                    algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])
+        out = {
+            "metric": "slides/sec (fwd+bwd) at N=8192 patches, d=512",
+            "value": round(slides / elapsed, 3),
+            "unit": "slides/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (torch.rand bags resident in HBM, random-init weights)",
+            "config": {"workload": f"TransMIL_feat {args.classes}-class, 1 bag N={args.n}x512 per GPU, "
+                                   "train step fwd+CE+bwd+allreduce+Lookahead(RAdam)",
+                       "global_batch": world, "seq_len": args.n, "parallelism": f"dp{world}"},
+            "roofline": roof,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.n, args.classes, args.cpu_steps)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/* C ABI of libtransmil_hip.so -- the MI355X (gfx950) TransMIL hot path.
+ *
+ * The reference has no native boundary: its plugin surface is Python
+ * (`models.TransMIL` imported by ModelInterface.load_model,
+ * code/models/model_interface.py:1256-1293, and the third-party
+ * `nystrom_attention.NystromAttention`, code/models/TransMIL.py:5,26-34,47).
+ * This ABI is what the drop-in Python module (transmil_deepgraft_amd/models/
+ * TransMIL.py and transmil_deepgraft_amd/nystrom_attention.py) binds through
+ * ctypes; each entry point below names the reference op it replaces.
+ *
+ * Conventions (all entry points):
+ *   - device pointers are caller-owned; nothing is allocated inside;
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
+ *   - no host synchronisation, so every call is hipGraph-capturable;
+ *   - deterministic: no float atomics, fixed reduction orders;
+ *   - return 0 on success, 1 on a bad argument, 2 on a launch error;
+ *     tm_last_error() returns the thread-local message.
+ *   - dtype enum: TM_F32 = 0, TM_BF16 = 1 (activations / MFMA operands).
+ */
+#ifndef TRANSMIL_HIP_H
+#define TRANSMIL_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- errors / build info ---------------------------------------------- */
+const char* tm_last_error(void);
+const char* tm_build_info(void);
+
+/* ---- dense GEMM with fused epilogues (gemm.hip) -----------------------
+ * C[m,n] = epi(alpha * sum_k A(m,k) B(k,n)),
+ *   A(m,k) = a_trans ? A[k*lda+m] : A[m*lda+k];  B(k,n) = b_kn ? B[k*ldb+n] : B[n*ldb+k].
+ * Replaces the nn.Linear call sites of _fc1 (code/models/TransMIL.py:128-133),
+ * NystromAttention.to_qkv / to_out (SURVEY.md App. A eq. 2, 10) and their
+ * backward products. */
+enum { TM_EPI_PLAIN = 0, TM_EPI_QKV = 1, TM_EPI_SPLITK = 2 };
+typedef struct tm_gemm_args {
+  int M, N, K;
+  int lda, ldb, ldc;
+  int a_trans, b_kn;
+  int ab_dtype, c_dtype;
+  int splits, k_per_split;
+  int mode;            /* TM_EPI_* */
+  float alpha;
+  const float* bias;   /* [N] fp32 or NULL */
+  int gelu;            /* exact erf GELU after bias */
+  void* pre;           /* pre-activation store (c_dtype), row m, ld_pre; or NULL */
+  int ld_pre;
+  float drop_p, drop_scale;
+  uint64_t seed;
+  const float* resid;  /* fp32 residual added last, indexed like C; or NULL */
+  int accumulate;      /* C += result */
+  /* output row map (grp_in > 0): bag = m / grp_in, t = m % grp_in - skip;
+   * t < 0 -> not stored; row = bag*grp_out + out_off + t; if t < dup_n also
+   * stored at bag*grp_out + dup_off + t (TransMIL grid padding, :177-180) */
+  int grp_in, skip, grp_out, out_off, dup_n, dup_off;
+  /* TM_EPI_QKV: m = bag*seq + t, n = which*(nh*dh) + head*dh + d ->
+   * C[((which*nbags + bag)*nh + head)*seq + t][d]; q (which==0) scaled by qscale */
+  int nbags, nh, dh, seq;
+  float qscale;
+} tm_gemm_args;
+
+int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* args, void* stream);
+int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
+                     int accumulate, void* stream);
+long long tm_colsum_workspace(int rows, int cols, int rows_per_chunk);
+int tm_colsum(const void* X, int dtype, int rows, int cols, int ld, int rows_per_chunk,
+              float* work, float* out, int accumulate, void* stream);
+
+/* ---- LayerNorm / head (layernorm.hip) ----------------------------------
+ * TransLayer.norm (code/models/TransMIL.py:23,47) and the final norm + _fc
+ * head (:154-155, 202-204).  x rows are [B*S, D] fp32; y is written into the
+ * front-padded [B, n_pad, D] layout (rows b*n_pad + pad + i; pad rows zeroed). */
+int tm_layernorm_fwd(const float* x, const float* gamma, const float* beta, float eps, int rows, int D,
+                     int S, int n_pad, int pad, int dtype, void* y, float* mean, float* rstd, void* stream);
+long long tm_layernorm_bwd_workspace(int rows, int D, int rows_per_block);
+/* dx_accum[r] += LN'(dy) (dy read from the padded layout); dgamma/dbeta written */
+int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const float* gamma, const float* mean,
+                     const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
+                     float* dx_accum, float* work, float* dgamma, float* dbeta, void* stream);
+int tm_head_fwd(const float* h, int B, int S, int D, const float* gamma, const float* beta, float eps,
+                const float* W, const float* bias, int C, float* logits, float* xhat, float* rstd,
+                void* stream);
+/* writes dh[b*S*D + :D] (row 0 of each bag); other rows untouched */
+int tm_head_bwd(const float* dlogits, int B, int C, int S, int D, const float* xhat, const float* rstd,
+                const float* gamma, const float* beta, const float* W, float* dW, float* dbias,
+                float* dgamma, float* dbeta, float* dh, void* stream);
+
+/* ---- NystromAttention core (nystrom.hip) --------------------------------
+ * SURVEY.md App. A eq. 4-9 of the third-party nystrom_attention package
+ * (call site code/models/TransMIL.py:47).  dim_head = 64, 256 landmarks.
+ * q/k/v: [B*h, n, 64] (T), n a multiple of 256; landmarks [B*h, 256, 64]. */
+int tm_nys_landmarks(int dtype, const void* q, const void* k, int nbh, int n, float* ql, float* kl,
+                     void* ql_t, void* kl_t, void* stream);
+int tm_nys_sim2_softmax(const float* ql, const float* kl, int nbh, float* a2, void* stream);
+int tm_softmax_bwd_rows256(const float* a, const float* da, float* ds, int rows, void* stream);
+long long tm_nys_a3_workspace(int nbh, int n);
+/* W = softmax(ql k^T) v  [B*h,256,64] fp32, lse3 [B*h,256] */
+int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
+                  float* w, float* lse3, void* stream);
+/* merged[b][t][head*64+d] = softmax(q kl^T) y + conv33(v); lse1 [B*h, n] */
+int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const float* kl, const float* y,
+                  const float* wconv, int nbh, int nh, int n, void* merged, float* lse1, void* stream);
+int tm_nys_rowdot_cast(int dtype, const float* dw, const float* w, int rows, float* dd, void* dw_t, void* stream);
+int tm_cast_f32(int dtype, const float* x, void* y, long long count, void* stream);
+long long tm_nys_conv_bwd_workspace(int nbags, int nh, int n);
+int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merged, const void* v, const float* wconv,
+                    int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv, void* stream);
+long long tm_nys_a1_bwd_workspace(int nbh, int n, int queries_per_wg);
+int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t,
+                  const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
+                  float* dq, float* work, float* dkl, float* dy, int accumulate, void* stream);
+long long tm_nys_a3_bwd_workspace(int nbh, int n);
+int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
+                  const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
+                  float* work, float* dql, void* stream);
+int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const float* dk, const float* dkl,
+                         const float* dv, int nbags, int nh, int n, float scale, void* dqkv, void* stream);
+
+/* ---- pseudo-inverse + small fp32 batched products (pinv.hip) -------------
+ * moore_penrose_iter_pinv of nystrom_attention (App. A eq. 7).
+ * C = diag*I + alpha*(op(A) op(B) [+ op(A2) op(B2)]) + e1*E1 + e2*E2, batched;
+ * op(X) = X^T when the t-flag is set; E1/E2 share C's layout. */
+typedef struct tm_bmm_job {
+  const float* A; const float* B; int ta, tb; int lda, ldb; long long sa, sb;
+  const float* A2; const float* B2; int ta2, tb2; int lda2, ldb2; long long sa2, sb2;
+  const float* E1; float e1; const float* E2; float e2;
+  float alpha, diag;
+  float* C; int ldc; long long sc;
+  int M, N, K;
+} tm_bmm_job;
+int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, void* stream);
+long long tm_pinv_saved_floats(int nbh, int iters);
+int tm_pinv_fwd(const float* X, int nbh, int iters, float* saved, void* stream);
+long long tm_pinv_bwd_workspace_floats(int nbh);
+int tm_pinv_bwd(const float* X, int nbh, int iters, const float* saved, float* dZ, float* work, float* dX,
+                void* stream);
+
+/* ---- PPEG (ppeg.hip) -- code/models/TransMIL.py:60-75 -------------------- */
+int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, const float* b5, const float* w3,
+                 const float* b3, int D, float* wfold, float* bfold, void* stream);
+int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
+                void* stream);
+long long tm_ppeg_bwd_workspace(int B, int G, int D);
+int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const float* wfold, float* dx,
+                float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
+                float* db3, void* stream);
+
+/* ---- glue (glue.hip) -- code/models/TransMIL.py:177-186 ------------------ */
+int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream);
+int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int pad, int D, float p,
+                       uint64_t seed, void* out, void* stream);
+/* NystromAttention eq. 1 for a raw input: [B*S, D] fp32 -> front-padded [B, n_pad, D] T */
+int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, int pad, int D, void* y, void* stream);
+int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
+                    void* dpre, float* dcls, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRANSMIL_HIP_H */

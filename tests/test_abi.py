@@ -1,0 +1,57 @@
+"""C-ABI checks that need no GPU: the library loads and exports every entry
+point ``include/transmil_hip.h`` declares; the ctypes table matches; no compute."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "transmil_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(tm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "tm_gemm" in syms and "tm_pinv_fwd" in syms and "tm_nys_a1_bwd" in syms
+    assert len(syms) >= 35
+
+
+def test_library_exports_every_declared_symbol():
+    from transmil_deepgraft_amd import _lib
+    lib = _lib.lib()
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_ctypes_table_covers_header():
+    from transmil_deepgraft_amd import _lib
+    assert set(declared_symbols()) == set(_lib.EXPORTED)
+
+
+def test_struct_layouts_match_c():
+    """Field offsets of the ctypes mirrors against the C compiler's view."""
+    from transmil_deepgraft_amd._lib import GemmArgs, BmmJob
+    # values printed by a g++ build of offsetof() over include/transmil_hip.h
+    assert ctypes.sizeof(GemmArgs) == 160
+    assert GemmArgs.seed.offset == 96 and GemmArgs.qscale.offset == 156
+    assert ctypes.sizeof(BmmJob) == 176
+    assert BmmJob.C.offset == 136 and BmmJob.K.offset == 168 and BmmJob.E1.offset == 96
+
+
+def test_error_path_without_gpu():
+    """A bad argument is rejected before any device work, with a message."""
+    from transmil_deepgraft_amd import _lib
+    with pytest.raises(RuntimeError, match="n must be a positive multiple of 256"):
+        _lib.call("tm_nys_landmarks", 1, None, None, 8, 100, None, None, None, None, None)
+    assert "multiple of 256" in _lib.last_error()
+
+
+def test_build_info():
+    from transmil_deepgraft_amd import _lib
+    assert b"gfx950" in _lib.lib().tm_build_info()

@@ -1,0 +1,241 @@
+"""Kernel-level numerics on the MI355X, each HIP entry point against a plain
+PyTorch fp64 reference of the same op (through the C ABI)."""
+import ctypes as C
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _lib():
+    from transmil_deepgraft_amd import _lib
+    return _lib
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("a_trans,b_kn", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_layouts(dtype, a_trans, b_kn):
+    from transmil_deepgraft_amd.engine import gemm
+    from transmil_deepgraft_amd._lib import BF16, F32
+    code = BF16 if dtype == torch.bfloat16 else F32
+    M, N, K = 300, 256, 168
+    g = torch.Generator(device="cpu").manual_seed(1)
+    A = torch.randn(M, K, generator=g).to(dtype)
+    B = torch.randn(K, N, generator=g).to(dtype)
+    ref = A.double() @ B.double()
+    As = (A.t().contiguous() if a_trans else A).to(DEV)
+    Bs = (B.contiguous() if b_kn else B.t().contiguous()).to(DEV)
+    out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    gemm(As, Bs, out, M, N, K, lda=M if a_trans else K, ldb=N if b_kn else K, ldc=N, a_trans=a_trans,
+         b_kn=b_kn, dtype=code, c_dtype=F32)
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogue_bias_gelu_rowmap_dup(dtype):
+    from transmil_deepgraft_amd.engine import gemm
+    from transmil_deepgraft_amd._lib import BF16, F32
+    code = BF16 if dtype == torch.bfloat16 else F32
+    Bg, Nn, F, D = 2, 37, 64, 128
+    G = 7
+    add, S = G * G - Nn, G * G + 1
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(Bg * Nn, F, generator=g).to(dtype)
+    w = torch.randn(D, F, generator=g).to(dtype) * 0.2
+    b = torch.randn(D, generator=g)
+    pre_ref = x.double() @ w.double().t() + b.double()
+    y_ref = torch.nn.functional.gelu(pre_ref)
+    H = torch.full((Bg * S, D), 7.0, device=DEV)
+    pre = torch.empty(Bg * Nn, D, device=DEV)
+    gemm(x.to(DEV), w.to(DEV), H, Bg * Nn, D, F, lda=F, ldb=F, ldc=D, dtype=code, c_dtype=F32, bias=b.to(DEV),
+         gelu=True, pre=pre, ld_pre=D, rowmap=(Nn, 0, S, 1, add, 1 + Nn))
+    torch.cuda.synchronize()
+    Hc = H.cpu().view(Bg, S, D)
+    yr = y_ref.view(Bg, Nn, D)
+    assert (Hc[:, 0] == 7.0).all()
+    assert _rel(Hc[:, 1:1 + Nn], yr) < 1e-5
+    assert _rel(Hc[:, 1 + Nn:], yr[:, :add]) < 1e-5
+    assert _rel(pre.cpu(), pre_ref) < 1e-5
+
+
+def test_gemm_dropout_residual_and_splitk():
+    from transmil_deepgraft_amd.engine import gemm, weight_grad, Pool
+    from transmil_deepgraft_amd._lib import F32
+    M, N, K = 512, 256, 128
+    g = torch.Generator().manual_seed(3)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g)
+    R = torch.randn(M, N, generator=g)
+    out = torch.empty(M, N, device=DEV)
+    gemm(A.to(DEV), W.to(DEV), out, M, N, K, lda=K, ldb=K, ldc=N, dtype=F32, c_dtype=F32, drop_p=0.7, seed=123,
+         resid=R.to(DEV))
+    torch.cuda.synchronize()
+    o = out.cpu() - R
+    full = (A.double() @ W.double().t()) / 0.3
+    kept = o.abs() > 0
+    frac = kept.double().mean().item()
+    assert abs(frac - 0.3) < 0.02
+    assert _rel(o[kept], full[kept]) < 1e-5
+    # split-K weight gradient: out[m,n] = sum_k dY[k,m] X[k,n]
+    dY = torch.randn(4000, 96, generator=g)
+    X = torch.randn(4000, 160, generator=g)
+    res = torch.empty(96, 160, device=DEV)
+    weight_grad(dY.to(DEV), X.to(DEV), res, 96, 160, 4000, ldy=96, ldx=160, dtype=F32, work_pool=Pool(DEV))
+    torch.cuda.synchronize()
+    assert _rel(res.cpu(), dY.double().t() @ X.double()) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_qkv_scatter(dtype):
+    from transmil_deepgraft_amd.engine import gemm
+    from transmil_deepgraft_amd._lib import BF16, F32
+    code = BF16 if dtype == torch.bfloat16 else F32
+    Bg, n, D, nh = 2, 256, 512, 8
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(Bg * n, D, generator=g).to(dtype)
+    w = (torch.randn(3 * D, D, generator=g) * 0.05).to(dtype)
+    out = torch.empty(3, Bg * nh, n, 64, dtype=dtype, device=DEV)
+    gemm(x.to(DEV), w.to(DEV), out, Bg * n, 3 * D, D, lda=D, ldb=D, ldc=0, dtype=code, qkv=(Bg, nh, 64, n, 0.125))
+    torch.cuda.synchronize()
+    ref = (x.double() @ w.double().t()).view(Bg, n, 3, nh, 64).permute(2, 0, 3, 1, 4).reshape(3, Bg * nh, n, 64)
+    ref[0] *= 0.125
+    tol = 1e-5 if dtype == torch.float32 else 8e-3
+    assert _rel(out.cpu(), ref) < tol
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+def test_layernorm_fwd_bwd():
+    from transmil_deepgraft_amd import ops
+    ln = torch.nn.LayerNorm(512).to(DEV)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(3, 77, 512, device=DEV, requires_grad=True)
+    y = ops.layer_norm(ln, x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    x2 = x.detach().double().requires_grad_()
+    w2 = ln.weight.detach().double().requires_grad_()
+    b2 = ln.bias.detach().double().requires_grad_()
+    y2 = torch.nn.functional.layer_norm(x2, (512,), w2, b2, 1e-5)
+    y2.backward(gy.double())
+    assert _rel(y, y2) < 1e-5
+    assert _rel(x.grad, x2.grad) < 1e-4
+    assert _rel(ln.weight.grad, w2.grad) < 1e-4
+    assert _rel(ln.bias.grad, b2.grad) < 1e-4
+
+
+# ----------------------------------------------------------------------------- PPEG
+@pytest.mark.parametrize("G", [1, 5, 32])
+def test_ppeg_fwd_bwd(G):
+    from oracle.transmil_ref import PPEG as RefPPEG
+    from transmil_deepgraft_amd.models.TransMIL import PPEG
+    torch.manual_seed(G)
+    ref = RefPPEG(64).double()
+    ours = PPEG(64).to(DEV)
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = torch.randn(2, 1 + G * G, 64, dtype=torch.float64)
+    y_ref = ref(x.clone().requires_grad_(), G, G)
+    xr = x.clone().requires_grad_()
+    y_ref = ref(xr, G, G)
+    gy = torch.randn_like(y_ref)
+    y_ref.backward(gy)
+    xo = x.float().to(DEV).requires_grad_()
+    y = ours(xo, G, G)
+    y.backward(gy.float().to(DEV))
+    assert _rel(y.cpu(), y_ref) < 1e-5
+    assert _rel(xo.grad.cpu(), xr.grad) < 1e-5
+    for (n1, p1), (n2, p2) in zip(ours.named_parameters(), ref.named_parameters()):
+        assert _rel(p1.grad.cpu(), p2.grad) < 1e-4, n1
+
+
+# ----------------------------------------------------------------------------- pinv
+def test_pinv_fwd_bwd_fp32_exact_path():
+    from oracle.nystrom_ref import moore_penrose_iter_pinv
+    from transmil_deepgraft_amd import _lib
+    from transmil_deepgraft_amd.engine import _p, _stream
+    nbh = 8
+    g = torch.Generator().manual_seed(7)
+    a = torch.softmax(torch.randn(nbh, 256, 256, generator=g, dtype=torch.float64) * 0.3, dim=-1)
+    a64 = a.clone().requires_grad_()
+    z_ref = moore_penrose_iter_pinv(a64, 6)
+    gz = torch.randn(nbh, 256, 256, generator=g, dtype=torch.float64) * 1e-3
+    z_ref.backward(gz)
+    X = a.float().to(DEV)
+    saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=DEV)
+    _lib.call("tm_pinv_fwd", _p(X), nbh, 6, _p(saved), _stream())
+    z = saved[6 * nbh * 65536:7 * nbh * 65536].view(nbh, 256, 256)
+    dz = gz.float().to(DEV).contiguous()
+    work = torch.empty(_lib.query("tm_pinv_bwd_workspace_floats", nbh), device=DEV)
+    dX = torch.empty(nbh, 256, 256, device=DEV)
+    _lib.call("tm_pinv_bwd", _p(X), nbh, 6, _p(saved), _p(dz), _p(work), _p(dX), _stream())
+    torch.cuda.synchronize()
+    assert _rel(z.cpu(), z_ref.detach()) < 2e-4
+    assert _rel(dX.cpu(), a64.grad) < 2e-3
+
+
+# ----------------------------------------------------------------------------- NystromAttention
+@pytest.mark.parametrize("S", [2, 101, 257, 1025, 2000])
+def test_nystrom_attention_fp32_vs_oracle(S):
+    from oracle.nystrom_ref import NystromAttention as Ref
+    from transmil_deepgraft_amd.nystrom_attention import NystromAttention
+    torch.manual_seed(S)
+    ref = Ref(dim=512, dim_head=64, heads=8, num_landmarks=256, pinv_iterations=6, residual=True).double().eval()
+    with torch.no_grad():
+        ref.res_conv.weight.mul_(3.0)
+    ours = NystromAttention(dim=512, dim_head=64, heads=8, num_landmarks=256, pinv_iterations=6,
+                            residual=True).to(DEV).eval()
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    ours.compute_dtype = torch.float32
+    x = torch.randn(2, S, 512, dtype=torch.float64)
+    xr = x.clone().requires_grad_()
+    out_ref = ref(xr)
+    gy = torch.randn_like(out_ref)
+    out_ref.backward(gy)
+    xo = x.float().to(DEV).requires_grad_()
+    out = ours(xo)
+    out.backward(gy.float().to(DEV))
+    assert _rel(out.cpu(), out_ref) < 1e-4
+    assert _rel(xo.grad.cpu(), xr.grad) < 1e-3
+    for (n1, p1), (n2, p2) in zip(ours.named_parameters(), ref.named_parameters()):
+        assert _rel(p1.grad.cpu(), p2.grad) < 1e-3, n1
+
+
+def test_nystrom_attention_bf16_close():
+    from oracle.nystrom_ref import NystromAttention as Ref
+    from transmil_deepgraft_amd.nystrom_attention import NystromAttention
+    torch.manual_seed(11)
+    ref = Ref(dim=512).double().eval()
+    ours = NystromAttention(dim=512).to(DEV).eval()
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = torch.randn(1, 1500, 512, dtype=torch.float64)
+    with torch.no_grad():
+        out_ref = ref(x)
+        out = ours(x.float().to(DEV))
+    assert _rel(out.cpu(), out_ref) < 3e-2
+
+
+def test_return_attn_matrix():
+    from oracle.nystrom_ref import NystromAttention as Ref
+    from transmil_deepgraft_amd.nystrom_attention import NystromAttention
+    torch.manual_seed(12)
+    ref = Ref(dim=512).double().eval()
+    ours = NystromAttention(dim=512).to(DEV).eval()
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    x = torch.randn(1, 300, 512, dtype=torch.float64)
+    with torch.no_grad():
+        _, attn_ref = ref(x, return_attn=True)
+        _, attn = ours(x.float().to(DEV), return_attn=True)
+    assert attn.shape == attn_ref.shape
+    assert _rel(attn.cpu(), attn_ref) < 1e-3

@@ -1,0 +1,119 @@
+"""ctypes binding of ``libtransmil_hip.so`` (the C ABI in ``include/transmil_hip.h``).
+
+The product path has no CPU or eager-PyTorch fallback: if the library is
+missing or cannot be loaded, :func:`lib` raises.  Every call checks the
+returned status and raises ``RuntimeError`` with ``tm_last_error()``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TRANSMIL_HIP_LIB", os.path.join(_HERE, "libtransmil_hip.so"))
+
+F32, BF16 = 0, 1
+EPI_PLAIN, EPI_QKV, EPI_SPLITK = 0, 1, 2
+
+P = C.c_void_p
+I = C.c_int
+L = C.c_longlong
+Fl = C.c_float
+U64 = C.c_uint64
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [("M", I), ("N", I), ("K", I), ("lda", I), ("ldb", I), ("ldc", I),
+                ("a_trans", I), ("b_kn", I), ("ab_dtype", I), ("c_dtype", I),
+                ("splits", I), ("k_per_split", I), ("mode", I), ("alpha", Fl),
+                ("bias", P), ("gelu", I), ("pre", P), ("ld_pre", I),
+                ("drop_p", Fl), ("drop_scale", Fl), ("seed", U64), ("resid", P),
+                ("accumulate", I), ("grp_in", I), ("skip", I), ("grp_out", I),
+                ("out_off", I), ("dup_n", I), ("dup_off", I), ("nbags", I), ("nh", I),
+                ("dh", I), ("seq", I), ("qscale", Fl)]
+
+
+class BmmJob(C.Structure):
+    _fields_ = [("A", P), ("B", P), ("ta", I), ("tb", I), ("lda", I), ("ldb", I), ("sa", L), ("sb", L),
+                ("A2", P), ("B2", P), ("ta2", I), ("tb2", I), ("lda2", I), ("ldb2", I), ("sa2", L), ("sb2", L),
+                ("E1", P), ("e1", Fl), ("E2", P), ("e2", Fl), ("alpha", Fl), ("diag", Fl),
+                ("C", P), ("ldc", I), ("sc", L), ("M", I), ("N", I), ("K", I)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "tm_last_error": (C.c_char_p, []),
+    "tm_build_info": (C.c_char_p, []),
+    "tm_gemm": (I, [P, P, P, C.POINTER(GemmArgs), P]),
+    "tm_splitk_reduce": (I, [P, P, I, L, Fl, I, P]),
+    "tm_colsum_workspace": (L, [I, I, I]),
+    "tm_colsum": (I, [P, I, I, I, I, I, P, P, I, P]),
+    "tm_layernorm_fwd": (I, [P, P, P, Fl, I, I, I, I, I, I, P, P, P, P]),
+    "tm_layernorm_bwd_workspace": (L, [I, I, I]),
+    "tm_layernorm_bwd": (I, [P, I, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P]),
+    "tm_head_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P]),
+    "tm_head_bwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
+    "tm_nys_landmarks": (I, [I, P, P, I, I, P, P, P, P, P]),
+    "tm_nys_sim2_softmax": (I, [P, P, I, P, P]),
+    "tm_softmax_bwd_rows256": (I, [P, P, P, I, P]),
+    "tm_nys_a3_workspace": (L, [I, I]),
+    "tm_nys_a3_fwd": (I, [I, P, P, P, I, I, P, P, P, P]),
+    "tm_nys_a1_fwd": (I, [I, P, P, P, P, P, I, I, I, P, P, P]),
+    "tm_nys_rowdot_cast": (I, [I, P, P, I, P, P, P]),
+    "tm_cast_f32": (I, [I, P, P, L, P]),
+    "tm_nys_conv_bwd_workspace": (L, [I, I, I]),
+    "tm_nys_conv_bwd": (I, [I, P, P, P, P, I, I, I, P, P, P, P, P]),
+    "tm_nys_a1_bwd_workspace": (L, [I, I, I]),
+    "tm_nys_a1_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P, P, P, P, I, P]),
+    "tm_nys_a3_bwd_workspace": (L, [I, I]),
+    "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, P]),
+    "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
+    "tm_bmm": (I, [C.POINTER(BmmJob), I, I, P]),
+    "tm_pinv_saved_floats": (L, [I, I]),
+    "tm_pinv_fwd": (I, [P, I, I, P, P]),
+    "tm_pinv_bwd_workspace_floats": (L, [I]),
+    "tm_pinv_bwd": (I, [P, I, I, P, P, P, P, P]),
+    "tm_ppeg_fold": (I, [P, P, P, P, P, P, I, P, P, P]),
+    "tm_ppeg_fwd": (I, [P, I, I, I, P, P, P, P]),
+    "tm_ppeg_bwd_workspace": (L, [I, I, I]),
+    "tm_ppeg_bwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
+    "tm_put_cls": (I, [P, I, I, I, P, P]),
+    "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P]),
+    "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
+    "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """Load the HIP library (once).  Raises if it is missing: there is no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"transmil_deepgraft_amd: HIP library not found at {LIB_PATH}; build it with "
+                "`make -C transmil_deepgraft_amd/csrc -j8` (or __graft_entry__.build())")
+        handle = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def last_error() -> str:
+    return lib().tm_last_error().decode()
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed (rc={rc}): {last_error()}")
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(lib(), name)(*args))

@@ -1,0 +1,109 @@
+// Glue around the TransMIL forward (code/models/TransMIL.py:167-211) that is not
+// a GEMM, attention or stencil: class-token rows, the dropout backward of
+// NystromAttention.to_out, the _fc1 GELU backward with the grid-padding fold
+// (:177-180), and the class-token gradient.  All HBM-bound, one pass each.
+#include "common.h"
+#include "../../include/transmil_hip.h"
+
+namespace {
+
+// H[b*S + 0][:] = cls[:]; grid (B), block 256
+__global__ void put_cls_kernel(const float* __restrict__ cls, int S, int D, float* __restrict__ H) {
+  for (int c = threadIdx.x; c < D; c += blockDim.x) H[(size_t)blockIdx.x * S * D + c] = cls[c];
+}
+
+// out[b][pad + i][c] = dH[b*S + i][c] * keep(b*S+i, c) * scale ; out[b][0..pad)[c] = 0
+// grid (n_pad, B), block 256
+template <typename T>
+__global__ void dropout_bwd_pad_kernel(const float* __restrict__ dH, int S, int n_pad, int pad, int D, float p,
+                                       float scale, uint64_t seed, T* __restrict__ out) {
+  const int t = blockIdx.x, b = blockIdx.y;
+  T* dst = out + ((size_t)b * n_pad + t) * D;
+  const int i = t - pad;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float v = 0.f;
+    if (i >= 0) {
+      const int row = b * S + i;
+      v = dH[(size_t)row * D + c];
+      if (p > 0.f) v = dropout_u01(seed, (uint32_t)row, (uint32_t)c) >= p ? v * scale : 0.f;
+    }
+    dst[c] = from_f<T>(v);
+  }
+}
+
+// dpre[b*N + i][c] = (dH[b*S + 1 + i][c] + (i < add ? dH[b*S + 1 + N + i][c] : 0)) * gelu'(pre[b*N+i][c])
+// grid (N, B), block 256
+template <typename T>
+__global__ void fc1_gelu_bwd_kernel(const float* __restrict__ dH, const float* __restrict__ pre, int N, int S, int add,
+                                    int D, T* __restrict__ dpre) {
+  const int i = blockIdx.x, b = blockIdx.y;
+  const float* g0 = dH + ((size_t)b * S + 1 + i) * D;
+  const float* g1 = dH + ((size_t)b * S + 1 + N + i) * D;
+  const size_t o = ((size_t)b * N + i) * D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float g = g0[c];
+    if (i < add) g += g1[c];
+    dpre[o + c] = from_f<T>(g * gelu_erf_grad(pre[o + c]));
+  }
+}
+
+// y[b][pad + i][c] = x[b*S + i][c] (cast to T), y[b][0..pad)[c] = 0; grid (n_pad, B)
+template <typename T>
+__global__ void pad_rows_kernel(const float* __restrict__ x, int S, int n_pad, int pad, int D, T* __restrict__ y) {
+  const int t = blockIdx.x, b = blockIdx.y, i = t - pad;
+  T* dst = y + ((size_t)b * n_pad + t) * D;
+  for (int c = threadIdx.x; c < D; c += blockDim.x)
+    dst[c] = from_f<T>(i >= 0 ? x[((size_t)b * S + i) * D + c] : 0.f);
+}
+
+// dcls[c] = sum_b dH[b*S][c]
+__global__ void cls_grad_kernel(const float* __restrict__ dH, int B, int S, int D, float* __restrict__ dcls) {
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dH[(size_t)b * S * D + c];
+    dcls[c] = s;
+  }
+}
+
+}  // namespace
+
+#define TM_DTYPE_DISPATCH(dt, CALL)                               \
+  if ((dt) == TM_BF16) { using T = bf16; CALL; }                  \
+  else if ((dt) == TM_F32) { using T = float; CALL; }             \
+  else { tm_set_error("glue: dtype must be TM_F32 or TM_BF16"); return 1; }
+
+extern "C" int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream) {
+  put_cls_kernel<<<B, 256, 0, (hipStream_t)stream>>>(cls, S, D, H);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int pad, int D, float p,
+                                  uint64_t seed, void* out, void* stream) {
+  TM_REQUIRE(n_pad >= S + pad, "dropout_bwd_pad: n_pad < S + pad");
+  const float scale = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
+  TM_DTYPE_DISPATCH(dtype, (dropout_bwd_pad_kernel<T><<<dim3(n_pad, B), 256, 0, (hipStream_t)stream>>>(
+                               dH, S, n_pad, pad, D, p, scale, seed, (T*)out)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, int pad, int D, void* y,
+                           void* stream) {
+  TM_REQUIRE(n_pad >= S + pad, "pad_rows: n_pad < S + pad");
+  TM_DTYPE_DISPATCH(dtype, (pad_rows_kernel<T><<<dim3(n_pad, B), 256, 0, (hipStream_t)stream>>>(
+                               x, S, n_pad, pad, D, (T*)y)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
+                               void* dpre, float* dcls, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  TM_DTYPE_DISPATCH(dtype, (fc1_gelu_bwd_kernel<T><<<dim3(N, B), 256, 0, st>>>(dH, pre, N, S, add, D,
+                                                                               (T*)dpre)));
+  TM_CHECK_LAUNCH();
+  cls_grad_kernel<<<1, 256, 0, st>>>(dH, B, S, D, dcls);
+  TM_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,837 @@
+// NystromAttention core (SURVEY.md section 8 App. A eq. 4-9), forward and backward.
+//
+// Replaces the arithmetic of the third-party `nystrom_attention.NystromAttention`
+// called at code/models/TransMIL.py:26-34,47 (not vendored).
+// Fixed geometry: dim_head = 64, num_landmarks = 256 (TransLayer always builds
+// dim_head = dim/8, num_landmarks = dim/2 with dim = 512, code/models/TransMIL.py:26-31).
+//
+// Layouts in HBM (bh = bag*heads + head, n = n' = padded length, l = n/256):
+//   q, k, v        [3][B*h][n][64]  T   (q pre-scaled by dim_head^-0.5)
+//   ql, kl         [B*h][256][64]   fp32 (+ T copies for the MFMA paths)
+//   merged out     [B][n][h*64]     T   (input of to_out)
+//
+// Forward (reassociated):  out = softmax(q kl^T) . (Z . (softmax(ql k^T) . v)) + conv33(v)
+// i.e. attn1 @ (Z @ (attn3 @ v)) instead of (attn1 @ Z) @ (attn3 @ v): saves
+// n*256*256*2 flop per head (8.86 GF/layer at N=8192); results agree to fp32
+// rounding (tests/test_parity_gpu.py).
+//
+// Kernels
+//   landmarks        segment means of q, k (eq. 4)                 HBM-bound
+//   sim2_softmax     A2 = softmax(ql kl^T) (eq. 5-6), fp32          tiny
+//   a3_fwd/combine   W = softmax(ql k^T) v, split over key blocks   flash-decode style
+//   a1_fwd           softmax(q kl^T) Y + conv(v) -> merged rows     one pass, 256 keys
+//   conv_bwd         conv33 backward + D1 = rowsum(dO * O_att)
+//   attn_bwd<MODE>   shared flash-style backward for the A1 and A3 products
+//   assemble_dqkv    dq, dk, dv + landmark terms -> [B][n][3*h*64]
+#include "common.h"
+#include "../../include/transmil_hip.h"
+
+namespace {
+
+constexpr int DH = 64;     // dim_head
+constexpr int NL = 256;    // landmarks
+constexpr int TAPS = 33;   // residual conv kernel
+constexpr int HALF = 16;   // conv padding
+
+// LDS row strides (elements).  Keys [256][KROW]: 144 B (bf16) / 272 B (f32) rows
+// -> conflict-free ds_read_b128 for 16 consecutive rows.  Values^T [64][VROW]:
+// 520 B (bf16, ds_read_b64 2 dwords/lane over all 64 banks) / 1040 B (f32).
+template <typename T> struct Lay {
+  static constexpr int KROW = DH + 16 / (int)sizeof(T);  // 72 bf16 / 68 f32
+  static constexpr int VROW = NL + 4;                                              // 260
+};
+
+TM_DEV long long hoff(long long bh, int nh, long long bag_stride, long long head_stride) {
+  return (bh / nh) * bag_stride + (bh % nh) * head_stride;
+}
+
+// ---------------------------------------------------------------------------
+// landmarks: out[bh][j][d] = sum_{t<l} x[bh][j*l+t][d] / l ; grid (nbh, 64), block 256 (4 landmarks x 64 d)
+template <typename T>
+__global__ void landmarks_kernel(const T* __restrict__ q, const T* __restrict__ k, int n, int l,
+                                 float* __restrict__ ql, float* __restrict__ kl, T* __restrict__ ql_t,
+                                 T* __restrict__ kl_t) {
+  const int bh = blockIdx.x, j = blockIdx.y * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
+  const T* qp = q + ((size_t)bh * n + (size_t)j * l) * DH + d;
+  const T* kp = k + ((size_t)bh * n + (size_t)j * l) * DH + d;
+  float sq = 0.f, sk = 0.f;
+  for (int t = 0; t < l; ++t) { sq += to_f(qp[(size_t)t * DH]); sk += to_f(kp[(size_t)t * DH]); }
+  const float inv_l = (float)l;
+  const size_t o = ((size_t)bh * NL + j) * DH + d;
+  const float vq = sq / inv_l, vk = sk / inv_l;
+  ql[o] = vq; kl[o] = vk;
+  ql_t[o] = from_f<T>(vq); kl_t[o] = from_f<T>(vk);
+}
+
+// ---------------------------------------------------------------------------
+// A2 = softmax_j(ql_i . kl_j), fp32 FMA.  grid (nbh, 16), block 256: 16 rows per block, thread = column j.
+__global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restrict__ ql, const float* __restrict__ kl,
+                                                           float* __restrict__ a2) {
+  const int bh = blockIdx.x, i0 = blockIdx.y * 16, j = threadIdx.x, lane = j & 63, wave = j >> 6;
+  __shared__ float kt[DH][NL + 1];
+  __shared__ float qs[16][DH];
+  __shared__ float red[4][16];
+  const float* kb = kl + (size_t)bh * NL * DH;
+  for (int e = threadIdx.x; e < NL * DH; e += 256) kt[e % DH][e / DH] = kb[e];
+  for (int e = threadIdx.x; e < 16 * DH; e += 256) qs[e / DH][e % DH] = ql[((size_t)bh * NL + i0) * DH + e];
+  __syncthreads();
+  float s[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s[r] = 0.f;
+  for (int d = 0; d < DH; ++d) {
+    const float kv = kt[d][j];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = fmaf(qs[r][d], kv, s[r]);
+  }
+  // row max
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float m = wave_max(s[r]);
+    if (lane == 0) red[wave][r] = m;
+  }
+  __syncthreads();
+  float mx[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) mx[r] = fmaxf(fmaxf(red[0][r], red[1][r]), fmaxf(red[2][r], red[3][r]));
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    s[r] = __expf(s[r] - mx[r]);
+    const float t = wave_sum(s[r]);
+    if (lane == 0) red[wave][r] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float tot = (red[0][r] + red[1][r]) + (red[2][r] + red[3][r]);
+    a2[((size_t)bh * NL + i0 + r) * NL + j] = s[r] / tot;
+  }
+}
+
+// dS2 = A2 * (dA2 - rowsum(dA2 * A2)); grid (nbh*256/4), block 256 (one wave per row)
+__global__ void softmax_bwd_rows_kernel(const float* __restrict__ a, const float* __restrict__ da,
+                                        float* __restrict__ ds, int rows) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const f32x4 av = *(const f32x4*)(a + (size_t)r * NL + lane * 4);
+  const f32x4 dv = *(const f32x4*)(da + (size_t)r * NL + lane * 4);
+  const float s = wave_sum(av[0] * dv[0] + av[1] * dv[1] + av[2] * dv[2] + av[3] * dv[3]);
+  f32x4 o;
+  o[0] = av[0] * (dv[0] - s); o[1] = av[1] * (dv[1] - s); o[2] = av[2] * (dv[2] - s); o[3] = av[3] * (dv[3] - s);
+  *(f32x4*)(ds + (size_t)r * NL + lane * 4) = o;
+}
+
+// ---------------------------------------------------------------------------
+// Shared forward block: one wave, 32 queries (B-operand fragments qf), 256 keys in
+// LDS (ks[key][KROW]), values^T in LDS (vt[d][VROW]).  Returns unnormalised O^T
+// (2 tiles: d 0-31, 32-63; col = query) plus per-query max and sum.
+template <typename T>
+TM_DEV void attn_fwd_wave(const T* ks, const T* vt, const vec8<T> (&qf)[4], f32x16 (&o)[2], float& mx, float& sum,
+                          int lane) {
+  constexpr int KROW = Lay<T>::KROW, VROW = Lay<T>::VROW;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 s[8];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    s[kt] = (f32x16){};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const vec8<T> a = load8(ks + (kt * 32 + r) * KROW + st * 16 + 8 * h);
+      mma16(s[kt], a, qf[st]);
+    }
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, s[kt][i]);
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = __expf(s[kt][i] - m);
+      s[kt][i] = p;
+      l += p;
+    }
+  l += __shfl_xor(l, 32, 64);
+  mx = m;
+  sum = l;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    o[dt] = (f32x16){};
+#pragma unroll
+    for (int kt = 0; kt < 8; ++kt)
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        const T* row = vt + (dt * 32 + r) * VROW + kt * 32 + 16 * sp + 4 * h;
+        const vec4<T> lo = load4(row), hi = load4(row + 8);
+        vec8<T> a;
+        a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
+        a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
+        mma16(o[dt], a, acc_as_operand<T>(s[kt], sp));
+      }
+  }
+}
+
+// stage fp32 [256][64] (keys) into LDS ks[key][KROW] as T
+template <typename T>
+TM_DEV void stage_keys_f32(T* ks, const float* src, int tid) {
+  constexpr int KROW = Lay<T>::KROW;
+  for (int i = tid; i < NL * DH / 4; i += 256) {
+    const int row = i >> 4, c = (i & 15) * 4;
+    const f32x4 v = *(const f32x4*)(src + (size_t)row * DH + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ks[row * KROW + c + e] = from_f<T>(v[e]);
+  }
+}
+// stage T rows [256][64] (row stride 64) into ks[key][KROW]
+template <typename T>
+TM_DEV void stage_keys_t(T* ks, const T* src, int tid) {
+  constexpr int KROW = Lay<T>::KROW, E = 16 / sizeof(T);
+  for (int i = tid; i < NL * DH / E; i += 256) {
+    const int row = i / (DH / E), c = (i % (DH / E)) * E;
+    *(f32x4*)(ks + row * KROW + c) = *(const f32x4*)(src + (size_t)row * DH + c);
+  }
+}
+// stage values [256][64] (fp32 or T) transposed into vt[d][VROW] as T
+template <typename T, typename S>
+TM_DEV void stage_values_t(T* vt, const S* src, int tid) {
+  constexpr int VROW = Lay<T>::VROW;
+  for (int i = tid; i < NL * DH; i += 256) {
+    const int key = i >> 6, d = i & 63;
+    vt[d * VROW + key] = from_f<T>(to_f(src[(size_t)key * DH + d]));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A1 path forward.  grid (n/128, nbh), block 256 (4 waves x 32 queries).
+//   merged[bag][t][head*64+d] = softmax_j(q_t . kl_j) . Y_j  + sum_tau w[head][tau] v[t+tau-16][d]
+//   lse1[bh][t] saved for backward.
+template <typename T>
+__global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, const T* __restrict__ v,
+                                                     const float* __restrict__ kl, const float* __restrict__ y,
+                                                     const float* __restrict__ wconv, int n, int nh,
+                                                     T* __restrict__ merged, float* __restrict__ lse1) {
+  constexpr int KROW = Lay<T>::KROW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* ks = (T*)smem;                                  // [256][KROW]
+  T* vt = ks + NL * KROW;                            // [64][VROW]
+  float* ost = (float*)smem;                         // reuse: [128][68] fp32 after the MFMA phase
+  const int bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int head = bh % nh, bag = bh / nh;
+  const int t0 = blockIdx.x * 128;
+  stage_keys_f32<T>(ks, kl + (size_t)bh * NL * DH, tid);
+  stage_values_t<T, float>(vt, y + (size_t)bh * NL * DH, tid);
+  const T* qb = q + (size_t)bh * n * DH;
+  vec8<T> qf[4];
+  const int qrow = t0 + wave * 32 + r;
+#pragma unroll
+  for (int st = 0; st < 4; ++st) qf[st] = load8(qb + (size_t)qrow * DH + st * 16 + 8 * h);
+  __syncthreads();
+  f32x16 o[2];
+  float mx, sum;
+  attn_fwd_wave<T>(ks, vt, qf, o, mx, sum, lane);
+  if (h == 0) lse1[(size_t)bh * n + qrow] = mx + __logf(sum);
+  const float inv = 1.0f / sum;
+  __syncthreads();  // everyone done reading ks/vt
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = dt * 32 + 8 * g4 + 4 * h;
+      f32x4 val;
+      val[0] = o[dt][4 * g4] * inv; val[1] = o[dt][4 * g4 + 1] * inv;
+      val[2] = o[dt][4 * g4 + 2] * inv; val[3] = o[dt][4 * g4 + 3] * inv;
+      *(f32x4*)(ost + (wave * 32 + r) * 68 + d0) = val;
+    }
+  __syncthreads();
+  // conv residual + coalesced store: item = (query, 8 d)
+  float w[TAPS];
+#pragma unroll
+  for (int tau = 0; tau < TAPS; ++tau) w[tau] = wconv[head * TAPS + tau];
+  const T* vb = v + (size_t)bh * n * DH;
+  for (int it = tid; it < 128 * 8; it += 256) {
+    const int ql = it >> 3, dc = (it & 7) * 8, t = t0 + ql;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = ost[ql * 68 + dc + e];
+#pragma unroll
+    for (int tau = 0; tau < TAPS; ++tau) {
+      const int src = t + tau - HALF;
+      if (src >= 0 && src < n) {
+        const vec8<T> vv = load8(vb + (size_t)src * DH + dc);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(w[tau], to_f(vv[e]), acc[e]);
+      }
+    }
+    vec8<T> outv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) outv[e] = from_f<T>(acc[e]);
+    store8(merged + ((size_t)bag * n + t) * (nh * DH) + head * DH + dc, outv);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// A3 path forward, one 256-key block x 128 landmark queries per workgroup.
+// grid (n/256, nbh, 2), block 256.
+//   part_o[kb][bh][q][d] = sum_{keys in kb} exp(s - m_kb) v ; part_ml[kb][bh][q] = (m, l)
+template <typename T>
+__global__ __launch_bounds__(256) void a3_fwd_kernel(const float* __restrict__ ql, const T* __restrict__ k,
+                                                     const T* __restrict__ v, int n, float* __restrict__ part_o,
+                                                     float* __restrict__ part_m, float* __restrict__ part_l) {
+  constexpr int KROW = Lay<T>::KROW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* ks = (T*)smem;
+  T* vt = ks + NL * KROW;
+  const int kb = blockIdx.x, bh = blockIdx.y, nbh = gridDim.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const size_t kv_off = ((size_t)bh * n + (size_t)kb * NL) * DH;
+  stage_keys_t<T>(ks, k + kv_off, tid);
+  stage_values_t<T, T>(vt, v + kv_off, tid);
+  __syncthreads();
+  {
+    const int qi = blockIdx.z * 128 + wave * 32 + r;  // query half per workgroup
+    vec8<T> qf[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) qf[st] = cvt8<T>(ql + ((size_t)bh * NL + qi) * DH + st * 16 + 8 * h);
+    f32x16 o[2];
+    float mx, sum;
+    attn_fwd_wave<T>(ks, vt, qf, o, mx, sum, lane);
+    const size_t pidx = ((size_t)kb * nbh + bh) * NL + qi;
+    if (h == 0) { part_m[pidx] = mx; part_l[pidx] = sum; }
+    float* po = part_o + pidx * DH;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        f32x4 val;
+        val[0] = o[dt][4 * g4]; val[1] = o[dt][4 * g4 + 1]; val[2] = o[dt][4 * g4 + 2]; val[3] = o[dt][4 * g4 + 3];
+        *(f32x4*)(po + dt * 32 + 8 * g4 + 4 * h) = val;
+      }
+  }
+}
+
+// combine the key-block partials: W[bh][q][d], lse3[bh][q]; grid (nbh, 64), block 256 (4 queries x 64 d)
+__global__ void a3_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_m,
+                                  const float* __restrict__ part_l, int nkb, int nbh, float* __restrict__ w,
+                                  float* __restrict__ lse3) {
+  const int bh = blockIdx.x, qi = blockIdx.y * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
+  float M = -INFINITY;
+  for (int kb = 0; kb < nkb; ++kb) M = fmaxf(M, part_m[((size_t)kb * nbh + bh) * NL + qi]);
+  float L = 0.f, acc = 0.f;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const size_t pidx = ((size_t)kb * nbh + bh) * NL + qi;
+    const float sc = __expf(part_m[pidx] - M);
+    L += part_l[pidx] * sc;
+    acc += part_o[pidx * DH + d] * sc;
+  }
+  w[((size_t)bh * NL + qi) * DH + d] = acc / L;
+  if (d == 0) lse3[(size_t)bh * NL + qi] = M + __logf(L);
+}
+
+// ---------------------------------------------------------------------------
+// D3[bh][q] = dW[q] . W[q]; dW_t = T(dW).  grid (nbh*256/4), block 256 (one wave per row)
+template <typename T>
+__global__ void rowdot_cast_kernel(const float* __restrict__ dw, const float* __restrict__ w, float* __restrict__ dd,
+                                   T* __restrict__ dw_t, int rows) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float a = dw[(size_t)r * DH + lane];
+  const float s = wave_sum(a * w[(size_t)r * DH + lane]);
+  dw_t[(size_t)r * DH + lane] = from_f<T>(a);
+  if (lane == 0) dd[r] = s;
+}
+
+// T copy of an fp32 [rows][64] matrix
+template <typename T>
+__global__ void cast_rows_kernel(const float* __restrict__ x, T* __restrict__ y, long long count) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < count) y[i] = from_f<T>(x[i]);
+}
+
+// ---------------------------------------------------------------------------
+// conv33 backward + D1.  grid (n/64, nbh), block 256.
+//   dv[bh][t][d]  = sum_tau w[tau] dO[t - tau + 16][d]          (written, fp32)
+//   c_tau(t)      = sum_d dO[t][d] v[t + tau - 16][d]
+//   D1[bh][t]     = dO[t].O[t] - sum_tau w[tau] c_tau(t)          (= dO . (attn1 Y) )
+//   dw_part[bag*ntb + tb][head*33 + tau] = sum_{t in block} c_tau(t)
+template <typename T>
+__global__ __launch_bounds__(256) void conv_bwd_kernel(const T* __restrict__ dmerged, const T* __restrict__ merged,
+                                                       const T* __restrict__ v, const float* __restrict__ wconv,
+                                                       int n, int nh, float* __restrict__ dv, float* __restrict__ d1,
+                                                       float* __restrict__ dw_part) {
+  constexpr int R = 64, HR = R + 2 * HALF;  // 96 staged rows
+  __shared__ float dos[HR][DH + 1];
+  __shared__ float vs[HR][DH + 1];
+  __shared__ float cred[R][TAPS + 1];
+  __shared__ float ws[TAPS];
+  const int bh = blockIdx.y, tb = blockIdx.x, tid = threadIdx.x;
+  const int head = bh % nh, bag = bh / nh, ntb = gridDim.x;
+  const int t0 = tb * R;
+  const int ld = nh * DH;
+  const T* dob = dmerged + (size_t)bag * n * ld + head * DH;
+  const T* ob = merged + (size_t)bag * n * ld + head * DH;
+  const T* vb = v + (size_t)bh * n * DH;
+  for (int i = tid; i < HR * DH; i += 256) {
+    const int rr = i >> 6, d = i & 63, t = t0 - HALF + rr;
+    const bool ok = t >= 0 && t < n;
+    dos[rr][d] = ok ? to_f(dob[(size_t)t * ld + d]) : 0.f;
+    vs[rr][d] = ok ? to_f(vb[(size_t)t * DH + d]) : 0.f;
+  }
+  if (tid < TAPS) ws[tid] = wconv[head * TAPS + tid];
+  __syncthreads();
+  // part A: thread (row rl, quarter qq)
+  {
+    const int rl = tid >> 2, qq = tid & 3;
+    float wc = 0.f;
+    for (int tau = qq; tau < TAPS; tau += 4) {
+      float c = 0.f;
+#pragma unroll 8
+      for (int d = 0; d < DH; ++d) c = fmaf(dos[rl + HALF][d], vs[rl + tau][d], c);
+      cred[rl][tau] = c;
+      wc = fmaf(ws[tau], c, wc);
+    }
+    float dd = 0.f;
+    const int t = t0 + rl;
+    if (t < n) {
+#pragma unroll
+      for (int d = qq * 16; d < qq * 16 + 16; ++d) dd = fmaf(dos[rl + HALF][d], to_f(ob[(size_t)t * ld + d]), dd);
+    }
+    float tot = dd - wc;
+    tot += __shfl_xor(tot, 1, 64);
+    tot += __shfl_xor(tot, 2, 64);
+    if (qq == 0 && t < n) d1[(size_t)bh * n + t] = tot;
+  }
+  __syncthreads();
+  if (tid < TAPS) {
+    float s = 0.f;
+    for (int rl = 0; rl < R; ++rl) s += cred[rl][tid];
+    dw_part[((size_t)bag * ntb + tb) * (nh * TAPS) + head * TAPS + tid] = s;
+  }
+  // part B: dv, thread (row rl, 16 d)
+  {
+    const int rl = tid >> 2, d0 = (tid & 3) * 16, t = t0 + rl;
+    if (t < n) {
+      float acc[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int tau = 0; tau < TAPS; ++tau) {
+        const float* src = dos[rl + 2 * HALF - tau] + d0;
+        const float wt = ws[tau];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = fmaf(wt, src[e], acc[e]);
+      }
+      float* dst = dv + ((size_t)bh * n + t) * DH + d0;
+#pragma unroll
+      for (int e = 0; e < 16; e += 4) *(f32x4*)(dst + e) = (f32x4){acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Flash-style backward shared by both attention products.  A workgroup owns a
+// block of 256 keys (4 waves x 64, key on the MFMA lane) and walks query chunks
+// of 32.  With P = exp(Q K^T - lse), dS = P (dO V^T - D):
+//   dV^T += dO^T P,  dK^T += Q^T dS   (registers, sum over the walked queries)
+//   dQ    = dS K                      (per chunk, dS through LDS)
+// MODE_A3: keys = k rows (block kb), queries = all 256 landmarks;
+//          dK -> dk (=), dV -> dv (+=), dQ -> partial slab [kb] (dql).
+// MODE_A1: keys = the 256 landmarks, queries = rows [qc*QC, (qc+1)*QC);
+//          dQ -> dq (=), dK -> partial slab [qc] (dkl), dV -> partial slab [qc] (dY).
+struct BwdArgs {
+  const void* q; long long q_bag, q_head; int q_row;    // queries (T)
+  const void* dO; long long o_bag, o_head; int o_row;   // upstream grad (T)
+  const void* k; long long k_bag, k_head;               // keys (T), row stride 64
+  const void* v; long long v_bag, v_head;               // values (T), row stride 64
+  const float* lse;  long long lse_bh;                  // [bh][...]
+  const float* dd;   long long dd_bh;                   // D per query
+  float* dq; long long dq_bh;                           // query-side grad (fp32, row stride 64)
+  float* dk; long long dk_bh;                           // key-side grads (fp32, row stride 64)
+  float* dv; long long dv_bh;
+  long long slab_stride;                                // per block partial slab stride (MODE dependent)
+  int nh, n_queries_per_wg, n_key_rows;
+};
+
+enum { MODE_A3 = 0, MODE_A1 = 1 };
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
+  constexpr int QT_ROW = 32 + 4;              // [64 d][36]  (T)
+  constexpr int KT_ROW = NL + 16 / sizeof(T); // [64 d][264 bf16 / 260 f32]
+  constexpr int DS_ROW = NL + 16 / sizeof(T); // [32 q][...]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* kt_s = (T*)smem;                                   // K^T  [64][KT_ROW]
+  T* ds_s = kt_s + DH * KT_ROW;                         // dS   [32][DS_ROW]
+  T* qt_s = ds_s + 32 * DS_ROW;                         // Q^T  [64][QT_ROW]
+  T* dot_s = qt_s + DH * QT_ROW;                        // dO^T [64][QT_ROW]
+  float* xch = (float*)(dot_s + DH * QT_ROW);           // [2][32*32] dQ partial exchange
+  float* lse_s = xch + 2 * 1024;                        // [32]
+  float* dd_s = lse_s + 32;                             // [32]
+  float* stage = (float*)smem;                          // epilogue reuse [256][68]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int blk = blockIdx.x, bh = blockIdx.y, nh = a.nh;
+  const int key0 = (MODE == MODE_A3) ? blk * NL : 0;      // first key row of this WG
+  const int q_begin = (MODE == MODE_A1) ? blk * a.n_queries_per_wg : 0;
+  const int q_count = a.n_queries_per_wg;
+
+  const T* Q = (const T*)a.q + hoff(bh, nh, a.q_bag, a.q_head);
+  const T* dO = (const T*)a.dO + hoff(bh, nh, a.o_bag, a.o_head);
+  const T* K = (const T*)a.k + hoff(bh, nh, a.k_bag, a.k_head) + (size_t)key0 * DH;
+  const T* V = (const T*)a.v + hoff(bh, nh, a.v_bag, a.v_head) + (size_t)key0 * DH;
+  const float* lse = a.lse + bh * a.lse_bh;
+  const float* dd = a.dd + bh * a.dd_bh;
+
+  // K^T into LDS (all 256 keys)
+  for (int i = tid; i < NL * DH; i += 256) {
+    const int key = i >> 6, d = i & 63;
+    kt_s[d * KT_ROW + key] = K[(size_t)key * DH + d];
+  }
+
+  f32x16 dvt[2][2], dkt[2][2];  // [d tile][key tile]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { dvt[i][j] = (f32x16){}; dkt[i][j] = (f32x16){}; }
+
+  const int mykey = wave * 64;  // this wave's 64 keys (local)
+#pragma unroll 1
+  for (int c0 = 0; c0 < q_count; c0 += 32) {
+    const int qa = q_begin + c0;  // absolute first query of the chunk
+    __syncthreads();              // previous chunk fully consumed
+    for (int i = tid; i < 32 * DH; i += 256) {
+      const int qq = i >> 6, d = i & 63;
+      qt_s[d * QT_ROW + qq] = Q[(size_t)(qa + qq) * a.q_row + d];
+      dot_s[d * QT_ROW + qq] = dO[(size_t)(qa + qq) * a.o_row + d];
+    }
+    if (tid < 32) { lse_s[tid] = lse[qa + tid]; dd_s[tid] = dd[qa + tid]; }
+    __syncthreads();
+    // S = Q K^T and dP = dO V^T for 32 queries x this wave's 64 keys
+    f32x16 s[2], dp[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) { s[kt] = (f32x16){}; dp[kt] = (f32x16){}; }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const vec8<T> qa_f = load8(Q + (size_t)(qa + r) * a.q_row + st * 16 + 8 * h);
+      const vec8<T> oa_f = load8(dO + (size_t)(qa + r) * a.o_row + st * 16 + 8 * h);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int key = mykey + kt * 32 + r;
+        const vec8<T> kb_f = load8(K + (size_t)key * DH + st * 16 + 8 * h);
+        const vec8<T> vb_f = load8(V + (size_t)key * DH + st * 16 + 8 * h);
+        mma16(s[kt], qa_f, kb_f);
+        mma16(dp[kt], oa_f, vb_f);
+      }
+    }
+    // P and dS (rows = queries on registers)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int qq = acc_row(i, h);
+        const float p = __expf(s[kt][i] - lse_s[qq]);
+        s[kt][i] = p;
+        dp[kt][i] = p * (dp[kt][i] - dd_s[qq]);
+      }
+    // dV^T += dO^T P ; dK^T += Q^T dS
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      vec8<T> ao[2], aq[2];
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const T* ro = dot_s + (dt * 32 + r) * QT_ROW + 16 * sp + 4 * h;
+        const T* rq = qt_s + (dt * 32 + r) * QT_ROW + 16 * sp + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          ao[dt][e] = ro[e]; ao[dt][4 + e] = ro[8 + e];
+          aq[dt][e] = rq[e]; aq[dt][4 + e] = rq[8 + e];
+        }
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const vec8<T> bp = acc_as_operand<T>(s[kt], sp);
+        const vec8<T> bs = acc_as_operand<T>(dp[kt], sp);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          mma16(dvt[dt][kt], ao[dt], bp);
+          mma16(dkt[dt][kt], aq[dt], bs);
+        }
+      }
+    }
+    // dS -> LDS [q][key]
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + kt * 32 + r] = from_f<T>(dp[kt][i]);
+    __syncthreads();
+    // dQ chunk [32 q x 64 d] = dS [32 x 256] . K [256 x 64]; wave w: d tile (w&1), key half (w>>1)
+    {
+      const int dt = wave & 1, kh = wave >> 1;
+      f32x16 acc = (f32x16){};
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        const int kk = kh * 128 + st * 16 + 8 * h;
+        const vec8<T> af = load8(ds_s + r * DS_ROW + kk);
+        const vec8<T> bf = load8(kt_s + (dt * 32 + r) * KT_ROW + kk);
+        mma16(acc, af, bf);
+      }
+      if (kh == 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xch[dt * 1024 + i * 64 + lane] = acc[i];
+      }
+      __syncthreads();
+      if (kh == 0) {
+        float* dst;
+        if (MODE == MODE_A1) dst = a.dq + bh * a.dq_bh;                            // rows = absolute query
+        else dst = a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;              // partial slab [kb]
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qq = qa + acc_row(i, h);
+          dst[(size_t)qq * DH + dt * 32 + r] = acc[i] + xch[dt * 1024 + i * 64 + lane];
+        }
+      }
+    }
+  }
+  // ---- key-side epilogue through LDS (transpose to [key][d]) ----
+  __syncthreads();
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const f32x16& accv = which == 0 ? dvt[dt][kt] : dkt[dt][kt];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) stage[(mykey + kt * 32 + r) * 68 + dt * 32 + acc_row(i, h)] = accv[i];
+      }
+    __syncthreads();
+    float* dst;
+    bool add = false;
+    if (MODE == MODE_A3) {
+      dst = (which == 0 ? a.dv + bh * a.dv_bh : a.dk + bh * a.dk_bh) + (size_t)key0 * DH;
+      add = (which == 0);
+    } else {
+      dst = (which == 0 ? a.dv : a.dk) + (size_t)blk * a.slab_stride + bh * (which == 0 ? a.dv_bh : a.dk_bh);
+    }
+    for (int i = tid; i < NL * DH / 4; i += 256) {
+      const int key = i >> 4, d4 = (i & 15) * 4;
+      f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
+      float* p = dst + (size_t)key * DH + d4;
+      if (add) val += *(const f32x4*)p;
+      *(f32x4*)p = val;
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+constexpr size_t bwd_smem_bytes() {
+  constexpr size_t QT_ROW = 32 + 4, KT_ROW = NL + 16 / sizeof(T), DS_ROW = KT_ROW;
+  constexpr size_t main = (DH * KT_ROW + 32 * DS_ROW + 2 * DH * QT_ROW) * sizeof(T) + (2 * 1024 + 64) * 4;
+  constexpr size_t epi = (size_t)NL * 68 * 4;
+  return main > epi ? main : epi;
+}
+
+// ---------------------------------------------------------------------------
+// dqkv[bag][t][which*h*64 + head*64 + d]:
+//   q: scale * (dq[t] + dql[t/l] / l);  k: dk[t] + dkl[t/l] / l;  v: dv[t]
+template <typename T>
+__global__ void assemble_dqkv_kernel(const float* __restrict__ dq, const float* __restrict__ dql,
+                                     const float* __restrict__ dk, const float* __restrict__ dkl,
+                                     const float* __restrict__ dv, int n, int l, int nh, float scale,
+                                     T* __restrict__ dqkv) {
+  // grid (n, nbh/?): one block per (bag, t) row, threads over 3*nh*64 columns
+  const int t = blockIdx.x, bag = blockIdx.y;
+  const int inner = nh * DH;
+  const float inv_l = 1.0f / (float)l;
+  for (int c = threadIdx.x; c < 3 * inner; c += blockDim.x) {
+    const int which = c / inner, head = (c % inner) / DH, d = c % DH;
+    const size_t bh = (size_t)bag * nh + head;
+    const size_t row = (bh * n + t) * DH + d;
+    const size_t lrow = (bh * NL + t / l) * DH + d;
+    float val;
+    if (which == 0) val = scale * (dq[row] + dql[lrow] * inv_l);
+    else if (which == 1) val = dk[row] + dkl[lrow] * inv_l;
+    else val = dv[row];
+    dqkv[((size_t)bag * n + t) * (3 * inner) + c] = from_f<T>(val);
+  }
+}
+
+}  // namespace
+
+// ============================ C entry points ===============================
+
+#define TM_DTYPE_DISPATCH(dt, CALL)                               \
+  if ((dt) == TM_BF16) { using T = bf16; CALL; }                  \
+  else if ((dt) == TM_F32) { using T = float; CALL; }             \
+  else { tm_set_error("nystrom: dtype must be TM_F32 or TM_BF16"); return 1; }
+
+extern "C" int tm_nys_landmarks(int dtype, const void* q, const void* k, int nbh, int n, float* ql, float* kl,
+                                void* ql_t, void* kl_t, void* stream) {
+  TM_REQUIRE(n > 0 && n % NL == 0, "landmarks: n must be a positive multiple of 256");
+  const int l = n / NL;
+  TM_DTYPE_DISPATCH(dtype, (landmarks_kernel<T><<<dim3(nbh, NL / 4), 256, 0, (hipStream_t)stream>>>(
+                               (const T*)q, (const T*)k, n, l, ql, kl, (T*)ql_t, (T*)kl_t)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_nys_sim2_softmax(const float* ql, const float* kl, int nbh, float* a2, void* stream) {
+  sim2_softmax_kernel<<<dim3(nbh, NL / 16), 256, 0, (hipStream_t)stream>>>(ql, kl, a2);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_softmax_bwd_rows256(const float* a, const float* da, float* ds, int rows, void* stream) {
+  softmax_bwd_rows_kernel<<<(rows + 3) / 4, 256, 0, (hipStream_t)stream>>>(a, da, ds, rows);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long long tm_nys_a3_workspace(int nbh, int n) {
+  const long long nkb = n / NL;
+  return nkb * nbh * NL * (DH + 2) * (long long)sizeof(float);
+}
+
+extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
+                             float* w, float* lse3, void* stream) {
+  TM_REQUIRE(n > 0 && n % NL == 0, "a3_fwd: n must be a positive multiple of 256");
+  const int nkb = n / NL;
+  float* po = work;
+  float* pm = po + (size_t)nkb * nbh * NL * DH;
+  float* pl = pm + (size_t)nkb * nbh * NL;
+  hipStream_t st = (hipStream_t)stream;
+  TM_DTYPE_DISPATCH(dtype, ({
+    const size_t sm = (size_t)NL * Lay<T>::KROW * sizeof(T) + (size_t)DH * Lay<T>::VROW * sizeof(T);
+    tm_allow_smem(a3_fwd_kernel<T>, sm);
+    a3_fwd_kernel<T><<<dim3(nkb, nbh, 2), 256, sm, st>>>(ql, (const T*)k, (const T*)v, n, po, pm, pl);
+  }));
+  TM_CHECK_LAUNCH();
+  a3_combine_kernel<<<dim3(nbh, NL / 4), 256, 0, st>>>(po, pm, pl, nkb, nbh, w, lse3);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const float* kl, const float* y,
+                             const float* wconv, int nbh, int nh, int n, void* merged, float* lse1, void* stream) {
+  TM_REQUIRE(n > 0 && n % NL == 0 && nbh % nh == 0, "a1_fwd: bad shape");
+  hipStream_t st = (hipStream_t)stream;
+  TM_DTYPE_DISPATCH(dtype, ({
+    const size_t sm1 = (size_t)NL * Lay<T>::KROW * sizeof(T) + (size_t)DH * Lay<T>::VROW * sizeof(T);
+    const size_t sm = sm1 > 128 * 68 * 4 ? sm1 : 128 * 68 * 4;
+    tm_allow_smem(a1_fwd_kernel<T>, sm);
+    a1_fwd_kernel<T><<<dim3(n / 128, nbh), 256, sm, st>>>((const T*)q, (const T*)v, kl, y, wconv, n, nh,
+                                                          (T*)merged, lse1);
+  }));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_nys_rowdot_cast(int dtype, const float* dw, const float* w, int rows, float* dd, void* dw_t,
+                                  void* stream) {
+  TM_DTYPE_DISPATCH(dtype, (rowdot_cast_kernel<T><<<(rows + 3) / 4, 256, 0, (hipStream_t)stream>>>(
+                               dw, w, dd, (T*)dw_t, rows)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_cast_f32(int dtype, const float* x, void* y, long long count, void* stream) {
+  if (count == 0) return 0;
+  TM_DTYPE_DISPATCH(dtype, (cast_rows_kernel<T><<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+                               x, (T*)y, count)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" long long tm_nys_conv_bwd_workspace(int nbags, int nh, int n) {
+  return (long long)nbags * ((n + 63) / 64) * nh * TAPS * (long long)sizeof(float);
+}
+
+extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merged, const void* v, const float* wconv,
+                               int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv,
+                               void* stream) {
+  TM_REQUIRE(nbh % nh == 0 && n > 0, "conv_bwd: bad shape");
+  const int ntb = (n + 63) / 64;
+  hipStream_t st = (hipStream_t)stream;
+  TM_DTYPE_DISPATCH(dtype, (conv_bwd_kernel<T><<<dim3(ntb, nbh), 256, 0, st>>>(
+                               (const T*)dmerged, (const T*)merged, (const T*)v, wconv, n, nh, dv, d1, work)));
+  TM_CHECK_LAUNCH();
+  return tm_splitk_reduce(work, dwconv, (nbh / nh) * ntb, (long long)nh * TAPS, 1.0f, 0, stream);
+}
+
+// A1 backward: keys = landmarks kl_t [bh][256][64], values = y_t, queries = q rows, dO = dmerged.
+// dq (fp32 [bh][n][64]) written; dkl/dy partial slabs [n/qpw][bh][256][64] in work.
+extern "C" long long tm_nys_a1_bwd_workspace(int nbh, int n, int queries_per_wg) {
+  return 2LL * (n / queries_per_wg) * nbh * NL * DH * (long long)sizeof(float);
+}
+
+extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t,
+                             const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
+                             float* dq, float* work, float* dkl, float* dy, int accumulate, void* stream) {
+  TM_REQUIRE(queries_per_wg % 32 == 0 && n % queries_per_wg == 0, "a1_bwd: queries_per_wg must divide n, x32");
+  const int nqc = n / queries_per_wg;
+  BwdArgs a{};
+  a.q = q; a.q_bag = (long long)nh * n * DH; a.q_head = (long long)n * DH; a.q_row = DH;
+  a.dO = dmerged; a.o_bag = (long long)n * nh * DH; a.o_head = DH; a.o_row = nh * DH;
+  a.k = kl_t; a.k_bag = (long long)nh * NL * DH; a.k_head = (long long)NL * DH;
+  a.v = y_t; a.v_bag = a.k_bag; a.v_head = a.k_head;
+  a.lse = lse1; a.lse_bh = n; a.dd = d1; a.dd_bh = n;
+  a.dq = dq; a.dq_bh = (long long)n * DH;
+  float* slab_k = work;
+  float* slab_v = work + (size_t)nqc * nbh * NL * DH;
+  a.dk = slab_k; a.dk_bh = (long long)NL * DH;
+  a.dv = slab_v; a.dv_bh = (long long)NL * DH;
+  a.slab_stride = (long long)nbh * NL * DH;
+  a.nh = nh; a.n_queries_per_wg = queries_per_wg; a.n_key_rows = NL;
+  hipStream_t st = (hipStream_t)stream;
+  TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A1>, bwd_smem_bytes<T>()),
+                            attn_bwd_kernel<T, MODE_A1><<<dim3(nqc, nbh), 256, bwd_smem_bytes<T>(), st>>>(a)));
+  TM_CHECK_LAUNCH();
+  const long long cnt = (long long)nbh * NL * DH;
+  int rc = tm_splitk_reduce(slab_k, dkl, nqc, cnt, 1.0f, accumulate, stream);
+  if (rc) return rc;
+  return tm_splitk_reduce(slab_v, dy, nqc, cnt, 1.0f, 0, stream);
+}
+
+// A3 backward: keys = k rows, values = v rows, queries = ql_t (256 landmarks), dO = dw_t.
+// dk written (=), dv accumulated (+=), dql accumulated from partial slabs.
+extern "C" long long tm_nys_a3_bwd_workspace(int nbh, int n) {
+  return (long long)(n / NL) * nbh * NL * DH * (long long)sizeof(float);
+}
+
+extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
+                             const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
+                             float* work, float* dql, void* stream) {
+  TM_REQUIRE(n % NL == 0, "a3_bwd: n must be a multiple of 256");
+  const int nkb = n / NL;
+  BwdArgs a{};
+  a.q = ql_t; a.q_bag = (long long)nh * NL * DH; a.q_head = (long long)NL * DH; a.q_row = DH;
+  a.dO = dw_t; a.o_bag = a.q_bag; a.o_head = a.q_head; a.o_row = DH;
+  a.k = k; a.k_bag = (long long)nh * n * DH; a.k_head = (long long)n * DH;
+  a.v = v; a.v_bag = a.k_bag; a.v_head = a.k_head;
+  a.lse = lse3; a.lse_bh = NL; a.dd = d3; a.dd_bh = NL;
+  a.dq = work; a.dq_bh = (long long)NL * DH;
+  a.slab_stride = (long long)nbh * NL * DH;
+  a.dk = dk; a.dk_bh = (long long)n * DH;
+  a.dv = dv; a.dv_bh = (long long)n * DH;
+  a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
+  hipStream_t st = (hipStream_t)stream;
+  TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A3>, bwd_smem_bytes<T>()),
+                            attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 256, bwd_smem_bytes<T>(), st>>>(a)));
+  TM_CHECK_LAUNCH();
+  return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, 1, stream);
+}
+
+extern "C" int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const float* dk, const float* dkl,
+                                    const float* dv, int nbags, int nh, int n, float scale, void* dqkv,
+                                    void* stream) {
+  TM_REQUIRE(n % NL == 0, "assemble_dqkv: n must be a multiple of 256");
+  TM_DTYPE_DISPATCH(dtype, (assemble_dqkv_kernel<T><<<dim3(n, nbags), 256, 0, (hipStream_t)stream>>>(
+                               dq, dql, dk, dkl, dv, n, n / NL, nh, scale, (T*)dqkv)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,321 @@
+// Moore-Penrose iterative pseudo-inverse (SURVEY.md App. A eq. 7) and the small
+// batched fp32 products around it (Y = Z W and their backward).
+//
+// Replaces `moore_penrose_iter_pinv` of the third-party nystrom_attention
+// package (called from NystromAttention.forward, code/models/TransMIL.py:47):
+//   Z0 = X^T / (max_all rowsum|X| * max_all colsum|X|)      (maxima over ALL bags and heads)
+//   6 x { P = X Z;  T3 = 15I - 7P + P P;  T5 = 13I - P T3;  Z = 0.25 Z T5 }
+// (= 0.25 Z (13I - XZ(15I - XZ(7I - XZ))) with the inner product expanded).
+//
+// Always fp32, on v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains): the
+// attn2 entries sit in a ~5 % band around 1/256 and do not survive bf16.
+// Every product is a 256x256(x64) fp32 batch over B*heads; one workgroup
+// computes one 32x32 output tile with its 4 waves splitting K (reduced in LDS
+// in a fixed order), batch index = blockIdx % nbatch so all tiles of one head
+// land on one XCD (blocks b and b+8 share an XCD) and its 256 KB operands stay
+// in that XCD's L2.
+#include "common.h"
+#include "../../include/transmil_hip.h"
+
+namespace {
+
+constexpr int NL = 256;
+
+struct JobPair { tm_bmm_job j[2]; int tiles0; };
+
+TM_DEV f32x8 frag_a(const float* A, int ta, int lda, int m, int k) {
+  if (ta == 0) return load8<float>(A + (size_t)m * lda + k);
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = A[(size_t)(k + e) * lda + m];
+  return r;
+}
+TM_DEV f32x8 frag_b(const float* B, int tb, int ldb, int k, int n) {
+  if (tb == 1) return load8<float>(B + (size_t)n * ldb + k);
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = B[(size_t)(k + e) * ldb + n];
+  return r;
+}
+
+__global__ __launch_bounds__(256) void bmm_kernel(JobPair jp, int nbatch) {
+  __shared__ float red[4][16][64];
+  int b = blockIdx.x;
+  const int which = b < jp.tiles0 * nbatch ? 0 : 1;
+  if (which) b -= jp.tiles0 * nbatch;
+  const tm_bmm_job& J = jp.j[which];
+  const int bh = b % nbatch, tile = b / nbatch;
+  const int ntn = J.N / 32;
+  const int tm = tile / ntn, tn = tile % ntn;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int nterms = J.A2 ? 2 : 1;
+  const int kchunk = J.K * nterms / 4;
+  f32x16 acc = (f32x16){};
+  for (int kk = wave * kchunk; kk < (wave + 1) * kchunk; kk += 16) {
+    const int term = kk / J.K, kl = kk % J.K;
+    const float* A = term ? J.A2 + bh * J.sa2 : J.A + bh * J.sa;
+    const float* B = term ? J.B2 + bh * J.sb2 : J.B + bh * J.sb;
+    const int ta = term ? J.ta2 : J.ta, tb = term ? J.tb2 : J.tb;
+    const int lda = term ? J.lda2 : J.lda, ldb = term ? J.ldb2 : J.ldb;
+    const f32x8 af = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
+    const f32x8 bf = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
+    mma16(acc, af, bf);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[wave][i][lane] = acc[i];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = tid + 256 * q, reg = e >> 6, ln = e & 63;
+    const float s = ((red[0][reg][ln] + red[1][reg][ln]) + red[2][reg][ln]) + red[3][reg][ln];
+    const int row = tm * 32 + acc_row(reg, ln >> 5), col = tn * 32 + (ln & 31);
+    const size_t off = (size_t)bh * J.sc + (size_t)row * J.ldc + col;
+    float v = J.alpha * s;
+    if (row == col) v += J.diag;
+    if (J.E1) v += J.e1 * J.E1[off];
+    if (J.E2) v += J.e2 * J.E2[off];
+    J.C[off] = v;
+  }
+}
+
+// rowsum / colsum of |X|: grid (nbh, 2), block 256
+__global__ void abs_sums_kernel(const float* __restrict__ X, float* __restrict__ sums, int nbh) {
+  const int bh = blockIdx.x, t = threadIdx.x;
+  const float* x = X + (size_t)bh * NL * NL;
+  float s = 0.f;
+  if (blockIdx.y == 0) {
+    for (int j = 0; j < NL; ++j) s += fabsf(x[(size_t)t * NL + j]);
+    sums[(size_t)bh * NL + t] = s;                       // rowsum ("col" in the package)
+  } else {
+    for (int i = 0; i < NL; ++i) s += fabsf(x[(size_t)i * NL + t]);
+    sums[(size_t)(nbh + bh) * NL + t] = s;               // colsum ("row" in the package)
+  }
+}
+
+struct MaxInfo { float maxc, maxr; float nc, nr; };
+
+TM_DEV MaxInfo block_maxima(const float* sums, int nbh, float* red) {
+  const int t = threadIdx.x, total = nbh * NL;
+  float mc = -INFINITY, mr = -INFINITY;
+  for (int i = t; i < total; i += 256) { mc = fmaxf(mc, sums[i]); mr = fmaxf(mr, sums[total + i]); }
+  mc = wave_max(mc); mr = wave_max(mr);
+  if ((t & 63) == 0) { red[t >> 6] = mc; red[4 + (t >> 6)] = mr; }
+  __syncthreads();
+  MaxInfo mi;
+  mi.maxc = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  mi.maxr = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+  __syncthreads();
+  float nc = 0.f, nr = 0.f;
+  for (int i = t; i < total; i += 256) { nc += sums[i] == mi.maxc; nr += sums[total + i] == mi.maxr; }
+  nc = wave_sum(nc); nr = wave_sum(nr);
+  if ((t & 63) == 0) { red[t >> 6] = nc; red[4 + (t >> 6)] = nr; }
+  __syncthreads();
+  mi.nc = red[0] + red[1] + red[2] + red[3];
+  mi.nr = red[4] + red[5] + red[6] + red[7];
+  __syncthreads();
+  return mi;
+}
+
+// Z0[bh][i][j] = X[bh][j][i] / (maxc * maxr); grid (nbh, 16), block 256 (16 rows of Z0 each)
+__global__ __launch_bounds__(256) void pinv_init_kernel(const float* __restrict__ X, const float* __restrict__ sums,
+                                                        int nbh, float* __restrict__ Z0, float* __restrict__ stats) {
+  __shared__ float red[8];
+  __shared__ float tile[NL][17];
+  const MaxInfo mi = block_maxima(sums, nbh, red);
+  const float denom = mi.maxc * mi.maxr;
+  const int bh = blockIdx.x, i0 = blockIdx.y * 16, t = threadIdx.x;
+  const float* x = X + (size_t)bh * NL * NL;
+  for (int e = t; e < NL * 16; e += 256) {
+    const int j = e >> 4, ii = e & 15;
+    tile[j][ii] = x[(size_t)j * NL + i0 + ii];          // X[j][i0+ii]
+  }
+  __syncthreads();
+  for (int ii = 0; ii < 16; ++ii) Z0[((size_t)bh * NL + i0 + ii) * NL + t] = tile[t][ii] / denom;
+  if (bh == 0 && blockIdx.y == 0 && t == 0) {
+    stats[0] = mi.maxc; stats[1] = mi.maxr; stats[2] = denom; stats[3] = mi.nc; stats[4] = mi.nr;
+  }
+}
+
+// partial sums of G0 * Z0 over 16-row slices: grid (nbh, 16)
+__global__ void dot_partial_kernel(const float* __restrict__ G, const float* __restrict__ Z, float* __restrict__ part) {
+  __shared__ float red[4];
+  const size_t base = ((size_t)blockIdx.x * NL + blockIdx.y * 16) * NL;
+  float s = 0.f;
+  for (int e = threadIdx.x; e < 16 * NL; e += 256) s += G[base + e] * Z[base + e];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x * gridDim.y + blockIdx.y] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// dX[bh][i][j] += G0[bh][j][i]/denom + sign(X_ij) * (tie_c(bh,i) dMc/nc + tie_r(bh,j) dMr/nr)
+// with dc = -sum(G0*Z0)/denom, dMc = dc*maxr, dMr = dc*maxc.  grid (nbh, 16)
+__global__ __launch_bounds__(256) void pinv_init_bwd_kernel(const float* __restrict__ X, const float* __restrict__ sums,
+                                                            const float* __restrict__ G0, const float* __restrict__ gz,
+                                                            int nbh, float* __restrict__ dX) {
+  __shared__ float red[8];
+  __shared__ float tile[NL][17];
+  const MaxInfo mi = block_maxima(sums, nbh, red);
+  const float denom = mi.maxc * mi.maxr;
+  const float dc = -gz[0] / denom;
+  const float dMc = dc * mi.maxr / mi.nc, dMr = dc * mi.maxc / mi.nr;
+  const int bh = blockIdx.x, i0 = blockIdx.y * 16, t = threadIdx.x;
+  const float* g = G0 + (size_t)bh * NL * NL;
+  for (int e = t; e < NL * 16; e += 256) {
+    const int j = e >> 4, ii = e & 15;
+    tile[j][ii] = g[(size_t)j * NL + i0 + ii];          // G0[j][i0+ii]
+  }
+  __syncthreads();
+  const float* rs = sums + (size_t)bh * NL;
+  const float* cs = sums + (size_t)(nbh + bh) * NL;
+  const float tie_r = cs[t] == mi.maxr ? dMr : 0.f;
+  for (int ii = 0; ii < 16; ++ii) {
+    const int i = i0 + ii;
+    const size_t off = ((size_t)bh * NL + i) * NL + t;
+    const float xv = X[off];
+    const float sg = xv > 0.f ? 1.f : (xv < 0.f ? -1.f : 0.f);
+    const float tie_c = rs[i] == mi.maxc ? dMc : 0.f;
+    dX[off] += tile[t][ii] / denom + sg * (tie_c + tie_r);
+  }
+}
+
+int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, hipStream_t st) {
+  TM_REQUIRE(njobs == 1 || njobs == 2, "bmm: njobs must be 1 or 2");
+  JobPair jp{};
+  int total = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const tm_bmm_job& J = jobs[i];
+    TM_REQUIRE(J.A && J.B && J.C, "bmm: null operand");
+    TM_REQUIRE(J.M % 32 == 0 && J.N % 32 == 0, "bmm: M, N must be multiples of 32");
+    const int nterms = J.A2 ? 2 : 1;
+    TM_REQUIRE((J.K * nterms) % 64 == 0 && J.K % ((J.K * nterms) / 4) == 0, "bmm: K split must be 16-aligned per wave");
+    jp.j[i] = J;
+    const int tiles = (J.M / 32) * (J.N / 32);
+    if (i == 0) jp.tiles0 = tiles;
+    total += tiles * nbatch;
+  }
+  bmm_kernel<<<total, 256, 0, st>>>(jp, nbatch);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+tm_bmm_job job(const float* A, int ta, const float* B, int tb, float* C, int M, int N, int K, float alpha,
+               float diag = 0.f) {
+  tm_bmm_job j{};
+  j.A = A; j.ta = ta; j.B = B; j.tb = tb;
+  j.lda = ta ? M : K;
+  j.ldb = tb ? K : N;
+  j.sa = (long long)M * K; j.sb = (long long)K * N;
+  j.C = C; j.ldc = N; j.sc = (long long)M * N;
+  j.M = M; j.N = N; j.K = K;
+  j.alpha = alpha; j.diag = diag;
+  return j;
+}
+void add_term(tm_bmm_job& j, const float* A, int ta, const float* B, int tb) {
+  j.A2 = A; j.ta2 = ta; j.B2 = B; j.tb2 = tb;
+  j.lda2 = ta ? j.M : j.K;
+  j.ldb2 = tb ? j.K : j.N;
+  j.sa2 = (long long)j.M * j.K; j.sb2 = (long long)j.K * j.N;
+}
+
+}  // namespace
+
+extern "C" int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, void* stream) {
+  return launch_bmm(jobs, njobs, nbatch, (hipStream_t)stream);
+}
+
+// workspace: Zs[iters+1], Ps[iters], T3s[iters], T5s[iters] (each nbh*256*256 fp32) + sums[2][nbh][256] + stats[8]
+extern "C" long long tm_pinv_saved_floats(int nbh, int iters) {
+  return (4LL * iters + 1) * nbh * NL * NL + 2LL * nbh * NL + 8;
+}
+
+extern "C" int tm_pinv_fwd(const float* X, int nbh, int iters, float* saved, void* stream) {
+  TM_REQUIRE(X && saved && iters >= 0, "pinv_fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t mat = (size_t)nbh * NL * NL;
+  float* Zs = saved;
+  float* Ps = Zs + (iters + 1) * mat;
+  float* T3s = Ps + iters * mat;
+  float* T5s = T3s + iters * mat;
+  float* sums = T5s + iters * mat;
+  float* stats = sums + 2 * (size_t)nbh * NL;
+  abs_sums_kernel<<<dim3(nbh, 2), 256, 0, st>>>(X, sums, nbh);
+  TM_CHECK_LAUNCH();
+  pinv_init_kernel<<<dim3(nbh, NL / 16), 256, 0, st>>>(X, sums, nbh, Zs, stats);
+  TM_CHECK_LAUNCH();
+  for (int it = 0; it < iters; ++it) {
+    float* Z = Zs + it * mat;
+    float* P = Ps + it * mat;
+    float* T3 = T3s + it * mat;
+    float* T5 = T5s + it * mat;
+    tm_bmm_job j = job(X, 0, Z, 0, P, NL, NL, NL, 1.f);               // P = X Z
+    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+    j = job(P, 0, P, 0, T3, NL, NL, NL, 1.f, 15.f);                    // T3 = 15I + P P - 7P
+    j.E1 = P; j.e1 = -7.f;
+    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+    j = job(P, 0, T3, 0, T5, NL, NL, NL, -1.f, 13.f);                  // T5 = 13I - P T3
+    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+    j = job(Z, 0, T5, 0, Zs + (it + 1) * mat, NL, NL, NL, 0.25f);      // Z' = 0.25 Z T5
+    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+  }
+  return 0;
+}
+
+// workspace: 5 matrices + partial dots (nbh*16) + 1
+extern "C" long long tm_pinv_bwd_workspace_floats(int nbh) {
+  return 5LL * nbh * NL * NL + nbh * 16LL + 16;
+}
+
+// dZ (gradient w.r.t. the final Z) is consumed (overwritten).  dX is written (=).
+extern "C" int tm_pinv_bwd(const float* X, int nbh, int iters, const float* saved, float* dZ, float* work, float* dX,
+                           void* stream) {
+  TM_REQUIRE(X && saved && dZ && work && dX, "pinv_bwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  const size_t mat = (size_t)nbh * NL * NL;
+  const float* Zs = saved;
+  const float* Ps = Zs + (iters + 1) * mat;
+  const float* T3s = Ps + iters * mat;
+  const float* T5s = T3s + iters * mat;
+  const float* sums = T5s + iters * mat;
+  float* dT5 = work;
+  float* dZa = dT5 + mat;
+  float* dP = dZa + mat;
+  float* dT3 = dP + mat;
+  float* part = dT3 + 2 * mat;  // (one spare matrix kept for alignment)
+  float* gz = part + nbh * 16;
+  float* G = dZ;
+  bool first = true;
+  for (int it = iters - 1; it >= 0; --it) {
+    const float* Z = Zs + it * mat;
+    const float* P = Ps + it * mat;
+    const float* T3 = T3s + it * mat;
+    const float* T5 = T5s + it * mat;
+    tm_bmm_job jb[2];
+    jb[0] = job(Z, 1, G, 0, dT5, NL, NL, NL, 0.25f);                    // dT5 = 0.25 Z^T G
+    jb[1] = job(G, 0, T5, 1, dZa, NL, NL, NL, 0.25f);                   // dZa = 0.25 G T5^T
+    if (int rc = launch_bmm(jb, 2, nbh, st)) return rc;
+    jb[0] = job(dT5, 0, T3, 1, dP, NL, NL, NL, -1.f);                   // dP  = -dT5 T3^T
+    jb[1] = job(P, 1, dT5, 0, dT3, NL, NL, NL, -1.f);                   // dT3 = -P^T dT5
+    if (int rc = launch_bmm(jb, 2, nbh, st)) return rc;
+    jb[0] = job(dT3, 0, P, 1, dP, NL, NL, NL, 1.f);                     // dP += dT3 P^T + P^T dT3 - 7 dT3
+    add_term(jb[0], P, 1, dT3, 0);
+    jb[0].E1 = dP; jb[0].e1 = 1.f; jb[0].E2 = dT3; jb[0].e2 = -7.f;
+    if (int rc = launch_bmm(jb, 1, nbh, st)) return rc;
+    jb[0] = job(dP, 0, Z, 1, dX, NL, NL, NL, 1.f);                      // dX (+)= dP Z^T
+    if (!first) { jb[0].E1 = dX; jb[0].e1 = 1.f; }
+    jb[1] = job(X, 1, dP, 0, G, NL, NL, NL, 1.f);                       // G = dZa + X^T dP
+    jb[1].E1 = dZa; jb[1].e1 = 1.f;
+    if (int rc = launch_bmm(jb, 2, nbh, st)) return rc;
+    first = false;
+  }
+  if (first) {  // iters == 0: dX starts at zero
+    if (hipMemsetAsync(dX, 0, mat * sizeof(float), st) != hipSuccess) { tm_set_error("pinv_bwd: memset"); return 2; }
+  }
+  // init: Z0 = X^T / (maxc * maxr)
+  dot_partial_kernel<<<dim3(nbh, 16), 256, 0, st>>>(G, Zs, part);
+  TM_CHECK_LAUNCH();
+  if (int rc = tm_splitk_reduce(part, gz, nbh * 16, 1, 1.0f, 0, stream)) return rc;
+  pinv_init_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, sums, G, gz, nbh, dX);
+  TM_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,509 @@
+"""Host-side orchestration of the TransMIL hot path on the HIP kernels.
+
+This is the MI355X replacement for the torch op sequence of
+``TransMIL.forward`` (code/models/TransMIL.py:167-211) and its autograd
+backward.  Every arithmetic step is one of the C-ABI entry points of
+``libtransmil_hip.so``; PyTorch only allocates device memory and supplies the
+stream.  There is no fallback: without the library this module raises.
+
+Shapes (B bags of N patches, D = 512 = 8 heads x 64):
+    G = ceil(sqrt(N)), add = G*G - N, S = G*G + 1        (grid pad + class token, :177-186)
+    n = ceil(S / 256) * 256, pad = n - S, l = n / 256    (NystromAttention front pad, App. A eq. 1)
+Buffers:
+    H*  [B*S, D] fp32 residual stream;  xn [B, n, D] T (LN output, pad rows 0)
+    qkv [3, B*8, n, 64] T;  merged [B, n, D] T
+``T`` is bf16 (bench mode) or fp32 (parity mode).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib
+from ._lib import BF16, F32, EPI_PLAIN, EPI_QKV, EPI_SPLITK, GemmArgs, BmmJob
+
+NL = 256        # landmarks
+DH = 64         # dim_head
+TAPS = 33       # residual conv
+PINV_ITERS = 6
+LN_EPS = 1e-5
+
+
+class _Probe:
+    """Optional HIP-event timing of ONE named call site (bench.py's roofline leg).
+
+    Events are recorded on the current stream -- the stream the kernel is
+    launched on -- so their difference is that launch's duration."""
+
+    def __init__(self):
+        self.target = None
+        self.events = []
+
+    def __call__(self, name):
+        return _ProbeCtx(self, name)
+
+
+class _ProbeCtx:
+    def __init__(self, probe, name):
+        self.p, self.name = probe, name
+
+    def __enter__(self):
+        if self.p.target == self.name:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.e = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.p.target == self.name:
+            self.e.record()
+            self.p.events.append((self.s, self.e))
+        return False
+
+
+probe = _Probe()
+
+
+def _p(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@dataclass
+class Geometry:
+    B: int
+    N: int
+    F: int
+    D: int
+    heads: int
+
+    def __post_init__(self):
+        self.G = int(math.ceil(math.sqrt(self.N)))
+        self.add = self.G * self.G - self.N
+        self.S = self.G * self.G + 1
+        self.n = ((self.S + NL - 1) // NL) * NL
+        self.pad = self.n - self.S
+        self.l = self.n // NL
+        self.nbh = self.B * self.heads
+
+
+# ----------------------------------------------------------------------------- GEMM helpers
+def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c_dtype=None,
+         alpha=1.0, bias=None, gelu=False, pre=None, ld_pre=0, drop_p=0.0, seed=0, resid=None,
+         accumulate=False, rowmap=None, qkv=None, splits=1, k_per_split=None):
+    g = GemmArgs()
+    g.M, g.N, g.K = M, N, K
+    g.lda, g.ldb, g.ldc = lda, ldb, ldc
+    g.a_trans, g.b_kn = a_trans, b_kn
+    g.ab_dtype = dtype
+    g.c_dtype = dtype if c_dtype is None else c_dtype
+    g.splits = splits
+    bk = 32 if dtype == BF16 else 16
+    if k_per_split is None:
+        k_per_split = ((K + splits - 1) // splits + bk - 1) // bk * bk
+    g.k_per_split = max(k_per_split, 1)
+    g.mode = EPI_PLAIN
+    g.alpha = alpha
+    g.bias = _p(bias)
+    g.gelu = int(gelu)
+    g.pre = _p(pre)
+    g.ld_pre = ld_pre
+    g.drop_p = drop_p
+    g.drop_scale = 1.0 / (1.0 - drop_p) if drop_p > 0 else 1.0
+    g.seed = seed
+    g.resid = _p(resid)
+    g.accumulate = int(accumulate)
+    if rowmap is not None:
+        g.grp_in, g.skip, g.grp_out, g.out_off, g.dup_n, g.dup_off = rowmap
+    if qkv is not None:
+        g.mode = EPI_QKV
+        g.nbags, g.nh, g.dh, g.seq, g.qscale = qkv
+    _lib.call("tm_gemm", _p(A), _p(B), _p(Cout), C.byref(g), _stream())
+
+
+def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool):
+    """out[M,N] (fp32) = sum_k dY[k, m] X[k, n]  (split-K, deterministic)."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    splits = max(1, min(16, 320 // max(tiles, 1), (K + 255) // 256))
+    if splits == 1:
+        gemm(dY, X, out, M, N, K, lda=ldy, ldb=ldx, ldc=N, a_trans=1, b_kn=1, dtype=dtype, c_dtype=F32)
+        return
+    bk = 32 if dtype == BF16 else 16
+    kps = ((K + splits - 1) // splits + bk - 1) // bk * bk
+    splits = (K + kps - 1) // kps
+    slab = work_pool(splits * M * N)
+    g = GemmArgs()
+    g.M, g.N, g.K = M, N, K
+    g.lda, g.ldb, g.ldc = ldy, ldx, N
+    g.a_trans, g.b_kn = 1, 1
+    g.ab_dtype, g.c_dtype = dtype, F32
+    g.splits, g.k_per_split = splits, kps
+    g.mode = EPI_SPLITK
+    g.alpha = 1.0
+    _lib.call("tm_gemm", _p(dY), _p(X), _p(slab), C.byref(g), _stream())
+    _lib.call("tm_splitk_reduce", _p(slab), _p(out), splits, M * N, C.c_float(1.0), 0, _stream())
+
+
+def colsum(X, rows, cols, ld, dtype, out, work_pool, accumulate=False):
+    rpc = 256
+    nchunk = (rows + rpc - 1) // rpc
+    work = work_pool(nchunk * cols)
+    _lib.call("tm_colsum", _p(X), dtype, rows, cols, ld, rpc, _p(work), _p(out), int(accumulate), _stream())
+
+
+def bmm_job(A, ta, B, tb, Cout, M, N, K, alpha=1.0, diag=0.0, E1=None, e1=0.0, E2=None, e2=0.0):
+    j = BmmJob()
+    j.A, j.B = A.data_ptr(), B.data_ptr()
+    j.ta, j.tb = ta, tb
+    j.lda = M if ta else K
+    j.ldb = K if tb else N
+    j.sa, j.sb = M * K, K * N
+    j.A2 = j.B2 = None
+    j.E1 = E1.data_ptr() if E1 is not None else None
+    j.e1 = e1
+    j.E2 = E2.data_ptr() if E2 is not None else None
+    j.e2 = e2
+    j.alpha, j.diag = alpha, diag
+    j.C = Cout.data_ptr()
+    j.ldc, j.sc = N, M * N
+    j.M, j.N, j.K = M, N, K
+    return j
+
+
+def bmm(jobs, nbatch):
+    arr = (BmmJob * len(jobs))(*jobs)
+    _lib.call("tm_bmm", arr, len(jobs), nbatch, _stream())
+
+
+class Pool:
+    """Scratch allocator for one forward or backward call (torch caching allocator underneath)."""
+
+    def __init__(self, device):
+        self.device = device
+
+    def __call__(self, numel, dtype=torch.float32):
+        return torch.empty(int(numel), dtype=dtype, device=self.device)
+
+
+# ----------------------------------------------------------------------------- NystromAttention core
+def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
+    """App. A eq. 4-9 on q, k, v [3, B*h, n, 64] -> merged [B, n, h*64] (T) + saved state."""
+    n, nbh, nh = geo.n, geo.nbh, geo.heads
+    q, k, v = qkv[0], qkv[1], qkv[2]
+    st = _stream()
+    ql = pool(nbh * NL * DH).view(nbh, NL, DH)
+    kl = pool(nbh * NL * DH).view(nbh, NL, DH)
+    ql_t = pool(nbh * NL * DH, tdtype).view(nbh, NL, DH)
+    kl_t = pool(nbh * NL * DH, tdtype).view(nbh, NL, DH)
+    _lib.call("tm_nys_landmarks", dt_code, _p(q), _p(k), nbh, n, _p(ql), _p(kl), _p(ql_t), _p(kl_t), st)
+    a2 = pool(nbh * NL * NL).view(nbh, NL, NL)
+    _lib.call("tm_nys_sim2_softmax", _p(ql), _p(kl), nbh, _p(a2), st)
+    saved = pool(_lib.query("tm_pinv_saved_floats", nbh, PINV_ITERS))
+    _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, _p(saved), st)
+    z = saved[PINV_ITERS * nbh * NL * NL:(PINV_ITERS + 1) * nbh * NL * NL].view(nbh, NL, NL)
+    w = pool(nbh * NL * DH).view(nbh, NL, DH)
+    lse3 = pool(nbh * NL)
+    work = pool(_lib.query("tm_nys_a3_workspace", nbh, n) // 4)
+    with probe("a3_fwd"):
+        _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
+    y = pool(nbh * NL * DH).view(nbh, NL, DH)
+    bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh)
+    merged = pool(geo.B * n * nh * DH, tdtype).view(geo.B, n, nh * DH)
+    lse1 = pool(nbh * n)
+    with probe("a1_fwd"):
+        _lib.call("tm_nys_a1_fwd", dt_code, _p(q), _p(v), _p(kl), _p(y), _p(wconv), nbh, nh, n, _p(merged),
+                  _p(lse1), st)
+    state = dict(ql=ql, kl=kl, ql_t=ql_t, kl_t=kl_t, a2=a2, pinv=saved, z=z, w=w, lse3=lse3, y=y, lse1=lse1)
+    return merged, state
+
+
+def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdtype, dt_code, pool,
+                          dwconv_out, scale):
+    """Backward of nystrom_core_forward: returns dqkv [B, n, 3*h*64] (T); writes dwconv_out."""
+    n, nbh, nh = geo.n, geo.nbh, geo.heads
+    q, k, v = qkv[0], qkv[1], qkv[2]
+    st = _stream()
+    mat = nbh * NL * NL
+    # conv33 backward + D1
+    dq = pool(nbh * n * DH)
+    dk = pool(nbh * n * DH)
+    dv = pool(nbh * n * DH)
+    d1 = pool(nbh * n)
+    work = pool(_lib.query("tm_nys_conv_bwd_workspace", geo.B, nh, n) // 4)
+    with probe("conv_bwd"):
+        _lib.call("tm_nys_conv_bwd", dt_code, _p(dmerged), _p(merged), _p(v), _p(wconv), nbh, nh, n, _p(dv),
+                  _p(d1), _p(work), _p(dwconv_out), st)
+    # A1 product backward: dq (complete), dkl, dY
+    y_t = pool(nbh * NL * DH, tdtype)
+    _lib.call("tm_cast_f32", dt_code, _p(state["y"]), _p(y_t), nbh * NL * DH, st)
+    qpw = 256 if n % 256 == 0 else 32
+    dkl = pool(nbh * NL * DH).view(nbh, NL, DH)
+    dy = pool(nbh * NL * DH).view(nbh, NL, DH)
+    work = pool(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, qpw) // 4)
+    with probe("a1_bwd"):
+        _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t), _p(state["lse1"]),
+                  _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, st)
+    # Y = Z W
+    dz = pool(mat).view(nbh, NL, NL)
+    dw = pool(nbh * NL * DH).view(nbh, NL, DH)
+    bmm([bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH),
+         bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh)
+    # pseudo-inverse backward -> dA2, then softmax backward
+    da2 = pool(mat).view(nbh, NL, NL)
+    pwork = pool(_lib.query("tm_pinv_bwd_workspace_floats", nbh))
+    _lib.call("tm_pinv_bwd", _p(state["a2"]), nbh, PINV_ITERS, _p(state["pinv"]), _p(dz), _p(pwork), _p(da2), st)
+    ds2 = pool(mat).view(nbh, NL, NL)
+    _lib.call("tm_softmax_bwd_rows256", _p(state["a2"]), _p(da2), _p(ds2), nbh * NL, st)
+    dql = pool(nbh * NL * DH).view(nbh, NL, DH)
+    bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL),
+         bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh)
+    # A3 product backward: dk (=), dv (+=), dql (+=)
+    d3 = pool(nbh * NL)
+    dw_t = pool(nbh * NL * DH, tdtype)
+    _lib.call("tm_nys_rowdot_cast", dt_code, _p(dw), _p(state["w"]), nbh * NL, _p(d3), _p(dw_t), st)
+    work = pool(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4)
+    with probe("a3_bwd"):
+        _lib.call("tm_nys_a3_bwd", dt_code, _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]), _p(d3),
+                  nbh, nh, n, _p(dk), _p(dv), _p(work), _p(dql), st)
+    dqkv = pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH)
+    _lib.call("tm_nys_assemble_dqkv", dt_code, _p(dq), _p(dql), _p(dk), _p(dkl), _p(dv), geo.B, nh, n,
+              C.c_float(scale), _p(dqkv), st)
+    return dqkv
+
+
+# ----------------------------------------------------------------------------- TransLayer
+def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, seed):
+    """H [B*S, D] fp32 -> H + NystromAttention(LN(H)) (code/models/TransMIL.py:45-57)."""
+    B, S, n, D, pad = geo.B, geo.S, geo.n, geo.D, geo.pad
+    st = _stream()
+    xn = pool(B * n * D, tdtype).view(B, n, D)
+    mean = pool(B * S)
+    rstd = pool(B * S)
+    _lib.call("tm_layernorm_fwd", _p(H), _p(prm["norm_w"]), _p(prm["norm_b"]), C.c_float(LN_EPS), B * S, D,
+              S, n, pad, dt_code, _p(xn), _p(mean), _p(rstd), st)
+    qkv = pool(3 * geo.nbh * n * DH, tdtype).view(3, geo.nbh, n, DH)
+    with probe("qkv_gemm"):
+        gemm(xn, prm["wqkv"], qkv, B * n, 3 * D, D, lda=D, ldb=D, ldc=0, dtype=dt_code,
+             qkv=(B, geo.heads, DH, n, DH ** -0.5))
+    merged, state = nystrom_core_forward(qkv, geo, prm["wconv"], tdtype, dt_code, pool)
+    Hout = pool(B * S * D).view(B * S, D)
+    gemm(merged, prm["wo"], Hout, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=dt_code, c_dtype=F32,
+         bias=prm["bo"], drop_p=drop_p, seed=seed, resid=H, rowmap=(n, pad, S, 0, 0, 0))
+    saved = dict(xn=xn, mean=mean, rstd=rstd, qkv=qkv, merged=merged, core=state, seed=seed, drop_p=drop_p)
+    return Hout, saved
+
+
+def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_code, pool):
+    """dH [B*S, D] fp32 (gradient of the layer output) is turned IN PLACE into the
+    gradient of the layer input.  Parameter gradients go to ``grads``."""
+    B, S, n, D, pad = geo.B, geo.S, geo.n, geo.D, geo.pad
+    st = _stream()
+    dout = pool(B * n * D, tdtype).view(B, n, D)
+    _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
+              C.c_uint64(saved["seed"]), _p(dout), st)
+    # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
+    weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code, work_pool=pool)
+    colsum(dout, B * n, D, D, dt_code, grads["bo"], pool)
+    dmerged = pool(B * n * D, tdtype).view(B, n, D)
+    gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
+    dqkv = nystrom_core_backward(dmerged, saved["merged"], saved["qkv"], saved["core"], geo, prm["wconv"],
+                                 tdtype, dt_code, pool, grads["wconv"], DH ** -0.5)
+    # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
+    weight_grad(dqkv, saved["xn"], grads["wqkv"], 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
+                work_pool=pool)
+    dxn = pool(B * n * D, tdtype).view(B, n, D)
+    gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
+    # LayerNorm backward, accumulated into dH (residual branch already there)
+    rpb = 64
+    work = pool(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4)
+    _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
+              _p(saved["rstd"]), B * S, D, S, n, pad, rpb, _p(dH), _p(work), _p(grads["norm_w"]),
+              _p(grads["norm_b"]), st)
+
+
+# ----------------------------------------------------------------------------- whole model
+class TransMILEngine:
+    """Fused TransMIL forward / backward for the ``in_features -> Linear+GELU`` branch
+    (code/models/TransMIL.py:128-133), heads = 8, dim_head = 64, 256 landmarks."""
+
+    def __init__(self, dtype: torch.dtype = torch.bfloat16):
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("compute dtype must be torch.bfloat16 or torch.float32")
+        self.tdtype = dtype
+        self.dt_code = BF16 if dtype == torch.bfloat16 else F32
+        _lib.lib()
+
+    def _cast(self, w, pool):
+        if self.dt_code == F32:
+            return w.contiguous()
+        out = pool(w.numel(), self.tdtype)
+        _lib.call("tm_cast_f32", self.dt_code, _p(w.contiguous()), _p(out), w.numel(), _stream())
+        return out.view(w.shape)
+
+    def prepare(self, params, pool):
+        """fp32 master parameters -> the per-call operand set (T copies of GEMM weights)."""
+        D = params["norm.weight"].shape[0]
+        p = {"D": D}
+        p["w1"] = self._cast(params["_fc1.0.weight"], pool)
+        p["b1"] = params["_fc1.0.bias"]
+        p["cls"] = params["cls_token"]
+        for li in (1, 2):
+            pre = f"layer{li}."
+            p[li] = {
+                "norm_w": params[pre + "norm.weight"], "norm_b": params[pre + "norm.bias"],
+                "wqkv": self._cast(params[pre + "attn.to_qkv.weight"], pool),
+                "wo": self._cast(params[pre + "attn.to_out.0.weight"], pool),
+                "bo": params[pre + "attn.to_out.0.bias"],
+                "wconv": params[pre + "attn.res_conv.weight"].contiguous(),
+            }
+        wfold = pool(D * 49)
+        bfold = pool(D)
+        _lib.call("tm_ppeg_fold", _p(params["pos_layer.proj.weight"]), _p(params["pos_layer.proj.bias"]),
+                  _p(params["pos_layer.proj1.weight"]), _p(params["pos_layer.proj1.bias"]),
+                  _p(params["pos_layer.proj2.weight"]), _p(params["pos_layer.proj2.bias"]), D, _p(wfold),
+                  _p(bfold), _stream())
+        p["wfold"], p["bfold"] = wfold, bfold
+        p["norm_w"], p["norm_b"] = params["norm.weight"], params["norm.bias"]
+        p["fc_w"], p["fc_b"] = params["_fc.weight"], params["_fc.bias"]
+        return p
+
+    def forward(self, x, params, drop_p=0.0, seeds=(0, 0)):
+        """x [B, N, F] fp32 (on the GPU) -> logits [B, C] fp32 and the saved context."""
+        dev = x.device
+        pool = Pool(dev)
+        B, N, F = x.shape
+        D = params["norm.weight"].shape[0]
+        heads = params["layer1.attn.res_conv.weight"].shape[0]
+        if D != heads * DH:
+            raise NotImplementedError(f"HIP NystromAttention needs dim_head == 64 (D={D}, heads={heads})")
+        geo = Geometry(B, N, F, D, heads)
+        prm = self.prepare(params, pool)
+        st = _stream()
+        xt = self._cast(x.reshape(B * N, F), pool) if self.dt_code == BF16 else x.reshape(B * N, F).contiguous()
+        # _fc1: Linear + GELU, grid pad (duplicate the first `add` rows) and class token
+        H0 = pool(B * geo.S * D).view(B * geo.S, D)
+        pre = pool(B * N * D).view(B * N, D)   # fp32 pre-activation for the GELU backward
+        gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
+             bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
+        _lib.call("tm_put_cls", _p(prm["cls"]), B, geo.S, D, _p(H0), st)
+        H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0])
+        H2 = pool(B * geo.S * D).view(B * geo.S, D)
+        _lib.call("tm_ppeg_fwd", _p(H1), B, geo.G, D, _p(prm["wfold"]), _p(prm["bfold"]), _p(H2), st)
+        H3, s2 = translayer_forward(H2, geo, prm[2], self.tdtype, self.dt_code, pool, drop_p, seeds[1])
+        Ccls = prm["fc_w"].shape[0]
+        logits = torch.empty(B, Ccls, dtype=torch.float32, device=dev)
+        xhat = pool(B * D)
+        hrstd = pool(B)
+        _lib.call("tm_head_fwd", _p(H3), B, geo.S, D, _p(prm["norm_w"]), _p(prm["norm_b"]), C.c_float(LN_EPS),
+                  _p(prm["fc_w"]), _p(prm["fc_b"]), Ccls, _p(logits), _p(xhat), _p(hrstd), st)
+        ctx = dict(geo=geo, prm=prm, xt=xt, pre=pre, H0=H0, H1=H1, H2=H2, s1=s1, s2=s2, xhat=xhat, hrstd=hrstd)
+        return logits, ctx
+
+    def backward(self, dlogits, ctx, params):
+        """Returns a dict name -> fp32 gradient with the reference parameter names."""
+        geo, prm = ctx["geo"], ctx["prm"]
+        dev = dlogits.device
+        pool = Pool(dev)
+        B, N, F, D, S = geo.B, geo.N, geo.F, geo.D, geo.S
+        st = _stream()
+        g = {name: torch.empty_like(p, dtype=torch.float32) for name, p in params.items()}
+        Ccls = prm["fc_w"].shape[0]
+        dH = torch.zeros(B * S, D, dtype=torch.float32, device=dev)
+        _lib.call("tm_head_bwd", _p(dlogits.contiguous()), B, Ccls, S, D, _p(ctx["xhat"]), _p(ctx["hrstd"]),
+                  _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g["_fc.weight"]), _p(g["_fc.bias"]),
+                  _p(g["norm.weight"]), _p(g["norm.bias"]), _p(dH), st)
+        for li, Hin, saved in ((2, ctx["H2"], ctx["s2"]), (1, ctx["H0"], ctx["s1"])):
+            pre = f"layer{li}."
+            gl = {"wo": g[pre + "attn.to_out.0.weight"], "bo": g[pre + "attn.to_out.0.bias"],
+                  "wqkv": g[pre + "attn.to_qkv.weight"], "wconv": g[pre + "attn.res_conv.weight"],
+                  "norm_w": g[pre + "norm.weight"], "norm_b": g[pre + "norm.bias"]}
+            translayer_backward(dH, Hin, saved, geo, prm[li], gl, self.tdtype, self.dt_code, pool)
+            if li == 2:
+                dH1 = pool(B * S * D).view(B * S, D)
+                work = pool(_lib.query("tm_ppeg_bwd_workspace", B, geo.G, D) // 4)
+                dwsum = pool(D * 50)
+                _lib.call("tm_ppeg_bwd", _p(ctx["H1"]), _p(dH), B, geo.G, D, _p(prm["wfold"]), _p(dH1), _p(work),
+                          _p(dwsum), _p(g["pos_layer.proj.weight"]), _p(g["pos_layer.proj.bias"]),
+                          _p(g["pos_layer.proj1.weight"]), _p(g["pos_layer.proj1.bias"]),
+                          _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), st)
+                dH = dH1
+        # _fc1 backward (GELU + grid-pad fold) and the class token
+        dpre = pool(B * N * D, self.tdtype).view(B * N, D)
+        _lib.call("tm_fc1_gelu_bwd", self.dt_code, _p(dH), _p(ctx["pre"]), B, N, S, geo.add, D, _p(dpre),
+                  _p(g["cls_token"]), st)
+        weight_grad(dpre, ctx["xt"], g["_fc1.0.weight"], D, F, B * N, ldy=D, ldx=F, dtype=self.dt_code,
+                    work_pool=pool)
+        colsum(dpre, B * N, D, D, self.dt_code, g["_fc1.0.bias"], pool)
+        return g
+
+
+# ----------------------------------------------------------------------------- standalone NystromAttention
+class NystromEngine:
+    """``nystrom_attention.NystromAttention.forward(x)`` (no mask) on the HIP kernels:
+    front pad, to_qkv, core, to_out (+ Dropout), keep the last n rows (App. A eq. 1-10)."""
+
+    def __init__(self, dtype: torch.dtype = torch.bfloat16):
+        self.tdtype = dtype
+        self.dt_code = BF16 if dtype == torch.bfloat16 else F32
+        _lib.lib()
+
+    def _cast(self, w, pool):
+        if self.dt_code == F32:
+            return w.contiguous()
+        out = pool(w.numel(), self.tdtype)
+        _lib.call("tm_cast_f32", self.dt_code, _p(w.contiguous()), _p(out), w.numel(), _stream())
+        return out.view(w.shape)
+
+    def forward(self, x, wqkv, wo, bo, wconv, heads, drop_p=0.0, seed=0):
+        B, S, D = x.shape
+        pool = Pool(x.device)
+        geo = Geometry(B, max(S - 1, 1), D, D, heads)
+        geo.S = S
+        geo.n = ((S + NL - 1) // NL) * NL
+        geo.pad = geo.n - S
+        geo.l = geo.n // NL
+        n, pad = geo.n, geo.pad
+        xc = x.reshape(B * S, D).contiguous()
+        xp = pool(B * n * D, self.tdtype).view(B, n, D)
+        _lib.call("tm_pad_rows", self.dt_code, _p(xc), B, S, n, pad, D, _p(xp), _stream())
+        wqkv_t, wo_t = self._cast(wqkv, pool), self._cast(wo, pool)
+        qkv = pool(3 * geo.nbh * n * DH, self.tdtype).view(3, geo.nbh, n, DH)
+        gemm(xp, wqkv_t, qkv, B * n, 3 * D, D, lda=D, ldb=D, ldc=0, dtype=self.dt_code,
+             qkv=(B, heads, DH, n, DH ** -0.5))
+        merged, state = nystrom_core_forward(qkv, geo, wconv.contiguous(), self.tdtype, self.dt_code, pool)
+        out = torch.empty(B, S, D, dtype=torch.float32, device=x.device)
+        gemm(merged, wo_t, out, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=self.dt_code, c_dtype=F32,
+             bias=bo, drop_p=drop_p, seed=seed, rowmap=(n, pad, S, 0, 0, 0))
+        ctx = dict(geo=geo, xp=xp, qkv=qkv, merged=merged, core=state, wqkv_t=wqkv_t, wo_t=wo_t,
+                   wconv=wconv.contiguous(), drop_p=drop_p, seed=seed)
+        return out, ctx
+
+    def backward(self, dout, ctx):
+        geo = ctx["geo"]
+        B, S, D, n, pad = geo.B, geo.S, geo.D, geo.n, geo.pad
+        pool = Pool(dout.device)
+        st = _stream()
+        dpad = pool(B * n * D, self.tdtype).view(B, n, D)
+        _lib.call("tm_dropout_bwd_pad", self.dt_code, _p(dout.contiguous()), B, S, n, pad, D,
+                  C.c_float(ctx["drop_p"]), C.c_uint64(ctx["seed"]), _p(dpad), st)
+        dwo = torch.empty(D, D, dtype=torch.float32, device=dout.device)
+        dbo = torch.empty(D, dtype=torch.float32, device=dout.device)
+        weight_grad(dpad, ctx["merged"], dwo, D, D, B * n, ldy=D, ldx=D, dtype=self.dt_code, work_pool=pool)
+        colsum(dpad, B * n, D, D, self.dt_code, dbo, pool)
+        dmerged = pool(B * n * D, self.tdtype).view(B, n, D)
+        gemm(dpad, ctx["wo_t"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=self.dt_code)
+        dwconv = torch.empty_like(ctx["wconv"], dtype=torch.float32)
+        dqkv = nystrom_core_backward(dmerged, ctx["merged"], ctx["qkv"], ctx["core"], geo, ctx["wconv"],
+                                     self.tdtype, self.dt_code, pool, dwconv, DH ** -0.5)
+        dwqkv = torch.empty(3 * D, D, dtype=torch.float32, device=dout.device)
+        weight_grad(dqkv, ctx["xp"], dwqkv, 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=self.dt_code, work_pool=pool)
+        dx = torch.empty(B, S, D, dtype=torch.float32, device=dout.device)
+        gemm(dqkv, ctx["wqkv_t"], dx, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=self.dt_code,
+             c_dtype=F32, rowmap=(n, pad, S, 0, 0, 0))
+        return dx, dwqkv, dwo, dbo, dwconv

@@ -1,0 +1,148 @@
+"""Drop-in ``models/TransMIL.py`` on the MI355X HIP kernels.
+
+Same classes, constructor signatures, ``forward(x, return_attn=False)``
+contract and state_dict keys as ``code/models/TransMIL.py`` (TransLayer :19-57,
+PPEG :60-75, TransMIL :78-211), so ``ModelInterface.load_model`` /
+``instancialize`` (code/models/model_interface.py:1256-1293) and Lightning
+checkpoints (``model.``-prefixed keys) work unchanged.
+
+``TransMIL.forward`` runs the whole model -- _fc1 + GELU, grid padding, class
+token, TransLayer x2 (LayerNorm, NystromAttention, residual), PPEG and the
+class-token head -- as one autograd node whose forward and backward are the
+hand-written HIP kernels of ``libtransmil_hip.so`` (``engine.TransMILEngine``).
+``compute_dtype`` selects bf16 MFMA operands (default, the benchmark mode) or
+fp32 (the parity mode: f32 MFMA, results within fp32 rounding of the CPU
+oracle).  There is no CPU / eager fallback: a CPU tensor raises.
+
+Supported _fc1 branch: ``in_features`` not in {2048, 1024, 768}, i.e.
+``Linear(in, out) + GELU`` (:128-133) -- the branch every d=512 config uses.
+``dim_head`` is fixed at 64 by TransLayer (dim // 8 with dim = 512).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ..engine import TransMILEngine, NystromEngine
+from ..nystrom_attention import NystromAttention, attention_matrix
+from .. import ops
+
+
+class TransLayer(nn.Module):
+    """``x + NystromAttention(LayerNorm(x))`` (code/models/TransMIL.py:19-57)."""
+
+    def __init__(self, norm_layer=nn.LayerNorm, dim=512):
+        super().__init__()
+        self.norm = norm_layer(dim)
+        heads = 8
+        self.attn = NystromAttention(dim=dim, dim_head=dim // heads, heads=heads, num_landmarks=dim // 2,
+                                     pinv_iterations=6, residual=True, dropout=0.7)
+
+    def forward(self, x):
+        out, attn = self.attn(ops.layer_norm(self.norm, x), return_attn=True)
+        return x + out, attn
+
+
+class PPEG(nn.Module):
+    """7x7 + identity + 5x5 + 3x3 depthwise positional encoding (code/models/TransMIL.py:60-75)."""
+
+    def __init__(self, dim=512):
+        super().__init__()
+        self.proj = nn.Conv2d(dim, dim, 7, 1, 7 // 2, groups=dim)
+        self.proj1 = nn.Conv2d(dim, dim, 5, 1, 5 // 2, groups=dim)
+        self.proj2 = nn.Conv2d(dim, dim, 3, 1, 3 // 2, groups=dim)
+
+    def forward(self, x, H, W):
+        if H != W:
+            raise NotImplementedError("PPEG on the HIP path needs a square grid (TransMIL always builds one)")
+        return ops.ppeg(self, x, H)
+
+
+class _TransMILFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, engine, names, drop_p, seeds, holder, x, *params):
+        prm = dict(zip(names, params))
+        logits, c = engine.forward(x, prm, drop_p, seeds)
+        ctx.engine, ctx.c, ctx.names, ctx.prm = engine, c, names, prm
+        if holder is not None:
+            holder["ctx"] = c
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        g = ctx.engine.backward(dlogits.float().contiguous(), ctx.c, ctx.prm)
+        ctx.c = None
+        return (None, None, None, None, None, None) + tuple(g[n] for n in ctx.names)
+
+
+class TransMIL(nn.Module):
+    def __init__(self, n_classes, in_features, out_features=512):
+        super().__init__()
+        norm_layer = nn.LayerNorm
+        self.pos_layer = PPEG(dim=out_features)
+        if in_features in (2048, 1024, 768):
+            self._fc1 = _reference_fc1(in_features, out_features, norm_layer)
+        else:
+            self._fc1 = nn.Sequential(nn.Linear(in_features, out_features), nn.GELU())
+        self.cls_token = nn.Parameter(torch.randn(1, 1, out_features))
+        self.n_classes = n_classes
+        self.in_features = in_features
+        self.layer1 = TransLayer(norm_layer=norm_layer, dim=out_features)
+        self.layer2 = TransLayer(norm_layer=norm_layer, dim=out_features)
+        self.norm = norm_layer(out_features)
+        self._fc = nn.Linear(out_features, self.n_classes)
+        self.compute_dtype = torch.bfloat16
+
+    def set_compute_dtype(self, dtype):
+        """torch.bfloat16 (bench) or torch.float32 (parity); propagates to submodules."""
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("compute dtype must be torch.bfloat16 or torch.float32")
+        self.compute_dtype = dtype
+        for m in self.modules():
+            if isinstance(m, NystromAttention):
+                m.compute_dtype = dtype
+        return self
+
+    def forward(self, x, return_attn=False):
+        if x.dim() > 3:                        # :170-173
+            x = x.squeeze(0)
+        elif x.dim() == 2:
+            x = x.unsqueeze(0)
+        if not x.is_cuda:
+            raise RuntimeError("TransMIL (HIP) needs a GPU tensor: there is no CPU path")
+        if len(self._fc1) != 2:
+            raise NotImplementedError(
+                f"in_features={self.in_features}: only the Linear+GELU _fc1 branch "
+                "(code/models/TransMIL.py:128-133) runs on the HIP path")
+        x = x.float().contiguous()             # :174
+        names = tuple(n for n, _ in self.named_parameters())
+        params = tuple(p for _, p in self.named_parameters())
+        drop_p = self.layer1.attn.to_out[1].p if self.training else 0.0
+        seeds = tuple(int(s) for s in torch.randint(0, 2 ** 62, (2,))) if drop_p > 0 else (0, 0)
+        holder = {} if return_attn else None
+        engine = TransMILEngine(self.compute_dtype)
+        logits = _TransMILFn.apply(engine, names, drop_p, seeds, holder, x, *params)
+        if return_attn:
+            c = holder["ctx"]
+            S = c["geo"].S
+            padding = 256 - S % 256 if S % 256 else 0      # :190-193
+            attn2 = attention_matrix(c["s2"]["qkv"], c["s2"]["core"], c["geo"].heads)
+            return logits, (attn2, padding)
+        return logits
+
+
+def _reference_fc1(in_features, out_features, norm_layer):
+    """Parameter layout of the other _fc1 branches (:100-126), kept so their
+    checkpoints load; their forward is not on the HIP path yet."""
+    if in_features == 2048:
+        return nn.Sequential(nn.Linear(in_features, in_features // 2), nn.GELU(), norm_layer(in_features // 2),
+                             nn.Linear(in_features // 2, out_features), nn.GELU())
+    if in_features == 1024:
+        return nn.Sequential(nn.Linear(in_features, in_features), nn.GELU(), nn.Dropout(p=0.2),
+                             norm_layer(out_features), nn.Linear(in_features, out_features), nn.GELU(),
+                             nn.Dropout(p=0.6), norm_layer(out_features))
+    return nn.Sequential(nn.Linear(in_features, in_features), nn.GELU(), nn.Dropout(p=0.6),
+                         norm_layer(in_features), nn.Linear(in_features, out_features), nn.GELU(),
+                         nn.Dropout(p=0.6), norm_layer(out_features))
