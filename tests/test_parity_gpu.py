@@ -26,13 +26,18 @@ def _pair(ncls, feat=512, seed=2021, dtype=torch.float32):
     return ref, ours
 
 
-def _ref_forward_backward(ref, x, label, ncls):
+def _ref64(ref, x, **kw):
+    """Run the oracle in fp64 (its `x.float()` at :174 is bypassed)."""
     orig = torch.Tensor.float
-    torch.Tensor.float = lambda self, *a, **k: self  # keep fp64 through `x.float()` (:174)
+    torch.Tensor.float = lambda self, *a, **k: self
     try:
-        logits = ref(x.double())
+        return ref(x.double(), **kw)
     finally:
         torch.Tensor.float = orig
+
+
+def _ref_forward_backward(ref, x, label, ncls):
+    logits = _ref64(ref, x)
     y = torch.tensor([label] * x.shape[0])
     loss = torch.nn.CrossEntropyLoss()(logits, torch.nn.functional.one_hot(y, ncls).double())
     loss.backward()
@@ -82,7 +87,7 @@ def test_bf16_mode_close_to_oracle(N):
     ref, ours = _pair(2, dtype=torch.bfloat16)
     x = torch.from_numpy(bag_input(N, 512, 5 + N))
     with torch.no_grad():
-        lr = ref(x.double())
+        lr = _ref64(ref, x)
         lo = ours(x.to(DEV)).cpu()
     np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=5e-2)
 
@@ -92,7 +97,7 @@ def test_return_attn_contract():
     ref, ours = _pair(2)
     x = torch.from_numpy(bag_input(200, 512, 9))
     with torch.no_grad():
-        lr, (ar, pr) = ref(x.double(), return_attn=True)
+        lr, (ar, pr) = _ref64(ref, x, return_attn=True)
         lo, (ao, po) = ours(x.to(DEV), return_attn=True)
     assert po == pr and ao.shape == ar.shape
     H = 200
