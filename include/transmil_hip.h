@@ -60,6 +60,9 @@ typedef struct tm_gemm_args {
    * C[((which*nbags + bag)*nh + head)*seq + t][d]; q (which==0) scaled by qscale */
   int nbags, nh, dh, seq;
   float qscale;
+  /* dropout seed read from device memory when non-NULL: seed = *seed_ptr * 0x9E3779B97F4A7C15 + seed
+   * (keeps a hipGraph replay drawing a fresh mask every step) */
+  const uint64_t* seed_ptr;
 } tm_gemm_args;
 
 int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* args, void* stream);
@@ -100,8 +103,8 @@ long long tm_nys_a3_workspace(int nbh, int n);
 /* W = softmax(ql k^T) v  [B*h,256,64] fp32, lse3 [B*h,256] */
 int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
                   float* w, float* lse3, void* stream);
-/* merged[b][t][head*64+d] = softmax(q kl^T) y + conv33(v); lse1 [B*h, n] */
-int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const float* kl, const float* y,
+/* merged[b][t][head*64+d] = softmax(q kl^T) y + conv33(v); lse1 [B*h, n]; kl_t, y_t: T copies */
+int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void* kl_t, const void* y_t,
                   const float* wconv, int nbh, int nh, int n, void* merged, float* lse1, void* stream);
 int tm_nys_rowdot_cast(int dtype, const float* dw, const float* w, int rows, float* dd, void* dw_t, void* stream);
 int tm_cast_f32(int dtype, const float* x, void* y, long long count, void* stream);
@@ -151,7 +154,7 @@ int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const floa
 /* ---- glue (glue.hip) -- code/models/TransMIL.py:177-186 ------------------ */
 int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream);
 int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int pad, int D, float p,
-                       uint64_t seed, void* out, void* stream);
+                       uint64_t seed, const uint64_t* seed_ptr, void* out, void* stream);
 /* NystromAttention eq. 1 for a raw input: [B*S, D] fp32 -> front-padded [B, n_pad, D] T */
 int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, int pad, int D, void* y, void* stream);
 int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,

@@ -1,0 +1,184 @@
+"""Per-kernel timing of the HIP entry points with HIP events (one process, interleaved rounds).
+
+    python scripts/microbench.py [--n 8192] [--reps 50]
+
+Each case is run `reps` times between two events on the current stream; the
+median of 5 rounds is printed.  Used to A/B kernel variants on the GPU box.
+"""
+import argparse
+import ctypes as C
+import math
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from transmil_deepgraft_amd import _lib  # noqa: E402
+from transmil_deepgraft_amd import engine as E  # noqa: E402
+from transmil_deepgraft_amd._lib import BF16, F32  # noqa: E402
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(5):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        out.append(s.elapsed_time(e) / reps * 1e3)
+    return statistics.median(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    dev = "cuda"
+    N = args.n
+    G = math.ceil(math.sqrt(N))
+    S = G * G + 1
+    n = (S + 255) // 256 * 256
+    nbh = 8
+    bf = torch.bfloat16
+    res = {}
+
+    def case(name, fn, flops=None, byts=None):
+        if args.only and args.only not in name:
+            return
+        us = timeit(fn, args.reps)
+        extra = ""
+        if flops:
+            extra += f" {flops / us / 1e6:8.1f} TF/s"
+        if byts:
+            extra += f" {byts / us / 1e3:8.1f} GB/s"
+        res[name] = us
+        print(f"{name:40s} {us:9.2f} us{extra}", flush=True)
+
+    st = E._stream
+    # ---------------- bmm (pinv building block) ----------------
+    X = torch.softmax(torch.randn(nbh, 256, 256, device=dev), -1)
+    Z = torch.randn(nbh, 256, 256, device=dev) * 1e-2
+    P = torch.empty_like(Z)
+    W = torch.randn(nbh, 256, 64, device=dev)
+    Y = torch.empty(nbh, 256, 64, device=dev)
+    f = 2 * nbh * 256 ** 3
+    case("bmm NN 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh), f)
+    case("bmm NT 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 1, P, 256, 256, 256)], nbh), f)
+    case("bmm TN 256^3 x8", lambda: E.bmm([E.bmm_job(X, 1, Z, 0, P, 256, 256, 256)], nbh), f)
+    case("bmm 2-job 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
+                                              E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh), 2 * f)
+    case("bmm Y=ZW 256x64x256 x8", lambda: E.bmm([E.bmm_job(Z, 0, W, 0, Y, 256, 64, 256)], nbh), f // 4)
+    case("torch bmm fp32 256^3 x8", lambda: torch.bmm(X, Z, out=P), f)
+    saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=dev)
+    case("pinv_fwd (26 launches)", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, E._p(saved), st()), 24 * f)
+    # ---------------- GEMMs ----------------
+    pool = E.Pool(dev)
+    xn = torch.randn(n, 512, device=dev).to(bf)
+    wqkv = (torch.randn(1536, 512, device=dev) * 0.05).to(bf)
+    qkv = torch.empty(3, nbh, n, 64, device=dev, dtype=bf)
+    case("gemm qkv (NT, scatter)", lambda: E.gemm(xn, wqkv, qkv, n, 1536, 512, lda=512, ldb=512, ldc=0, dtype=BF16,
+                                                  qkv=(1, 8, 64, n, 0.125)), 2 * n * 1536 * 512)
+    slabq = torch.empty(n, 1536, device=dev)
+
+    def plain_gemm(K_):
+        g = _lib.GemmArgs()
+        g.M, g.N, g.K = n, 1536, K_
+        g.lda, g.ldb, g.ldc = 512, 512, 1536
+        g.ab_dtype, g.c_dtype = BF16, F32
+        g.splits, g.k_per_split = 1, 512
+        g.mode = _lib.EPI_SPLITK
+        g.alpha = 1.0
+        _lib.call("tm_gemm", E._p(xn), E._p(wqkv), E._p(slabq), C.byref(g), st())
+    case("gemm qkv shape, plain fp32 store", lambda: plain_gemm(512), 2 * n * 1536 * 512)
+    case("gemm qkv shape, K=64 plain store", lambda: plain_gemm(64), 2 * n * 1536 * 64)
+    outb = torch.empty(n, 1536, device=dev, dtype=bf)
+    case("torch.matmul bf16 (hipBLASLt) qkv", lambda: torch.matmul(xn, wqkv.t(), out=outb), 2 * n * 1536 * 512)
+    H = torch.randn(S, 512, device=dev)
+    Ho = torch.empty_like(H)
+    wo = (torch.randn(512, 512, device=dev) * 0.05).to(bf)
+    bo = torch.randn(512, device=dev)
+    case("gemm to_out (NT, drop+resid)", lambda: E.gemm(xn, wo, Ho, n, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16,
+                                                        c_dtype=F32, bias=bo, drop_p=0.7, seed=3, resid=H,
+                                                        rowmap=(n, n - S, S, 0, 0, 0)), 2 * n * 512 * 512)
+    dq = torch.randn(n, 1536, device=dev).to(bf)
+    dx = torch.empty(n, 512, device=dev, dtype=bf)
+    case("gemm dxn (B k-strided)", lambda: E.gemm(dq, wqkv, dx, n, 512, 1536, lda=1536, ldb=512, ldc=512, b_kn=1,
+                                                  dtype=BF16), 2 * n * 1536 * 512)
+    dW = torch.empty(1536, 512, device=dev)
+    case("wgrad dWqkv (split-K + reduce)", lambda: E.weight_grad(dq, xn, dW, 1536, 512, n, ldy=1536, ldx=512,
+                                                                 dtype=BF16, work_pool=pool), 2 * n * 1536 * 512)
+    slab = torch.randn(8, 1536 * 512, device=dev)
+    case("splitk_reduce 8 x 786K", lambda: _lib.call("tm_splitk_reduce", E._p(slab), E._p(dW), 8, 1536 * 512,
+                                                     C.c_float(1.0), 0, st()), byts=9 * 1536 * 512 * 4)
+    slab2 = torch.randn(33, 512, device=dev)
+    ob = torch.empty(512, device=dev)
+    case("splitk_reduce 33 x 512", lambda: _lib.call("tm_splitk_reduce", E._p(slab2), E._p(ob), 33, 512,
+                                                     C.c_float(1.0), 0, st()))
+    # ---------------- NystromAttention core ----------------
+    q = (torch.randn(nbh, n, 64, device=dev) * 0.3).to(bf)
+    k = (torch.randn(nbh, n, 64, device=dev) * 0.3).to(bf)
+    v = torch.randn(nbh, n, 64, device=dev).to(bf)
+    ql = torch.randn(nbh, 256, 64, device=dev) * 0.3
+    kl = torch.randn(nbh, 256, 64, device=dev) * 0.3
+    ql_t, kl_t = ql.to(bf), kl.to(bf)
+    qkv3 = torch.stack([q, k, v])
+    case("landmarks", lambda: _lib.call("tm_nys_landmarks", BF16, E._p(q), E._p(k), nbh, n, E._p(ql), E._p(kl),
+                                        E._p(ql_t), E._p(kl_t), st()), byts=2 * nbh * n * 64 * 2)
+    a3w = torch.empty(_lib.query("tm_nys_a3_workspace", nbh, n) // 4, device=dev)
+    w_ = torch.empty(nbh, 256, 64, device=dev)
+    lse3 = torch.empty(nbh, 256, device=dev)
+    case("a3_fwd (+combine)", lambda: _lib.call("tm_nys_a3_fwd", BF16, E._p(ql), E._p(k), E._p(v), nbh, n, E._p(a3w),
+                                                E._p(w_), E._p(lse3), st()), 4 * nbh * 256 * n * 64)
+    y_t = torch.randn(nbh, 256, 64, device=dev).to(bf)
+    wconv = torch.randn(8, 33, device=dev) * 0.1
+    merged = torch.empty(1, n, 512, device=dev, dtype=bf)
+    lse1 = torch.empty(nbh, n, device=dev)
+    case("a1_fwd", lambda: _lib.call("tm_nys_a1_fwd", BF16, E._p(q), E._p(v), E._p(kl_t), E._p(y_t), E._p(wconv),
+                                     nbh, 8, n, E._p(merged), E._p(lse1), st()),
+         4 * nbh * n * 256 * 64, 3 * n * 512 * 2)
+    dmerged = torch.randn(1, n, 512, device=dev).to(bf)
+    dv = torch.empty(nbh, n, 64, device=dev)
+    d1 = torch.empty(nbh, n, device=dev)
+    cw = torch.empty(_lib.query("tm_nys_conv_bwd_workspace", 1, 8, n) // 4, device=dev)
+    dwc = torch.empty(8, 33, device=dev)
+    case("conv_bwd", lambda: _lib.call("tm_nys_conv_bwd", BF16, E._p(dmerged), E._p(merged), E._p(v), E._p(wconv),
+                                       nbh, 8, n, E._p(dv), E._p(d1), E._p(cw), E._p(dwc), st()),
+         byts=4 * n * 512 * 2)
+    dqf = torch.empty(nbh, n, 64, device=dev)
+    a1w = torch.empty(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, 256) // 4, device=dev)
+    dkl = torch.empty(nbh, 256, 64, device=dev)
+    dy = torch.empty(nbh, 256, 64, device=dev)
+    lse1.uniform_(3, 4)
+    case("a1_bwd (+2 reduces)", lambda: _lib.call("tm_nys_a1_bwd", BF16, E._p(q), E._p(dmerged), E._p(kl_t),
+                                                  E._p(y_t), E._p(lse1), E._p(d1), nbh, 8, n, 256, E._p(dqf),
+                                                  E._p(a1w), E._p(dkl), E._p(dy), 0, st()), 10 * nbh * n * 256 * 64)
+    a3bw = torch.empty(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4, device=dev)
+    d3 = torch.randn(nbh, 256, device=dev)
+    dw_t = torch.randn(nbh, 256, 64, device=dev).to(bf)
+    dk = torch.empty(nbh, n, 64, device=dev)
+    dql = torch.zeros(nbh, 256, 64, device=dev)
+    lse3.uniform_(8, 9)
+    case("a3_bwd (+reduce)", lambda: _lib.call("tm_nys_a3_bwd", BF16, E._p(ql_t), E._p(dw_t), E._p(k), E._p(v),
+                                               E._p(lse3), E._p(d3), nbh, 8, n, E._p(dk), E._p(dv), E._p(a3bw),
+                                               E._p(dql), st()), 10 * nbh * n * 256 * 64)
+    # ---------------- PPEG ----------------
+    x = torch.randn(1, S, 512, device=dev)
+    wf = torch.randn(512 * 49, device=dev) * 0.1
+    bfo = torch.randn(512, device=dev)
+    yp = torch.empty_like(x)
+    case("ppeg_fwd", lambda: _lib.call("tm_ppeg_fwd", E._p(x), 1, G, 512, E._p(wf), E._p(bfo), E._p(yp), st()),
+         byts=2 * S * 512 * 4)
+
+
+if __name__ == "__main__":
+    main()

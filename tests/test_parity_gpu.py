@@ -107,17 +107,82 @@ def test_return_attn_contract():
 
 
 def test_train_mode_dropout_is_applied_and_reproducible():
+    """The mask stream is a device-side counter (hipGraph-safe): restoring the
+    counter reproduces the mask; every forward advances it; eval mode has none."""
     _, ours = _pair(2)
     ours.train()
     x = torch.from_numpy(bag_input(500, 512, 3)).to(DEV)
-    torch.manual_seed(5)
+    start = ours._dropout_counter.clone()
     a = ours(x).detach()
-    torch.manual_seed(5)
-    b = ours(x).detach()
-    torch.manual_seed(6)
     c = ours(x).detach()
+    ours._dropout_counter.copy_(start)
+    b = ours(x).detach()
     ours.eval()
     with torch.no_grad():
         e = ours(x)
     assert torch.equal(a, b)
     assert not torch.equal(a, c) and not torch.equal(a, e)
+
+
+def _mix32(h):
+    h = h.astype(np.uint32)
+    h ^= h >> np.uint32(16)
+    h = (h * np.uint32(0x85EBCA6B)).astype(np.uint32)
+    h ^= h >> np.uint32(13)
+    h = (h * np.uint32(0xC2B2AE35)).astype(np.uint32)
+    h ^= h >> np.uint32(16)
+    return h
+
+
+def dropout_keep(seed_dev_value, layer_seed, rows, cols, p):
+    """Host restatement of common.h dropout_u01 / effective_seed (the kernels' hash)."""
+    seed = (int(seed_dev_value) * 0x9E3779B97F4A7C15 + int(layer_seed)) & (2 ** 64 - 1)
+    lo, hi = np.uint32(seed & 0xFFFFFFFF), np.uint32(seed >> 32)
+    r = np.arange(rows, dtype=np.uint32)[:, None]
+    c = np.arange(cols, dtype=np.uint32)[None, :]
+    with np.errstate(over="ignore"):
+        h = _mix32(lo ^ _mix32((r * np.uint32(0x9E3779B1) + hi).astype(np.uint32)))
+        h = _mix32(h ^ (c * np.uint32(0x7FEB352D)).astype(np.uint32))
+    u = (h >> np.uint32(8)).astype(np.float64) / 16777216.0
+    return u >= p
+
+
+def test_train_mode_dropout_matches_oracle_with_same_mask():
+    """Train mode (dropout 0.7 on to_out): the forward mask and the mask the
+    backward re-derives equal the host restatement of the kernel hash; logits and
+    every gradient match the oracle with that mask applied (fp32 parity mode)."""
+    import math
+    from transmil_deepgraft_amd.engine import TransMILEngine
+    ref, ours = _pair(2)
+    ours.train()
+    N, B = 300, 1
+    G = math.ceil(math.sqrt(N))
+    S = G * G + 1
+    npad = (S + 255) // 256 * 256
+    pad = npad - S
+    seed_val = int(ours._dropout_counter.item()) + 1
+    layer_seeds = TransMILEngine.forward.__defaults__[1]
+    x = torch.from_numpy(bag_input(N, 512, 21, B))
+    lo, go = _ours_forward_backward(ours, x, 1, 2)
+    hooks = []
+    for li, layer in ((0, ref.layer1), (1, ref.layer2)):
+        keep = dropout_keep(seed_val, layer_seeds[li], B * S, 512, 0.7).reshape(B, S, 512)
+        m = torch.from_numpy(keep.astype(np.float64) / 0.3)
+
+        def hook(_mod, _inp, out, m=m):
+            out = out.clone()
+            out[:, pad:, :] = out[:, pad:, :] * m
+            return out
+        hooks.append(layer.attn.to_out[0].register_forward_hook(hook))
+    try:
+        lr, gr = _ref_forward_backward(ref, x, 1, 2)
+    finally:
+        for h in hooks:
+            h.remove()
+    np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=1e-4)
+    bad = []
+    for name, g in gr.items():
+        err = ((go[name].double() - g).abs().max() / g.abs().max().clamp_min(1e-12)).item()
+        if err > 2e-3:
+            bad.append((name, err))
+    assert not bad, bad

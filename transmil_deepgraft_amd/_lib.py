@@ -30,7 +30,7 @@ class GemmArgs(C.Structure):
                 ("drop_p", Fl), ("drop_scale", Fl), ("seed", U64), ("resid", P),
                 ("accumulate", I), ("grp_in", I), ("skip", I), ("grp_out", I),
                 ("out_off", I), ("dup_n", I), ("dup_off", I), ("nbags", I), ("nh", I),
-                ("dh", I), ("seq", I), ("qscale", Fl)]
+                ("dh", I), ("seq", I), ("qscale", Fl), ("seed_ptr", P)]
 
 
 class BmmJob(C.Structure):
@@ -78,7 +78,7 @@ _SIGS = {
     "tm_ppeg_bwd_workspace": (L, [I, I, I]),
     "tm_ppeg_bwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "tm_put_cls": (I, [P, I, I, I, P, P]),
-    "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P]),
+    "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),
 }

@@ -122,6 +122,10 @@ TM_DEV float dropout_u01(uint64_t seed, uint32_t row, uint32_t col) {
   return (float)(h >> 8) * (1.0f / 16777216.0f);
 }
 
+TM_DEV uint64_t effective_seed(uint64_t seed, const uint64_t* seed_ptr) {
+  return seed_ptr ? (*seed_ptr) * 0x9E3779B97F4A7C15ull + seed : seed;
+}
+
 // Error plumbing shared by every C entry point.
 const char* tm_set_error(const char* msg);
 #define TM_CHECK_LAUNCH()                                                   \

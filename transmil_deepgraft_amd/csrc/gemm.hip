@@ -9,10 +9,18 @@
 //   A(m,k) = A_T ? A[k*lda + m] : A[m*lda + k]
 //   B(k,n) = B_KN ? B[k*ldb + n] : B[n*ldb + k]
 //
-// Block tile 128x128, 4 waves in 2x2, each wave 64x64 = 2x2 MFMA 32x32 tiles.
-// K staged through LDS in 64-byte rows (+16 B pad: conflict-free ds_read_b128
-// for the 16-lane groups), register double buffering.  Split-K writes fp32
-// slabs that tm_splitk_reduce sums in a fixed order (bitwise reproducible).
+// Block tile 128x128, 4 waves in 2x2, each wave 64x64 = 2x2 v_mfma 32x32 tiles.
+// K staged through LDS in 128-byte slices (BK = 64 bf16 / 32 f32), register
+// double buffering, 16 MFMAs per wave between barriers.
+//   * k-contiguous operand: LDS [row][BK + 16 B]  -> ds_read_b128 fragments
+//     (144 B rows: the 16-lane groups hit 16 distinct 16-B slots).
+//   * k-strided operand (weight gradients, X^T dY), bf16: the tile is stored
+//     as it lies in HBM, LDS [k][128 + 32] (320 B rows, 64 distinct banks per
+//     32-lane half), and read with ds_read_b64_tr_b16, the gfx950 transposing
+//     LDS read: two 4(k) x 16(m) blocks form one 8-deep fragment.  No scalar
+//     transposes anywhere.  (fp32 parity mode transposes on the LDS write.)
+// Split-K writes fp32 slabs that tm_splitk_reduce sums in a fixed order
+// (bitwise reproducible; no float atomics).
 #include "common.h"
 #include "../../include/transmil_hip.h"
 
@@ -21,22 +29,25 @@ namespace {
 constexpr int BM = 128, BN = 128;
 
 template <typename T> struct Tile {
-  static constexpr int E = 16 / sizeof(T);            // elements per 16-B chunk
-  static constexpr int BK = 64 / sizeof(T);           // 32 bf16, 16 f32
-  static constexpr int ROW = BK + E;                  // LDS row (elements), 80 B
+  static constexpr int E = 16 / sizeof(T);             // elements per 16-B chunk
+  static constexpr int BK = 128 / sizeof(T);           // 64 bf16, 32 f32: one 128-B slice
+  static constexpr int KROW = BK + E;                  // k-contiguous LDS row: 144 B
+  static constexpr int TROW = BM + 32;                 // bf16 k-strided LDS row: 320 B
   static constexpr int KSTEPS = BK / 16;
+  static constexpr int CHUNKS = BM * BK / E / 256;     // 16-B chunks per thread per operand (4)
 };
 
 template <typename T> union Chunk { f32x4 raw; T e[16 / sizeof(T)]; };
 
-// Non-transposed operand: rows r0.., k contiguous.  Chunk c: row c>>2, col (c&3)*E.
+// k-contiguous operand rows r0.. : chunk c -> row c / (BK/E), col (c % (BK/E)) * E
 template <typename T>
-TM_DEV void load_rows(Chunk<T> (&st)[2], const T* X, int ld, int r0, int rmax, int k0, int kend, int tid) {
-  constexpr int E = Tile<T>::E;
+TM_DEV void load_rows(Chunk<T> (&st)[Tile<T>::CHUNKS], const T* X, int ld, int r0, int rmax, int k0, int kend,
+                      int tid) {
+  constexpr int E = Tile<T>::E, CPR = Tile<T>::BK / E;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < Tile<T>::CHUNKS; ++i) {
     const int c = tid + 256 * i;
-    const int row = c >> 2, col = (c & 3) * E;
+    const int row = c / CPR, col = (c % CPR) * E;
     const int gr = r0 + row, gk = k0 + col;
     if (gr < rmax && gk + E <= kend) {
       st[i].raw = *(const f32x4*)(X + (size_t)gr * ld + gk);
@@ -48,20 +59,21 @@ TM_DEV void load_rows(Chunk<T> (&st)[2], const T* X, int ld, int r0, int rmax, i
   }
 }
 template <typename T>
-TM_DEV void store_rows(T* S, const Chunk<T> (&st)[2], int tid) {
-  constexpr int E = Tile<T>::E, ROW = Tile<T>::ROW;
+TM_DEV void store_rows(T* S, const Chunk<T> (&st)[Tile<T>::CHUNKS], int tid) {
+  constexpr int E = Tile<T>::E, CPR = Tile<T>::BK / E, ROW = Tile<T>::KROW;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < Tile<T>::CHUNKS; ++i) {
     const int c = tid + 256 * i;
-    *(f32x4*)(S + (c >> 2) * ROW + (c & 3) * E) = st[i].raw;
+    *(f32x4*)(S + (c / CPR) * ROW + (c % CPR) * E) = st[i].raw;
   }
 }
-// Transposed operand: global [k][m] (m contiguous).  Chunk c: k-row c / CPR, m-col (c % CPR)*E.
+// k-strided operand: global [k][m] (m contiguous).  chunk c -> k-row c / CPR, m-col (c % CPR) * E
 template <typename T>
-TM_DEV void load_cols(Chunk<T> (&st)[2], const T* X, int ld, int m0, int mmax, int k0, int kend, int tid) {
+TM_DEV void load_cols(Chunk<T> (&st)[Tile<T>::CHUNKS], const T* X, int ld, int m0, int mmax, int k0, int kend,
+                      int tid) {
   constexpr int E = Tile<T>::E, CPR = BM / E;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < Tile<T>::CHUNKS; ++i) {
     const int c = tid + 256 * i;
     const int kr = c / CPR, mc = (c % CPR) * E;
     const int gk = k0 + kr, gm = m0 + mc;
@@ -74,75 +86,69 @@ TM_DEV void load_cols(Chunk<T> (&st)[2], const T* X, int ld, int m0, int mmax, i
     }
   }
 }
+// bf16: keep the HBM orientation, LDS [k][TROW]; f32: transpose into [m][KROW]
 template <typename T>
-TM_DEV void store_cols(T* S, const Chunk<T> (&st)[2], int tid) {
-  constexpr int E = Tile<T>::E, CPR = BM / E, ROW = Tile<T>::ROW;
+TM_DEV void store_cols(T* S, const Chunk<T> (&st)[Tile<T>::CHUNKS], int tid) {
+  constexpr int E = Tile<T>::E, CPR = BM / E;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < Tile<T>::CHUNKS; ++i) {
     const int c = tid + 256 * i;
     const int kr = c / CPR, mc = (c % CPR) * E;
+    if constexpr (sizeof(T) == 2) {
+      *(f32x4*)(S + kr * Tile<T>::TROW + mc) = st[i].raw;
+    } else {
 #pragma unroll
-    for (int e = 0; e < E; ++e) S[(mc + e) * ROW + kr] = st[i].e[e];
+      for (int e = 0; e < E; ++e) S[(mc + e) * Tile<T>::KROW + kr] = st[i].e[e];
+    }
   }
+}
+
+// Fragment of a k-strided bf16 tile via two transposing reads.  Lane l: m = mb + (l&31),
+// k = kb + 8*(l>>5) + j.  16-lane group g: lane 4q+p addresses row k0+q, cols m0+4p..+3.
+TM_DEV bf16x8 frag_tr(const bf16* S, int mb, int kb, int lane) {
+  constexpr int TROW = Tile<bf16>::TROW;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int m = mb + (g & 1) * 16 + 4 * p;
+  const int k = kb + 8 * (g >> 1) + q;
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(S + k * TROW + m));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(S + (k + 4) * TROW + m));
+  return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <typename T, bool TRANS>
+TM_DEV vec8<T> frag(const T* S, int mb, int kb, int lane) {
+  if constexpr (TRANS && sizeof(T) == 2) {
+    return frag_tr((const bf16*)S, mb, kb, lane);
+  } else {
+    return load8(S + (mb + (lane & 31)) * Tile<T>::KROW + kb + 8 * (lane >> 5));
+  }
+}
+
+template <typename T, bool TRANS>
+constexpr int tile_elems() {
+  return (TRANS && sizeof(T) == 2) ? Tile<T>::BK * Tile<T>::TROW : BM * Tile<T>::KROW;
 }
 
 template <typename OutT>
 TM_DEV void put(OutT* p, float v) { *p = from_f<OutT>(v); }
 
-// One output element of the GEMM epilogue (kept out of line of the unrolled
-// accumulator loops so the accumulators stay in registers).
-template <typename OutT>
-TM_DEV void epilogue_elem(OutT* __restrict__ C, const tm_gemm_args& g, int m, int n, float v) {
-  if (m >= g.M || n >= g.N) return;
-  if (g.mode == TM_EPI_SPLITK) {  // fp32 slab [split][M][N]
-    ((float*)C)[((size_t)blockIdx.z * g.M + m) * g.N + n] = v;
-    return;
-  }
-  v *= g.alpha;
-  if (g.bias) v += g.bias[n];
-  if (g.mode == TM_EPI_QKV) {
-    const int bag = m / g.seq, t = m % g.seq;
-    const int inner = g.nh * g.dh;
-    const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
-    if (which == 0) v *= g.qscale;
-    const size_t dst = (((size_t)which * g.nbags * g.nh + (size_t)bag * g.nh + hh) * g.seq + t) * g.dh + d;
-    put(C + dst, v);
-    return;
-  }
-  if (g.pre) put((OutT*)g.pre + (size_t)m * g.ld_pre + n, v);
-  if (g.gelu) v = gelu_erf(v);
-  int row = m, dup_row = -1;
-  if (g.grp_in > 0) {
-    const int bag = m / g.grp_in, t = m % g.grp_in - g.skip;
-    if (t < 0) return;
-    row = bag * g.grp_out + g.out_off + t;
-    if (t < g.dup_n) dup_row = bag * g.grp_out + g.dup_off + t;
-  }
-  if (g.drop_p > 0.f) {
-    const float u = dropout_u01(g.seed, (uint32_t)row, (uint32_t)n);
-    v = (u >= g.drop_p) ? v * g.drop_scale : 0.f;
-  }
-  const size_t off = (size_t)row * g.ldc + n;
-  if (g.resid) v += g.resid[off];
-  if (g.accumulate) v += to_f(C[off]);
-  put(C + off, v);
-  if (dup_row >= 0) put(C + (size_t)dup_row * g.ldc + n, v);
-}
-
 template <typename T, typename OutT, bool A_T, bool B_KN>
 __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                    OutT* __restrict__ C, tm_gemm_args g) {
   using TT = Tile<T>;
-  constexpr int ROW = TT::ROW, BK = TT::BK;
-  __shared__ __attribute__((aligned(16))) T As[2][BM * ROW];
-  __shared__ __attribute__((aligned(16))) T Bs[2][BN * ROW];
+  constexpr int BK = TT::BK;
+  constexpr int AE = tile_elems<T, A_T>(), BE = tile_elems<T, B_KN>();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* As0 = (T*)smem;
+  T* Bs0 = As0 + 2 * AE;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int kbeg = blockIdx.z * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
-  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -150,7 +156,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
 
-  Chunk<T> sa[2], sb[2];
+  Chunk<T> sa[TT::CHUNKS], sb[TT::CHUNKS];
   auto gload = [&](int k0) {
     if constexpr (A_T) load_cols(sa, A, g.lda, m0, g.M, k0, kend, tid);
     else load_rows(sa, A, g.lda, m0, g.M, k0, kend, tid);
@@ -158,8 +164,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
     else load_rows(sb, B, g.ldb, n0, g.N, k0, kend, tid);
   };
   auto lstore = [&](int buf) {
-    if constexpr (A_T) store_cols(As[buf], sa, tid); else store_rows(As[buf], sa, tid);
-    if constexpr (B_KN) store_cols(Bs[buf], sb, tid); else store_rows(Bs[buf], sb, tid);
+    if constexpr (A_T) store_cols(As0 + buf * AE, sa, tid); else store_rows(As0 + buf * AE, sa, tid);
+    if constexpr (B_KN) store_cols(Bs0 + buf * BE, sb, tid); else store_rows(Bs0 + buf * BE, sb, tid);
   };
 
   if (nk > 0) {
@@ -170,15 +176,15 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
-    const T* as = As[cur];
-    const T* bs = Bs[cur];
+    const T* as = As0 + cur * AE;
+    const T* bs = Bs0 + cur * BE;
 #pragma unroll
     for (int s = 0; s < TT::KSTEPS; ++s) {
       vec8<T> af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = load8(as + (wm * 64 + i * 32 + l32) * ROW + s * 16 + 8 * h);
+      for (int i = 0; i < 2; ++i) af[i] = frag<T, A_T>(as, wm * 64 + i * 32, s * 16, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = load8(bs + (wn * 64 + j * 32 + l32) * ROW + s * 16 + 8 * h);
+      for (int j = 0; j < 2; ++j) bfr[j] = frag<T, B_KN>(bs, wn * 64 + j * 32, s * 16, lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -188,17 +194,82 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
-  auto tile_epi = [&](const f32x16& a, int i, int j) {
-    const int n = n0 + wn * 64 + j * 32 + l32;
-    const int mb = m0 + wm * 64 + i * 32;
+  // ---------------- epilogue: row / column bookkeeping hoisted out of the element loop ----------------
+  int ncol[2];
+  float bcol[2];
+  long long cpart[2];   // QKV: column part of the scatter offset
+  bool qcol[2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) epilogue_elem<OutT>(C, g, mb + acc_row(r, h), n, a[r]);
-  };
-  tile_epi(acc[0][0], 0, 0);
-  tile_epi(acc[0][1], 0, 1);
-  tile_epi(acc[1][0], 1, 0);
-  tile_epi(acc[1][1], 1, 1);
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + j * 32 + l32;
+    ncol[j] = n;
+    bcol[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+    if (g.mode == TM_EPI_QKV) {
+      const int inner = g.nh * g.dh;
+      const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
+      cpart[j] = ((long long)which * g.nbags * g.nh + hh) * g.seq * g.dh + d;
+      qcol[j] = which == 0;
+    } else {
+      cpart[j] = 0;
+      qcol[j] = false;
+    }
+  }
+  const size_t slab = (size_t)blockIdx.z * g.M * g.N;
+  const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 64 + i * 32 + acc_row(r, h);
+      if (m >= g.M) continue;
+      if (g.mode == TM_EPI_SPLITK) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (ncol[j] < g.N) ((float*)C)[slab + (size_t)m * g.N + ncol[j]] = acc[i][j][r];
+        continue;
+      }
+      if (g.mode == TM_EPI_QKV) {
+        const int bag = m / g.seq, t = m - bag * g.seq;
+        const long long rpart = ((long long)bag * g.nh * g.seq + t) * g.dh;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (ncol[j] >= g.N) continue;
+          float v = acc[i][j][r] * g.alpha + bcol[j];
+          if (qcol[j]) v *= g.qscale;
+          put(C + rpart + cpart[j], v);
+        }
+        continue;
+      }
+      int row = m, dup_row = -1;
+      if (g.grp_in > 0) {
+        const int bag = m / g.grp_in, t = m - bag * g.grp_in - g.skip;
+        if (t < 0) continue;
+        row = bag * g.grp_out + g.out_off + t;
+        if (t < g.dup_n) dup_row = bag * g.grp_out + g.dup_off + t;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = ncol[j];
+        if (n >= g.N) continue;
+        float v = acc[i][j][r] * g.alpha + bcol[j];
+        if (g.pre) put((OutT*)g.pre + (size_t)m * g.ld_pre + n, v);
+        if (g.gelu) v = gelu_erf(v);
+        if (g.drop_p > 0.f) {
+          const float u = dropout_u01(seed, (uint32_t)row, (uint32_t)n);
+          v = (u >= g.drop_p) ? v * g.drop_scale : 0.f;
+        }
+        const size_t off = (size_t)row * g.ldc + n;
+        if (g.resid) v += g.resid[off];
+        if (g.accumulate) v += to_f(C[off]);
+        put(C + off, v);
+        if (dup_row >= 0) put(C + (size_t)dup_row * g.ldc + n, v);
+      }
+    }
+}
+
+template <typename T, bool A_T, bool B_KN>
+constexpr size_t gemm_smem() {
+  return 2 * (tile_elems<T, A_T>() + tile_elems<T, B_KN>()) * sizeof(T);
 }
 
 template <typename T, typename OutT>
@@ -207,8 +278,14 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
   const T* a = (const T*)A;
   const T* b = (const T*)B;
   OutT* c = (OutT*)C;
-#define TM_GEMM_CASE(AT, BKN) \
-  if (g.a_trans == AT && g.b_kn == BKN) { gemm_kernel<T, OutT, AT, BKN><<<grid, 256, 0, st>>>(a, b, c, g); TM_CHECK_LAUNCH(); return 0; }
+#define TM_GEMM_CASE(AT, BKN)                                                       \
+  if (g.a_trans == AT && g.b_kn == BKN) {                                           \
+    constexpr size_t sm = gemm_smem<T, AT, BKN>();                                  \
+    tm_allow_smem(gemm_kernel<T, OutT, AT, BKN>, sm);                               \
+    gemm_kernel<T, OutT, AT, BKN><<<grid, 256, sm, st>>>(a, b, c, g);               \
+    TM_CHECK_LAUNCH();                                                              \
+    return 0;                                                                       \
+  }
   TM_GEMM_CASE(0, 0) TM_GEMM_CASE(0, 1) TM_GEMM_CASE(1, 0) TM_GEMM_CASE(1, 1)
 #undef TM_GEMM_CASE
   tm_set_error("gemm: bad transpose flags");
@@ -221,6 +298,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ slab, float* __re
   if (i4 * 4 >= count) return;
   if (i4 * 4 + 4 <= count) {
     f32x4 s = *(const f32x4*)(slab + i4 * 4);
+#pragma unroll 8
     for (int z = 1; z < splits; ++z) s += *(const f32x4*)(slab + (size_t)z * count + i4 * 4);
     s *= alpha;
     if (accumulate) s += *(f32x4*)(out + i4 * 4);
@@ -266,10 +344,12 @@ extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args
   if (g->M == 0 || g->N == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (g->ab_dtype == TM_BF16) {
+    TM_REQUIRE(g->k_per_split % 64 == 0 || g->splits == 1, "gemm: bf16 k_per_split must be a multiple of 64");
     if (g->c_dtype == TM_BF16) return launch_t<bf16, bf16>(A, B, C, *g, st);
     return launch_t<bf16, float>(A, B, C, *g, st);
   }
   TM_REQUIRE(g->ab_dtype == TM_F32, "gemm: ab_dtype");
+  TM_REQUIRE(g->k_per_split % 32 == 0 || g->splits == 1, "gemm: f32 k_per_split must be a multiple of 32");
   if (g->c_dtype == TM_BF16) return launch_t<float, bf16>(A, B, C, *g, st);
   return launch_t<float, float>(A, B, C, *g, st);
 }

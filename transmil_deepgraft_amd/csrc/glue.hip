@@ -16,8 +16,10 @@ __global__ void put_cls_kernel(const float* __restrict__ cls, int S, int D, floa
 // grid (n_pad, B), block 256
 template <typename T>
 __global__ void dropout_bwd_pad_kernel(const float* __restrict__ dH, int S, int n_pad, int pad, int D, float p,
-                                       float scale, uint64_t seed, T* __restrict__ out) {
+                                       float scale, uint64_t seed0, const uint64_t* __restrict__ seed_ptr,
+                                       T* __restrict__ out) {
   const int t = blockIdx.x, b = blockIdx.y;
+  const uint64_t seed = p > 0.f ? effective_seed(seed0, seed_ptr) : 0;
   T* dst = out + ((size_t)b * n_pad + t) * D;
   const int i = t - pad;
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
@@ -79,11 +81,11 @@ extern "C" int tm_put_cls(const float* cls, int B, int S, int D, float* H, void*
 }
 
 extern "C" int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int pad, int D, float p,
-                                  uint64_t seed, void* out, void* stream) {
+                                  uint64_t seed, const uint64_t* seed_ptr, void* out, void* stream) {
   TM_REQUIRE(n_pad >= S + pad, "dropout_bwd_pad: n_pad < S + pad");
   const float scale = p > 0.f ? 1.0f / (1.0f - p) : 1.0f;
   TM_DTYPE_DISPATCH(dtype, (dropout_bwd_pad_kernel<T><<<dim3(n_pad, B), 256, 0, (hipStream_t)stream>>>(
-                               dH, S, n_pad, pad, D, p, scale, seed, (T*)out)));
+                               dH, S, n_pad, pad, D, p, scale, seed, seed_ptr, (T*)out)));
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -34,12 +34,17 @@ constexpr int TAPS = 33;   // residual conv kernel
 constexpr int HALF = 16;   // conv padding
 
 // LDS row strides (elements).  Keys [256][KROW]: 144 B (bf16) / 272 B (f32) rows
-// -> conflict-free ds_read_b128 for 16 consecutive rows.  Values^T [64][VROW]:
-// 520 B (bf16, ds_read_b64 2 dwords/lane over all 64 banks) / 1040 B (f32).
+// -> conflict-free ds_read_b128 for 16 consecutive rows.
+// Values, bf16: natural [256 keys][VROW = 80] (160-B rows: the transposing
+// ds_read_b64_tr_b16 of 4 keys x 16 d hits 64 distinct banks per 32-lane half);
+// fp32 (parity mode, no 32-bit transposing read): values^T [64][VROW = 260].
 template <typename T> struct Lay {
-  static constexpr int KROW = DH + 16 / (int)sizeof(T);  // 72 bf16 / 68 f32
-  static constexpr int VROW = NL + 4;                                              // 260
+  static constexpr int KROW = DH + 16 / (int)sizeof(T);    // 72 bf16 / 68 f32
+  static constexpr int VROW = sizeof(T) == 2 ? 80 : NL + 4;
+  static constexpr int VELEMS = sizeof(T) == 2 ? NL * VROW : DH * VROW;
 };
+
+template <typename T> union Chunk16 { f32x4 raw; T e[16 / sizeof(T)]; };
 
 TM_DEV long long hoff(long long bh, int nh, long long bag_stride, long long head_stride) {
   return (bh / nh) * bag_stride + (bh % nh) * head_stride;
@@ -121,6 +126,28 @@ __global__ void softmax_bwd_rows_kernel(const float* __restrict__ a, const float
   *(f32x4*)(ds + (size_t)r * NL + lane * 4) = o;
 }
 
+// A operand of O^T = V^T P^T for d tile dt and the 16-key step starting at key kb:
+// element j of lane (r, h) = V[kb + 8(j>>2) + 4h + (j&3)][dt*32 + r]  (acc_k_index order).
+template <typename T> TM_DEV vec8<T> value_frag(const T* vs, int dt, int kb, int lane);
+template <> TM_DEV bf16x8 value_frag<bf16>(const bf16* vs, int dt, int kb, int lane) {
+  // natural [key][80] layout, two transposing reads of 4 keys x 16 d
+  constexpr int VROW = Lay<bf16>::VROW;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int d = dt * 32 + (g & 1) * 16 + 4 * p;
+  const int key = kb + 4 * (g >> 1) + q;
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(vs + key * VROW + d));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(vs + (key + 8) * VROW + d));
+  return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+template <> TM_DEV f32x8 value_frag<float>(const float* vt, int dt, int kb, int lane) {
+  // transposed [d][260] layout
+  constexpr int VROW = Lay<float>::VROW;
+  const float* row = vt + (dt * 32 + (lane & 31)) * VROW + kb + 4 * (lane >> 5);
+  const f32x4 lo = *(const f32x4*)row, hi = *(const f32x4*)(row + 8);
+  return (f32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
 // ---------------------------------------------------------------------------
 // Shared forward block: one wave, 32 queries (B-operand fragments qf), 256 keys in
 // LDS (ks[key][KROW]), values^T in LDS (vt[d][VROW]).  Returns unnormalised O^T
@@ -128,7 +155,7 @@ __global__ void softmax_bwd_rows_kernel(const float* __restrict__ a, const float
 template <typename T>
 TM_DEV void attn_fwd_wave(const T* ks, const T* vt, const vec8<T> (&qf)[4], f32x16 (&o)[2], float& mx, float& sum,
                           int lane) {
-  constexpr int KROW = Lay<T>::KROW, VROW = Lay<T>::VROW;
+  constexpr int KROW = Lay<T>::KROW;
   const int r = lane & 31, h = lane >> 5;
   f32x16 s[8];
 #pragma unroll
@@ -164,28 +191,11 @@ TM_DEV void attn_fwd_wave(const T* ks, const T* vt, const vec8<T> (&qf)[4], f32x
 #pragma unroll
     for (int kt = 0; kt < 8; ++kt)
 #pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        const T* row = vt + (dt * 32 + r) * VROW + kt * 32 + 16 * sp + 4 * h;
-        const vec4<T> lo = load4(row), hi = load4(row + 8);
-        vec8<T> a;
-        a[0] = lo[0]; a[1] = lo[1]; a[2] = lo[2]; a[3] = lo[3];
-        a[4] = hi[0]; a[5] = hi[1]; a[6] = hi[2]; a[7] = hi[3];
-        mma16(o[dt], a, acc_as_operand<T>(s[kt], sp));
-      }
+      for (int sp = 0; sp < 2; ++sp)
+        mma16(o[dt], value_frag<T>(vt, dt, kt * 32 + 16 * sp, lane), acc_as_operand<T>(s[kt], sp));
   }
 }
 
-// stage fp32 [256][64] (keys) into LDS ks[key][KROW] as T
-template <typename T>
-TM_DEV void stage_keys_f32(T* ks, const float* src, int tid) {
-  constexpr int KROW = Lay<T>::KROW;
-  for (int i = tid; i < NL * DH / 4; i += 256) {
-    const int row = i >> 4, c = (i & 15) * 4;
-    const f32x4 v = *(const f32x4*)(src + (size_t)row * DH + c);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) ks[row * KROW + c + e] = from_f<T>(v[e]);
-  }
-}
 // stage T rows [256][64] (row stride 64) into ks[key][KROW]
 template <typename T>
 TM_DEV void stage_keys_t(T* ks, const T* src, int tid) {
@@ -195,13 +205,19 @@ TM_DEV void stage_keys_t(T* ks, const T* src, int tid) {
     *(f32x4*)(ks + row * KROW + c) = *(const f32x4*)(src + (size_t)row * DH + c);
   }
 }
-// stage values [256][64] (fp32 or T) transposed into vt[d][VROW] as T
-template <typename T, typename S>
-TM_DEV void stage_values_t(T* vt, const S* src, int tid) {
-  constexpr int VROW = Lay<T>::VROW;
-  for (int i = tid; i < NL * DH; i += 256) {
-    const int key = i >> 6, d = i & 63;
-    vt[d * VROW + key] = from_f<T>(to_f(src[(size_t)key * DH + d]));
+// stage values [256 keys][64] (T rows, stride 64) into the value layout of Lay<T>
+template <typename T>
+TM_DEV void stage_values(T* vs, const T* src, int tid) {
+  constexpr int VROW = Lay<T>::VROW, E = 16 / sizeof(T);
+  for (int i = tid; i < NL * DH / E; i += 256) {
+    const int key = i / (DH / E), d0 = (i % (DH / E)) * E;
+    if constexpr (sizeof(T) == 2) {
+      *(f32x4*)(vs + key * VROW + d0) = *(const f32x4*)(src + (size_t)key * DH + d0);
+    } else {
+      const f32x4 v4 = *(const f32x4*)(src + (size_t)key * DH + d0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) vs[(d0 + e) * VROW + key] = v4[e];
+    }
   }
 }
 
@@ -211,20 +227,20 @@ TM_DEV void stage_values_t(T* vt, const S* src, int tid) {
 //   lse1[bh][t] saved for backward.
 template <typename T>
 __global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, const T* __restrict__ v,
-                                                     const float* __restrict__ kl, const float* __restrict__ y,
+                                                     const T* __restrict__ kl_t, const T* __restrict__ y_t,
                                                      const float* __restrict__ wconv, int n, int nh,
                                                      T* __restrict__ merged, float* __restrict__ lse1) {
   constexpr int KROW = Lay<T>::KROW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* ks = (T*)smem;                                  // [256][KROW]
-  T* vt = ks + NL * KROW;                            // [64][VROW]
+  T* vt = ks + NL * KROW;                            // values (Lay<T>)
   float* ost = (float*)smem;                         // reuse: [128][68] fp32 after the MFMA phase
   const int bh = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int head = bh % nh, bag = bh / nh;
   const int t0 = blockIdx.x * 128;
-  stage_keys_f32<T>(ks, kl + (size_t)bh * NL * DH, tid);
-  stage_values_t<T, float>(vt, y + (size_t)bh * NL * DH, tid);
+  stage_keys_t<T>(ks, kl_t + (size_t)bh * NL * DH, tid);
+  stage_values<T>(vt, y_t + (size_t)bh * NL * DH, tid);
   const T* qb = q + (size_t)bh * n * DH;
   vec8<T> qf[4];
   const int qrow = t0 + wave * 32 + r;
@@ -290,7 +306,7 @@ __global__ __launch_bounds__(256) void a3_fwd_kernel(const float* __restrict__ q
   const int r = lane & 31, h = lane >> 5;
   const size_t kv_off = ((size_t)bh * n + (size_t)kb * NL) * DH;
   stage_keys_t<T>(ks, k + kv_off, tid);
-  stage_values_t<T, T>(vt, v + kv_off, tid);
+  stage_values<T>(vt, v + kv_off, tid);
   __syncthreads();
   {
     const int qi = blockIdx.z * 128 + wave * 32 + r;  // query half per workgroup
@@ -358,14 +374,17 @@ __global__ void cast_rows_kernel(const float* __restrict__ x, T* __restrict__ y,
 //   c_tau(t)      = sum_d dO[t][d] v[t + tau - 16][d]
 //   D1[bh][t]     = dO[t].O[t] - sum_tau w[tau] c_tau(t)          (= dO . (attn1 Y) )
 //   dw_part[bag*ntb + tb][head*33 + tau] = sum_{t in block} c_tau(t)
+// 96 staged rows (64 + 2*16 halo) of dO and v in fp32 LDS (272-B rows, b128 reads);
+// a thread owns one row and every 4th tap, so each dO piece is read once per 9 taps.
 template <typename T>
-__global__ __launch_bounds__(256) void conv_bwd_kernel(const T* __restrict__ dmerged, const T* __restrict__ merged,
+__global__ __launch_bounds__(256, 2) void conv_bwd_kernel(const T* __restrict__ dmerged, const T* __restrict__ merged,
                                                        const T* __restrict__ v, const float* __restrict__ wconv,
                                                        int n, int nh, float* __restrict__ dv, float* __restrict__ d1,
                                                        float* __restrict__ dw_part) {
-  constexpr int R = 64, HR = R + 2 * HALF;  // 96 staged rows
-  __shared__ float dos[HR][DH + 1];
-  __shared__ float vs[HR][DH + 1];
+  constexpr int R = 64, HR = R + 2 * HALF, RW = DH + 4;  // 96 staged rows, 68-float rows
+  constexpr int NTQ = (TAPS + 3) / 4;                    // taps per thread (9)
+  __shared__ __attribute__((aligned(16))) float dos[HR][RW];
+  __shared__ __attribute__((aligned(16))) float vs[HR][RW];
   __shared__ float cred[R][TAPS + 1];
   __shared__ float ws[TAPS];
   const int bh = blockIdx.y, tb = blockIdx.x, tid = threadIdx.x;
@@ -375,30 +394,65 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(const T* __restrict__ dme
   const T* dob = dmerged + (size_t)bag * n * ld + head * DH;
   const T* ob = merged + (size_t)bag * n * ld + head * DH;
   const T* vb = v + (size_t)bh * n * DH;
-  for (int i = tid; i < HR * DH; i += 256) {
-    const int rr = i >> 6, d = i & 63, t = t0 - HALF + rr;
+  constexpr int E = 16 / sizeof(T);
+  for (int i = tid; i < HR * DH / E; i += 256) {
+    const int rr = i / (DH / E), d0 = (i % (DH / E)) * E, t = t0 - HALF + rr;
     const bool ok = t >= 0 && t < n;
-    dos[rr][d] = ok ? to_f(dob[(size_t)t * ld + d]) : 0.f;
-    vs[rr][d] = ok ? to_f(vb[(size_t)t * DH + d]) : 0.f;
+    Chunk16<T> a, b;
+    if (ok) {
+      a.raw = *(const f32x4*)(dob + (size_t)t * ld + d0);
+      b.raw = *(const f32x4*)(vb + (size_t)t * DH + d0);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      dos[rr][d0 + e] = ok ? to_f(a.e[e]) : 0.f;
+      vs[rr][d0 + e] = ok ? to_f(b.e[e]) : 0.f;
+    }
   }
   if (tid < TAPS) ws[tid] = wconv[head * TAPS + tid];
   __syncthreads();
-  // part A: thread (row rl, quarter qq)
+  // part A: thread (row rl, tap phase qq): taps qq, qq+4, ...
   {
-    const int rl = tid >> 2, qq = tid & 3;
-    float wc = 0.f;
-    for (int tau = qq; tau < TAPS; tau += 4) {
-      float c = 0.f;
-#pragma unroll 8
-      for (int d = 0; d < DH; ++d) c = fmaf(dos[rl + HALF][d], vs[rl + tau][d], c);
-      cred[rl][tau] = c;
-      wc = fmaf(ws[tau], c, wc);
-    }
-    float dd = 0.f;
-    const int t = t0 + rl;
-    if (t < n) {
+    const int rl = tid >> 2, qq = tid & 3, t = t0 + rl;
+    float c[NTQ];
 #pragma unroll
-      for (int d = qq * 16; d < qq * 16 + 16; ++d) dd = fmaf(dos[rl + HALF][d], to_f(ob[(size_t)t * ld + d]), dd);
+    for (int k = 0; k < NTQ; ++k) c[k] = 0.f;
+    float dd = 0.f;
+#pragma unroll
+    for (int dc = 0; dc < DH; dc += 16) {
+      float g[16];
+#pragma unroll
+      for (int e = 0; e < 16; e += 4) {
+        const f32x4 x4 = *(const f32x4*)&dos[rl + HALF][dc + e];
+        g[e] = x4[0]; g[e + 1] = x4[1]; g[e + 2] = x4[2]; g[e + 3] = x4[3];
+      }
+#pragma unroll
+      for (int k = 0; k < NTQ; ++k) {
+        const int tau = qq + 4 * k;
+        if (tau < TAPS) {
+#pragma unroll
+          for (int e = 0; e < 16; e += 4) {
+            const f32x4 x4 = *(const f32x4*)&vs[rl + tau][dc + e];
+            c[k] = fmaf(g[e], x4[0], c[k]); c[k] = fmaf(g[e + 1], x4[1], c[k]);
+            c[k] = fmaf(g[e + 2], x4[2], c[k]); c[k] = fmaf(g[e + 3], x4[3], c[k]);
+          }
+        }
+      }
+      if (dc / 16 == qq && t < n) {  // this thread's quarter of dO . O
+#pragma unroll
+        for (int part = 0; part < 16 / E; ++part) {
+          Chunk16<T> o;
+          o.raw = *(const f32x4*)(ob + (size_t)t * ld + dc + part * E);
+#pragma unroll
+          for (int e = 0; e < E; ++e) dd = fmaf(g[part * E + e], to_f(o.e[e]), dd);
+        }
+      }
+    }
+    float wc = 0.f;
+#pragma unroll
+    for (int k = 0; k < NTQ; ++k) {
+      const int tau = qq + 4 * k;
+      if (tau < TAPS) { cred[rl][tau] = c[k]; wc = fmaf(ws[tau], c[k], wc); }
     }
     float tot = dd - wc;
     tot += __shfl_xor(tot, 1, 64);
@@ -407,9 +461,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(const T* __restrict__ dme
   }
   __syncthreads();
   if (tid < TAPS) {
-    float s = 0.f;
-    for (int rl = 0; rl < R; ++rl) s += cred[rl][tid];
-    dw_part[((size_t)bag * ntb + tb) * (nh * TAPS) + head * TAPS + tid] = s;
+    float sum = 0.f;
+    for (int rl = 0; rl < R; ++rl) sum += cred[rl][tid];
+    dw_part[((size_t)bag * ntb + tb) * (nh * TAPS) + head * TAPS + tid] = sum;
   }
   // part B: dv, thread (row rl, 16 d)
   {
@@ -418,12 +472,15 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(const T* __restrict__ dme
       float acc[16];
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
+#pragma unroll 3
       for (int tau = 0; tau < TAPS; ++tau) {
-        const float* src = dos[rl + 2 * HALF - tau] + d0;
         const float wt = ws[tau];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = fmaf(wt, src[e], acc[e]);
+        for (int e = 0; e < 16; e += 4) {
+          const f32x4 x4 = *(const f32x4*)&dos[rl + 2 * HALF - tau][d0 + e];
+          acc[e] = fmaf(wt, x4[0], acc[e]); acc[e + 1] = fmaf(wt, x4[1], acc[e + 1]);
+          acc[e + 2] = fmaf(wt, x4[2], acc[e + 2]); acc[e + 3] = fmaf(wt, x4[3], acc[e + 3]);
+        }
       }
       float* dst = dv + ((size_t)bh * n + t) * DH + d0;
 #pragma unroll
@@ -458,24 +515,41 @@ struct BwdArgs {
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
 
+template <typename T> struct BwdLay {
+  static constexpr int QT_ROW = 32 + 4;              // Q^T / dO^T chunk [64 d][36]
+  static constexpr int KT_ROW = NL + 16 / sizeof(T); // K^T [64 d][264 bf16 / 260 f32]
+  static constexpr int DS_ROW = KT_ROW;              // dS  [32 q][...]
+  static constexpr size_t KT_OFF = 0;
+  static constexpr size_t DS_OFF = KT_OFF + DH * KT_ROW * sizeof(T);
+  static constexpr size_t QT_OFF = DS_OFF + 32 * DS_ROW * sizeof(T);
+  static constexpr size_t OT_OFF = QT_OFF + DH * QT_ROW * sizeof(T);
+  static constexpr size_t XC_OFF = OT_OFF + DH * QT_ROW * sizeof(T);   // fp32 [3][2][1024]
+  static constexpr size_t LS_OFF = XC_OFF + 6 * 1024 * 4;              // fp32 lse[32], D[32]
+  static constexpr size_t MAIN = LS_OFF + 64 * 4;
+  static constexpr size_t EPI = (size_t)NL * 68 * 4;                   // key-side transpose stage
+  static constexpr size_t BYTES = MAIN > EPI ? MAIN : EPI;
+};
+
+// 8 waves x 32 keys.  The wave's K and V fragments stay in registers for the
+// whole query walk; per 32-query chunk: S, dP (8 MFMAs), dV^T, dK^T (8 MFMAs),
+// and a quarter of dQ = dS K (4 MFMAs) reduced across the 4 key quarters in LDS.
 template <typename T, int MODE>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
-  constexpr int QT_ROW = 32 + 4;              // [64 d][36]  (T)
-  constexpr int KT_ROW = NL + 16 / sizeof(T); // [64 d][264 bf16 / 260 f32]
-  constexpr int DS_ROW = NL + 16 / sizeof(T); // [32 q][...]
+__global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
+  using LY = BwdLay<T>;
+  constexpr int QT_ROW = LY::QT_ROW, KT_ROW = LY::KT_ROW, DS_ROW = LY::DS_ROW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* kt_s = (T*)smem;                                   // K^T  [64][KT_ROW]
-  T* ds_s = kt_s + DH * KT_ROW;                         // dS   [32][DS_ROW]
-  T* qt_s = ds_s + 32 * DS_ROW;                         // Q^T  [64][QT_ROW]
-  T* dot_s = qt_s + DH * QT_ROW;                        // dO^T [64][QT_ROW]
-  float* xch = (float*)(dot_s + DH * QT_ROW);           // [2][32*32] dQ partial exchange
-  float* lse_s = xch + 2 * 1024;                        // [32]
-  float* dd_s = lse_s + 32;                             // [32]
-  float* stage = (float*)smem;                          // epilogue reuse [256][68]
+  T* kt_s = (T*)(smem + LY::KT_OFF);
+  T* ds_s = (T*)(smem + LY::DS_OFF);
+  T* qt_s = (T*)(smem + LY::QT_OFF);
+  T* dot_s = (T*)(smem + LY::OT_OFF);
+  float* xch = (float*)(smem + LY::XC_OFF);
+  float* lse_s = (float*)(smem + LY::LS_OFF);
+  float* dd_s = lse_s + 32;
+  float* stage = (float*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, bh = blockIdx.y, nh = a.nh;
-  const int key0 = (MODE == MODE_A3) ? blk * NL : 0;      // first key row of this WG
+  const int key0 = (MODE == MODE_A3) ? blk * NL : 0;
   const int q_begin = (MODE == MODE_A1) ? blk * a.n_queries_per_wg : 0;
   const int q_count = a.n_queries_per_wg;
 
@@ -486,112 +560,121 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
   const float* lse = a.lse + bh * a.lse_bh;
   const float* dd = a.dd + bh * a.dd_bh;
 
-  // K^T into LDS (all 256 keys)
-  for (int i = tid; i < NL * DH; i += 256) {
-    const int key = i >> 6, d = i & 63;
-    kt_s[d * KT_ROW + key] = K[(size_t)key * DH + d];
+  // K^T into LDS (all 256 keys): 16-B row loads, transposed element writes
+  {
+    constexpr int E = 16 / sizeof(T);
+    for (int c = tid; c < NL * DH / E; c += 512) {
+      const int key = c / (DH / E), d0 = (c % (DH / E)) * E;
+      const vec8<T> v8 = E == 8 ? load8(K + (size_t)key * DH + d0) : vec8<T>{};
+      if constexpr (E == 8) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) kt_s[(d0 + e) * KT_ROW + key] = v8[e];
+      } else {
+        const vec4<T> v4 = load4(K + (size_t)key * DH + d0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kt_s[(d0 + e) * KT_ROW + key] = v4[e];
+      }
+    }
+  }
+  const int mykey = wave * 32;
+  vec8<T> kf[4], vf[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    kf[st] = load8(K + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
+    vf[st] = load8(V + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
   }
 
-  f32x16 dvt[2][2], dkt[2][2];  // [d tile][key tile]
+  f32x16 dvt[2], dkt[2];  // [d tile], cols = this wave's 32 keys
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) { dvt[i][j] = (f32x16){}; dkt[i][j] = (f32x16){}; }
+  for (int i = 0; i < 2; ++i) { dvt[i] = (f32x16){}; dkt[i] = (f32x16){}; }
 
-  const int mykey = wave * 64;  // this wave's 64 keys (local)
+  const int dt_q = wave & 1, kq = wave >> 1;  // dQ role: d tile, key quarter
 #pragma unroll 1
   for (int c0 = 0; c0 < q_count; c0 += 32) {
-    const int qa = q_begin + c0;  // absolute first query of the chunk
-    __syncthreads();              // previous chunk fully consumed
-    for (int i = tid; i < 32 * DH; i += 256) {
-      const int qq = i >> 6, d = i & 63;
-      qt_s[d * QT_ROW + qq] = Q[(size_t)(qa + qq) * a.q_row + d];
-      dot_s[d * QT_ROW + qq] = dO[(size_t)(qa + qq) * a.o_row + d];
+    const int qa = q_begin + c0;
+    __syncthreads();  // previous chunk fully consumed
+    {
+      // one 16-B row piece per thread: threads 0..255 Q, 256..511 dO (bf16: 8 d each)
+      constexpr int E = 16 / sizeof(T);
+      const int which = tid >> 8, c = tid & 255;
+      const T* src = which ? dO : Q;
+      const int row = which ? a.o_row : a.q_row;
+      T* dst = which ? dot_s : qt_s;
+      for (int cc = c; cc < 32 * DH / E; cc += 256) {
+        const int qq = cc / (DH / E), d0 = (cc % (DH / E)) * E;
+        if constexpr (E == 8) {
+          const vec8<T> v8 = load8(src + (size_t)(qa + qq) * row + d0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dst[(d0 + e) * QT_ROW + qq] = v8[e];
+        } else {
+          const vec4<T> v4 = load4(src + (size_t)(qa + qq) * row + d0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dst[(d0 + e) * QT_ROW + qq] = v4[e];
+        }
+      }
     }
     if (tid < 32) { lse_s[tid] = lse[qa + tid]; dd_s[tid] = dd[qa + tid]; }
     __syncthreads();
-    // S = Q K^T and dP = dO V^T for 32 queries x this wave's 64 keys
-    f32x16 s[2], dp[2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) { s[kt] = (f32x16){}; dp[kt] = (f32x16){}; }
+    // S = Q K^T, dP = dO V^T: rows = queries (registers), cols = this wave's keys (lanes)
+    f32x16 s = (f32x16){}, dp = (f32x16){};
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const vec8<T> qa_f = load8(Q + (size_t)(qa + r) * a.q_row + st * 16 + 8 * h);
       const vec8<T> oa_f = load8(dO + (size_t)(qa + r) * a.o_row + st * 16 + 8 * h);
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const int key = mykey + kt * 32 + r;
-        const vec8<T> kb_f = load8(K + (size_t)key * DH + st * 16 + 8 * h);
-        const vec8<T> vb_f = load8(V + (size_t)key * DH + st * 16 + 8 * h);
-        mma16(s[kt], qa_f, kb_f);
-        mma16(dp[kt], oa_f, vb_f);
-      }
+      mma16(s, qa_f, kf[st]);
+      mma16(dp, oa_f, vf[st]);
     }
-    // P and dS (rows = queries on registers)
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qq = acc_row(i, h);
-        const float p = __expf(s[kt][i] - lse_s[qq]);
-        s[kt][i] = p;
-        dp[kt][i] = p * (dp[kt][i] - dd_s[qq]);
-      }
+    for (int i = 0; i < 16; ++i) {
+      const int qq = acc_row(i, h);
+      const float p = __expf(s[i] - lse_s[qq]);
+      s[i] = p;
+      dp[i] = p * (dp[i] - dd_s[qq]);
+    }
     // dV^T += dO^T P ; dK^T += Q^T dS
 #pragma unroll
     for (int sp = 0; sp < 2; ++sp) {
-      vec8<T> ao[2], aq[2];
+      const vec8<T> bp = acc_as_operand<T>(s, sp);
+      const vec8<T> bs = acc_as_operand<T>(dp, sp);
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
         const T* ro = dot_s + (dt * 32 + r) * QT_ROW + 16 * sp + 4 * h;
         const T* rq = qt_s + (dt * 32 + r) * QT_ROW + 16 * sp + 4 * h;
+        const vec4<T> o0 = load4(ro), o1 = load4(ro + 8), q0 = load4(rq), q1 = load4(rq + 8);
+        vec8<T> ao, aq;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          ao[dt][e] = ro[e]; ao[dt][4 + e] = ro[8 + e];
-          aq[dt][e] = rq[e]; aq[dt][4 + e] = rq[8 + e];
-        }
-      }
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const vec8<T> bp = acc_as_operand<T>(s[kt], sp);
-        const vec8<T> bs = acc_as_operand<T>(dp[kt], sp);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          mma16(dvt[dt][kt], ao[dt], bp);
-          mma16(dkt[dt][kt], aq[dt], bs);
-        }
+        for (int e = 0; e < 4; ++e) { ao[e] = o0[e]; ao[4 + e] = o1[e]; aq[e] = q0[e]; aq[4 + e] = q1[e]; }
+        mma16(dvt[dt], ao, bp);
+        mma16(dkt[dt], aq, bs);
       }
     }
     // dS -> LDS [q][key]
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + kt * 32 + r] = from_f<T>(dp[kt][i]);
+    for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + r] = from_f<T>(dp[i]);
     __syncthreads();
-    // dQ chunk [32 q x 64 d] = dS [32 x 256] . K [256 x 64]; wave w: d tile (w&1), key half (w>>1)
+    // dQ chunk [32 q x 64 d] = dS [32 x 256] . K [256 x 64]: this wave: d tile dt_q, keys 64*kq..+63
     {
-      const int dt = wave & 1, kh = wave >> 1;
       f32x16 acc = (f32x16){};
 #pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        const int kk = kh * 128 + st * 16 + 8 * h;
-        const vec8<T> af = load8(ds_s + r * DS_ROW + kk);
-        const vec8<T> bf = load8(kt_s + (dt * 32 + r) * KT_ROW + kk);
-        mma16(acc, af, bf);
+      for (int st = 0; st < 4; ++st) {
+        const int kk = kq * 64 + st * 16 + 8 * h;
+        mma16(acc, load8(ds_s + r * DS_ROW + kk), load8(kt_s + (dt_q * 32 + r) * KT_ROW + kk));
       }
-      if (kh == 1) {
+      if (kq > 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) xch[dt * 1024 + i * 64 + lane] = acc[i];
+        for (int i = 0; i < 16; ++i) xch[((kq - 1) * 2 + dt_q) * 1024 + i * 64 + lane] = acc[i];
       }
       __syncthreads();
-      if (kh == 0) {
+      if (kq == 0) {
         float* dst;
-        if (MODE == MODE_A1) dst = a.dq + bh * a.dq_bh;                            // rows = absolute query
-        else dst = a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;              // partial slab [kb]
+        if (MODE == MODE_A1) dst = a.dq + bh * a.dq_bh;
+        else dst = a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int qq = qa + acc_row(i, h);
-          dst[(size_t)qq * DH + dt * 32 + r] = acc[i] + xch[dt * 1024 + i * 64 + lane];
+          const float v = ((acc[i] + xch[(0 * 2 + dt_q) * 1024 + i * 64 + lane]) +
+                           xch[(1 * 2 + dt_q) * 1024 + i * 64 + lane]) + xch[(2 * 2 + dt_q) * 1024 + i * 64 + lane];
+          dst[(size_t)qq * DH + dt_q * 32 + r] = v;
         }
       }
     }
@@ -601,13 +684,15 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
 #pragma unroll
   for (int which = 0; which < 2; ++which) {
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < 2; ++dt) {
+      const f32x16& accv = which == 0 ? dvt[dt] : dkt[dt];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const f32x16& accv = which == 0 ? dvt[dt][kt] : dkt[dt][kt];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) stage[(mykey + kt * 32 + r) * 68 + dt * 32 + acc_row(i, h)] = accv[i];
+      for (int g4 = 0; g4 < 4; ++g4) {
+        // registers 4g4..4g4+3 hold d = dt*32 + 8*g4 + 4h + 0..3 for key mykey + r
+        *(f32x4*)(stage + (mykey + r) * 68 + dt * 32 + 8 * g4 + 4 * h) =
+            (f32x4){accv[4 * g4], accv[4 * g4 + 1], accv[4 * g4 + 2], accv[4 * g4 + 3]};
       }
+    }
     __syncthreads();
     float* dst;
     bool add = false;
@@ -617,7 +702,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
     } else {
       dst = (which == 0 ? a.dv : a.dk) + (size_t)blk * a.slab_stride + bh * (which == 0 ? a.dv_bh : a.dk_bh);
     }
-    for (int i = tid; i < NL * DH / 4; i += 256) {
+    for (int i = tid; i < NL * DH / 4; i += 512) {
       const int key = i >> 4, d4 = (i & 15) * 4;
       f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
       float* p = dst + (size_t)key * DH + d4;
@@ -630,10 +715,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(BwdArgs a) {
 
 template <typename T>
 constexpr size_t bwd_smem_bytes() {
-  constexpr size_t QT_ROW = 32 + 4, KT_ROW = NL + 16 / sizeof(T), DS_ROW = KT_ROW;
-  constexpr size_t main = (DH * KT_ROW + 32 * DS_ROW + 2 * DH * QT_ROW) * sizeof(T) + (2 * 1024 + 64) * 4;
-  constexpr size_t epi = (size_t)NL * 68 * 4;
-  return main > epi ? main : epi;
+  return BwdLay<T>::BYTES;
 }
 
 // ---------------------------------------------------------------------------
@@ -706,7 +788,7 @@ extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const vo
   float* pl = pm + (size_t)nkb * nbh * NL;
   hipStream_t st = (hipStream_t)stream;
   TM_DTYPE_DISPATCH(dtype, ({
-    const size_t sm = (size_t)NL * Lay<T>::KROW * sizeof(T) + (size_t)DH * Lay<T>::VROW * sizeof(T);
+    const size_t sm = ((size_t)NL * Lay<T>::KROW + Lay<T>::VELEMS) * sizeof(T);
     tm_allow_smem(a3_fwd_kernel<T>, sm);
     a3_fwd_kernel<T><<<dim3(nkb, nbh, 2), 256, sm, st>>>(ql, (const T*)k, (const T*)v, n, po, pm, pl);
   }));
@@ -716,16 +798,16 @@ extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const vo
   return 0;
 }
 
-extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const float* kl, const float* y,
+extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void* kl_t, const void* y_t,
                              const float* wconv, int nbh, int nh, int n, void* merged, float* lse1, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0 && nbh % nh == 0, "a1_fwd: bad shape");
   hipStream_t st = (hipStream_t)stream;
   TM_DTYPE_DISPATCH(dtype, ({
-    const size_t sm1 = (size_t)NL * Lay<T>::KROW * sizeof(T) + (size_t)DH * Lay<T>::VROW * sizeof(T);
+    const size_t sm1 = ((size_t)NL * Lay<T>::KROW + Lay<T>::VELEMS) * sizeof(T);
     const size_t sm = sm1 > 128 * 68 * 4 ? sm1 : 128 * 68 * 4;
     tm_allow_smem(a1_fwd_kernel<T>, sm);
-    a1_fwd_kernel<T><<<dim3(n / 128, nbh), 256, sm, st>>>((const T*)q, (const T*)v, kl, y, wconv, n, nh,
-                                                          (T*)merged, lse1);
+    a1_fwd_kernel<T><<<dim3(n / 128, nbh), 256, sm, st>>>((const T*)q, (const T*)v, (const T*)kl_t,
+                                                          (const T*)y_t, wconv, n, nh, (T*)merged, lse1);
   }));
   TM_CHECK_LAUNCH();
   return 0;
@@ -789,7 +871,7 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
   a.nh = nh; a.n_queries_per_wg = queries_per_wg; a.n_key_rows = NL;
   hipStream_t st = (hipStream_t)stream;
   TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A1>, bwd_smem_bytes<T>()),
-                            attn_bwd_kernel<T, MODE_A1><<<dim3(nqc, nbh), 256, bwd_smem_bytes<T>(), st>>>(a)));
+                            attn_bwd_kernel<T, MODE_A1><<<dim3(nqc, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
   TM_CHECK_LAUNCH();
   const long long cnt = (long long)nbh * NL * DH;
   int rc = tm_splitk_reduce(slab_k, dkl, nqc, cnt, 1.0f, accumulate, stream);
@@ -821,7 +903,7 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
   a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
   hipStream_t st = (hipStream_t)stream;
   TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A3>, bwd_smem_bytes<T>()),
-                            attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 256, bwd_smem_bytes<T>(), st>>>(a)));
+                            attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
   TM_CHECK_LAUNCH();
   return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, 1, stream);
 }

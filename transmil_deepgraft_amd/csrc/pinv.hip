@@ -51,15 +51,27 @@ __global__ __launch_bounds__(256) void bmm_kernel(JobPair jp, int nbatch) {
   const int nterms = J.A2 ? 2 : 1;
   const int kchunk = J.K * nterms / 4;
   f32x16 acc = (f32x16){};
-  for (int kk = wave * kchunk; kk < (wave + 1) * kchunk; kk += 16) {
-    const int term = kk / J.K, kl = kk % J.K;
-    const float* A = term ? J.A2 + bh * J.sa2 : J.A + bh * J.sa;
-    const float* B = term ? J.B2 + bh * J.sb2 : J.B + bh * J.sb;
-    const int ta = term ? J.ta2 : J.ta, tb = term ? J.tb2 : J.tb;
-    const int lda = term ? J.lda2 : J.lda, ldb = term ? J.ldb2 : J.ldb;
-    const f32x8 af = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
-    const f32x8 bf = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
-    mma16(acc, af, bf);
+  // all fragments of up to 4 k-steps are requested before the first MFMA, so the
+  // L2 round trips overlap instead of serialising step by step
+  for (int kb = wave * kchunk; kb < (wave + 1) * kchunk; kb += 64) {
+    f32x8 af[4], bf[4];
+    const int nst = min(4, ((wave + 1) * kchunk - kb) / 16);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s < nst) {
+        const int kk = kb + 16 * s;
+        const int term = kk / J.K, kl = kk % J.K;
+        const float* A = term ? J.A2 + bh * J.sa2 : J.A + bh * J.sa;
+        const float* B = term ? J.B2 + bh * J.sb2 : J.B + bh * J.sb;
+        const int ta = term ? J.ta2 : J.ta, tb = term ? J.tb2 : J.tb;
+        const int lda = term ? J.lda2 : J.lda, ldb = term ? J.ldb2 : J.ldb;
+        af[s] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
+        bf[s] = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      if (s < nst) mma16(acc, af[s], bf[s]);
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[wave][i][lane] = acc[i];

@@ -95,7 +95,7 @@ class Geometry:
 
 # ----------------------------------------------------------------------------- GEMM helpers
 def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c_dtype=None,
-         alpha=1.0, bias=None, gelu=False, pre=None, ld_pre=0, drop_p=0.0, seed=0, resid=None,
+         alpha=1.0, bias=None, gelu=False, pre=None, ld_pre=0, drop_p=0.0, seed=0, seed_ptr=None, resid=None,
          accumulate=False, rowmap=None, qkv=None, splits=1, k_per_split=None):
     g = GemmArgs()
     g.M, g.N, g.K = M, N, K
@@ -104,7 +104,7 @@ def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c
     g.ab_dtype = dtype
     g.c_dtype = dtype if c_dtype is None else c_dtype
     g.splits = splits
-    bk = 32 if dtype == BF16 else 16
+    bk = 64 if dtype == BF16 else 32
     if k_per_split is None:
         k_per_split = ((K + splits - 1) // splits + bk - 1) // bk * bk
     g.k_per_split = max(k_per_split, 1)
@@ -117,6 +117,7 @@ def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c
     g.drop_p = drop_p
     g.drop_scale = 1.0 / (1.0 - drop_p) if drop_p > 0 else 1.0
     g.seed = seed
+    g.seed_ptr = _p(seed_ptr)
     g.resid = _p(resid)
     g.accumulate = int(accumulate)
     if rowmap is not None:
@@ -134,7 +135,7 @@ def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool):
     if splits == 1:
         gemm(dY, X, out, M, N, K, lda=ldy, ldb=ldx, ldc=N, a_trans=1, b_kn=1, dtype=dtype, c_dtype=F32)
         return
-    bk = 32 if dtype == BF16 else 16
+    bk = 64 if dtype == BF16 else 32
     kps = ((K + splits - 1) // splits + bk - 1) // bk * bk
     splits = (K + kps - 1) // kps
     slab = work_pool(splits * M * N)
@@ -214,12 +215,15 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
         _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
     y = pool(nbh * NL * DH).view(nbh, NL, DH)
     bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh)
+    y_t = pool(nbh * NL * DH, tdtype)
+    _lib.call("tm_cast_f32", dt_code, _p(y), _p(y_t), nbh * NL * DH, st)
     merged = pool(geo.B * n * nh * DH, tdtype).view(geo.B, n, nh * DH)
     lse1 = pool(nbh * n)
     with probe("a1_fwd"):
-        _lib.call("tm_nys_a1_fwd", dt_code, _p(q), _p(v), _p(kl), _p(y), _p(wconv), nbh, nh, n, _p(merged),
+        _lib.call("tm_nys_a1_fwd", dt_code, _p(q), _p(v), _p(kl_t), _p(y_t), _p(wconv), nbh, nh, n, _p(merged),
                   _p(lse1), st)
-    state = dict(ql=ql, kl=kl, ql_t=ql_t, kl_t=kl_t, a2=a2, pinv=saved, z=z, w=w, lse3=lse3, y=y, lse1=lse1)
+    state = dict(ql=ql, kl=kl, ql_t=ql_t, kl_t=kl_t, a2=a2, pinv=saved, z=z, w=w, lse3=lse3, y=y, y_t=y_t,
+                 lse1=lse1)
     return merged, state
 
 
@@ -240,8 +244,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         _lib.call("tm_nys_conv_bwd", dt_code, _p(dmerged), _p(merged), _p(v), _p(wconv), nbh, nh, n, _p(dv),
                   _p(d1), _p(work), _p(dwconv_out), st)
     # A1 product backward: dq (complete), dkl, dY
-    y_t = pool(nbh * NL * DH, tdtype)
-    _lib.call("tm_cast_f32", dt_code, _p(state["y"]), _p(y_t), nbh * NL * DH, st)
+    y_t = state["y_t"]
     qpw = 256 if n % 256 == 0 else 32
     dkl = pool(nbh * NL * DH).view(nbh, NL, DH)
     dy = pool(nbh * NL * DH).view(nbh, NL, DH)
@@ -278,7 +281,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
 
 
 # ----------------------------------------------------------------------------- TransLayer
-def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, seed):
+def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, seed, seed_dev=None):
     """H [B*S, D] fp32 -> H + NystromAttention(LN(H)) (code/models/TransMIL.py:45-57)."""
     B, S, n, D, pad = geo.B, geo.S, geo.n, geo.D, geo.pad
     st = _stream()
@@ -294,8 +297,9 @@ def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, see
     merged, state = nystrom_core_forward(qkv, geo, prm["wconv"], tdtype, dt_code, pool)
     Hout = pool(B * S * D).view(B * S, D)
     gemm(merged, prm["wo"], Hout, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=dt_code, c_dtype=F32,
-         bias=prm["bo"], drop_p=drop_p, seed=seed, resid=H, rowmap=(n, pad, S, 0, 0, 0))
-    saved = dict(xn=xn, mean=mean, rstd=rstd, qkv=qkv, merged=merged, core=state, seed=seed, drop_p=drop_p)
+         bias=prm["bo"], drop_p=drop_p, seed=seed, seed_ptr=seed_dev, resid=H, rowmap=(n, pad, S, 0, 0, 0))
+    saved = dict(xn=xn, mean=mean, rstd=rstd, qkv=qkv, merged=merged, core=state, seed=seed, seed_dev=seed_dev,
+                 drop_p=drop_p)
     return Hout, saved
 
 
@@ -306,7 +310,7 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
     st = _stream()
     dout = pool(B * n * D, tdtype).view(B, n, D)
     _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
-              C.c_uint64(saved["seed"]), _p(dout), st)
+              C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(dout), st)
     # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
     weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code, work_pool=pool)
     colsum(dout, B * n, D, D, dt_code, grads["bo"], pool)
@@ -373,8 +377,12 @@ class TransMILEngine:
         p["fc_w"], p["fc_b"] = params["_fc.weight"], params["_fc.bias"]
         return p
 
-    def forward(self, x, params, drop_p=0.0, seeds=(0, 0)):
-        """x [B, N, F] fp32 (on the GPU) -> logits [B, C] fp32 and the saved context."""
+    def forward(self, x, params, drop_p=0.0, seeds=(0x1F123BB5, 0x2A9F4C61), seed_dev=None):
+        """x [B, N, F] fp32 (on the GPU) -> logits [B, C] fp32 and the saved context.
+
+        Dropout (train mode) hashes (row, col) with a per-layer seed; with ``seed_dev``
+        (a 1-element int64 device tensor) the seed is read on the device, so a
+        captured hipGraph draws a fresh mask every replay."""
         dev = x.device
         pool = Pool(dev)
         B, N, F = x.shape
@@ -392,10 +400,10 @@ class TransMILEngine:
         gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
              bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
         _lib.call("tm_put_cls", _p(prm["cls"]), B, geo.S, D, _p(H0), st)
-        H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0])
+        H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0], seed_dev)
         H2 = pool(B * geo.S * D).view(B * geo.S, D)
         _lib.call("tm_ppeg_fwd", _p(H1), B, geo.G, D, _p(prm["wfold"]), _p(prm["bfold"]), _p(H2), st)
-        H3, s2 = translayer_forward(H2, geo, prm[2], self.tdtype, self.dt_code, pool, drop_p, seeds[1])
+        H3, s2 = translayer_forward(H2, geo, prm[2], self.tdtype, self.dt_code, pool, drop_p, seeds[1], seed_dev)
         Ccls = prm["fc_w"].shape[0]
         logits = torch.empty(B, Ccls, dtype=torch.float32, device=dev)
         xhat = pool(B * D)
@@ -460,7 +468,7 @@ class NystromEngine:
         _lib.call("tm_cast_f32", self.dt_code, _p(w.contiguous()), _p(out), w.numel(), _stream())
         return out.view(w.shape)
 
-    def forward(self, x, wqkv, wo, bo, wconv, heads, drop_p=0.0, seed=0):
+    def forward(self, x, wqkv, wo, bo, wconv, heads, drop_p=0.0, seed=0, seed_dev=None):
         B, S, D = x.shape
         pool = Pool(x.device)
         geo = Geometry(B, max(S - 1, 1), D, D, heads)
@@ -479,9 +487,9 @@ class NystromEngine:
         merged, state = nystrom_core_forward(qkv, geo, wconv.contiguous(), self.tdtype, self.dt_code, pool)
         out = torch.empty(B, S, D, dtype=torch.float32, device=x.device)
         gemm(merged, wo_t, out, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=self.dt_code, c_dtype=F32,
-             bias=bo, drop_p=drop_p, seed=seed, rowmap=(n, pad, S, 0, 0, 0))
+             bias=bo, drop_p=drop_p, seed=seed, seed_ptr=seed_dev, rowmap=(n, pad, S, 0, 0, 0))
         ctx = dict(geo=geo, xp=xp, qkv=qkv, merged=merged, core=state, wqkv_t=wqkv_t, wo_t=wo_t,
-                   wconv=wconv.contiguous(), drop_p=drop_p, seed=seed)
+                   wconv=wconv.contiguous(), drop_p=drop_p, seed=seed, seed_dev=seed_dev)
         return out, ctx
 
     def backward(self, dout, ctx):
@@ -491,7 +499,7 @@ class NystromEngine:
         st = _stream()
         dpad = pool(B * n * D, self.tdtype).view(B, n, D)
         _lib.call("tm_dropout_bwd_pad", self.dt_code, _p(dout.contiguous()), B, S, n, pad, D,
-                  C.c_float(ctx["drop_p"]), C.c_uint64(ctx["seed"]), _p(dpad), st)
+                  C.c_float(ctx["drop_p"]), C.c_uint64(ctx["seed"]), _p(ctx["seed_dev"]), _p(dpad), st)
         dwo = torch.empty(D, D, dtype=torch.float32, device=dout.device)
         dbo = torch.empty(D, dtype=torch.float32, device=dout.device)
         weight_grad(dpad, ctx["merged"], dwo, D, D, B * n, ldy=D, ldx=D, dtype=self.dt_code, work_pool=pool)

@@ -43,7 +43,13 @@ def add_weight_decay(model: nn.Module, weight_decay: float = 1e-5, skip_list=())
 
 
 class Lookahead(torch.optim.Optimizer):
-    """Every k inner steps: slow += alpha * (fast - slow); fast = slow."""
+    """Every k inner steps: slow += alpha * (fast - slow); fast = slow.
+
+    Same schedule as the reference wrapper (code/MyOptimizer/lookahead.py; the
+    first sync only initialises the slow weights), but branch-free on the device:
+    the step counter and the "slow weights initialised" flag are device scalars
+    and the update is masked, so the whole optimizer step can be captured in a
+    hipGraph and replayed."""
 
     def __init__(self, base: torch.optim.Optimizer, alpha: float = 0.5, k: int = 6):
         if not 0.0 <= alpha <= 1.0 or k < 1:
@@ -52,32 +58,39 @@ class Lookahead(torch.optim.Optimizer):
         self.param_groups = base.param_groups
         self.defaults = dict(base.defaults, lookahead_alpha=alpha, lookahead_k=k, lookahead_step=0)
         self.state = defaultdict(dict)
+        self._dev = None
         for g in self.param_groups:
             g.setdefault("lookahead_alpha", alpha)
             g.setdefault("lookahead_k", k)
             g.setdefault("lookahead_step", 0)
 
     @torch.no_grad()
-    def _sync_group(self, g):
+    def _sync_group(self, gi, g):
         fast = [p for p in g["params"] if p.grad is not None]
         if not fast:
             return
-        slow = []
-        for p in fast:
-            st = self.state[p]
-            if "slow_buffer" not in st:
-                st["slow_buffer"] = p.detach().clone()
-            slow.append(st["slow_buffer"])
+        key = ("group", gi)
+        st = self.state[key]
+        if "slow" not in st:
+            dev = fast[0].device
+            st["slow"] = [torch.zeros_like(p) for p in fast]
+            st["step"] = torch.zeros((), device=dev)
+            st["init"] = torch.zeros((), device=dev)
+        slow, step, init = st["slow"], st["step"], st["init"]
+        step.add_(1.0)
+        m = (torch.remainder(step, float(g["lookahead_k"])) == 0).float()
+        coef = m * (1.0 - init * (1.0 - g["lookahead_alpha"]))
         diff = torch._foreach_sub(fast, slow)
-        torch._foreach_add_(slow, diff, alpha=g["lookahead_alpha"])
-        torch._foreach_copy_(fast, slow)
+        torch._foreach_add_(slow, torch._foreach_mul(diff, coef))
+        back = torch._foreach_sub(slow, fast)
+        torch._foreach_add_(fast, torch._foreach_mul(back, m))
+        torch.maximum(init, m, out=init)
 
     def step(self, closure=None):
         loss = self.base_optimizer.step(closure)
-        for g in self.param_groups:
+        for gi, g in enumerate(self.param_groups):
             g["lookahead_step"] += 1
-            if g["lookahead_step"] % g["lookahead_k"] == 0:
-                self._sync_group(g)
+            self._sync_group(gi, g)
         return loss
 
     def zero_grad(self, set_to_none: bool = True):
@@ -97,7 +110,7 @@ def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float =
     name = parts[-1]
     fused = torch.cuda.is_available()
     if name == "radam":
-        base = torch.optim.RAdam(params, foreach=True, **kw)
+        base = torch.optim.RAdam(params, foreach=True, capturable=fused, **kw)
     elif name == "adam":
         base = torch.optim.Adam(params, foreach=not fused, fused=fused, **kw)
     elif name == "adamw":

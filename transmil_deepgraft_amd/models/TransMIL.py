@@ -62,9 +62,9 @@ class PPEG(nn.Module):
 
 class _TransMILFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine, names, drop_p, seeds, holder, x, *params):
+    def forward(ctx, engine, names, drop_p, seed_dev, holder, x, *params):
         prm = dict(zip(names, params))
-        logits, c = engine.forward(x, prm, drop_p, seeds)
+        logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev)
         ctx.engine, ctx.c, ctx.names, ctx.prm = engine, c, names, prm
         if holder is not None:
             holder["ctx"] = c
@@ -94,6 +94,10 @@ class TransMIL(nn.Module):
         self.norm = norm_layer(out_features)
         self._fc = nn.Linear(out_features, self.n_classes)
         self.compute_dtype = torch.bfloat16
+        # dropout stream: a device-side counter advanced by every train-mode forward
+        # (hipGraph-safe); seeded from torch's generator so torch.manual_seed pins it
+        self.register_buffer("_dropout_counter", torch.randint(0, 2 ** 62, (1,), dtype=torch.int64),
+                             persistent=False)
 
     def set_compute_dtype(self, dtype):
         """torch.bfloat16 (bench) or torch.float32 (parity); propagates to submodules."""
@@ -120,10 +124,13 @@ class TransMIL(nn.Module):
         names = tuple(n for n, _ in self.named_parameters())
         params = tuple(p for _, p in self.named_parameters())
         drop_p = self.layer1.attn.to_out[1].p if self.training else 0.0
-        seeds = tuple(int(s) for s in torch.randint(0, 2 ** 62, (2,))) if drop_p > 0 else (0, 0)
+        seed_dev = None
+        if drop_p > 0:
+            self._dropout_counter.add_(1)
+            seed_dev = self._dropout_counter.clone()   # snapshot for this forward's backward
         holder = {} if return_attn else None
         engine = TransMILEngine(self.compute_dtype)
-        logits = _TransMILFn.apply(engine, names, drop_p, seeds, holder, x, *params)
+        logits = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, x, *params)
         if return_attn:
             c = holder["ctx"]
             S = c["geo"].S

@@ -34,8 +34,8 @@ def _check_dtype(dtype):
 
 class _NystromFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine, heads, drop_p, seed, x, wqkv, wo, bo, wconv):
-        out, c = engine.forward(x, wqkv, wo, bo, wconv, heads, drop_p, seed)
+    def forward(ctx, engine, heads, drop_p, seed_dev, x, wqkv, wo, bo, wconv):
+        out, c = engine.forward(x, wqkv, wo, bo, wconv, heads, drop_p, 0x51ED27, seed_dev)
         ctx.engine, ctx.c = engine, c
         return out
 
@@ -64,6 +64,8 @@ class NystromAttention(nn.Module):
             k = residual_conv_kernel
             self.res_conv = nn.Conv2d(heads, heads, (k, 1), padding=(k // 2, 0), groups=heads, bias=False)
         self.compute_dtype = torch.bfloat16
+        self.register_buffer("_dropout_counter", torch.randint(0, 2 ** 62, (1,), dtype=torch.int64),
+                             persistent=False)
 
     def _supported(self, mask):
         if mask is not None:
@@ -80,8 +82,11 @@ class NystromAttention(nn.Module):
             raise RuntimeError("HIP NystromAttention needs a GPU tensor (no CPU path)")
         engine = NystromEngine(_check_dtype(self.compute_dtype))
         drop_p = self.to_out[1].p if self.training else 0.0
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop_p > 0 else 0
-        out = _NystromFn.apply(engine, self.heads, drop_p, seed, x.float(), self.to_qkv.weight,
+        seed_dev = None
+        if drop_p > 0:
+            self._dropout_counter.add_(1)
+            seed_dev = self._dropout_counter.clone()
+        out = _NystromFn.apply(engine, self.heads, drop_p, seed_dev, x.float(), self.to_qkv.weight,
                                self.to_out[0].weight, self.to_out[0].bias, self.res_conv.weight)
         if return_attn:
             return out, self._attn_matrix(x)
