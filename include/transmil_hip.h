@@ -134,12 +134,15 @@ typedef struct tm_bmm_job {
   float* C; int ldc; long long sc;
   int M, N, K;
 } tm_bmm_job;
-int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, void* stream);
+/* prec 0: exact fp32 MFMA; prec 1: bf16x3 (hi/lo split, ~16-bit operands, fp32 accumulate) */
+int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream);
+/* microbenchmark ablation switch (which = 0: bmm kernel variant); not for production use */
+void tm_debug_set_variant(int which, int value);
 long long tm_pinv_saved_floats(int nbh, int iters);
-int tm_pinv_fwd(const float* X, int nbh, int iters, float* saved, void* stream);
+int tm_pinv_fwd(const float* X, int nbh, int iters, int prec, float* saved, void* stream);
 long long tm_pinv_bwd_workspace_floats(int nbh);
-int tm_pinv_bwd(const float* X, int nbh, int iters, const float* saved, float* dZ, float* work, float* dX,
-                void* stream);
+int tm_pinv_bwd(const float* X, int nbh, int iters, int prec, const float* saved, float* dZ, float* work,
+                float* dX, void* stream);
 
 /* ---- PPEG (ppeg.hip) -- code/models/TransMIL.py:60-75 -------------------- */
 int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, const float* b5, const float* w3,
@@ -159,6 +162,31 @@ int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int 
 int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, int pad, int D, void* y, void* stream);
 int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
                     void* dpre, float* dcls, void* stream);
+
+/* ---- optimizer step (optim.hip) ----------------------------------------
+ * torch.optim.RAdam (L2 decay, code/MyOptimizer/optim_factory.py:77-79) + the
+ * Lookahead sync (code/MyOptimizer/lookahead.py, wrapped at optim_factory.py:118-121)
+ * over up to 40 parameter tensors in one launch.  exp_avg / exp_avg_sq / slow are
+ * flat fp32 buffers indexed by the table's prefix offsets; counters (int32[2], device)
+ * hold the RAdam and Lookahead step counts and are advanced by the call itself.
+ * lookahead_k == 0 disables the sync (plain RAdam). */
+#define TM_OPTIM_MAX_TENSORS 40
+typedef struct tm_optim_tensor {
+  float* param;
+  const float* grad;
+  long long numel;
+  float lr;
+  float weight_decay;
+} tm_optim_tensor;
+typedef struct tm_optim_table {
+  int count;
+  int reserved;
+  long long offset[TM_OPTIM_MAX_TENSORS + 1];
+  tm_optim_tensor t[TM_OPTIM_MAX_TENSORS];
+} tm_optim_table;
+int tm_radam_lookahead_step(const tm_optim_table* table, float* exp_avg, float* exp_avg_sq, float* slow,
+                            int* counters, float beta1, float beta2, float eps, int lookahead_k,
+                            float lookahead_alpha, void* stream);
 
 #ifdef __cplusplus
 }

@@ -22,15 +22,33 @@ from transmil_deepgraft_amd import engine as E  # noqa: E402
 from transmil_deepgraft_amd._lib import BF16, F32  # noqa: E402
 
 
-def timeit(fn, reps):
+def timeit(fn, reps, graph=True):
+    """GPU time per call: `reps` calls captured in one hipGraph and replayed, so the
+    Python/launch cost of a call does not hide short kernels (eager if graph=False)."""
     fn()
     torch.cuda.synchronize()
+    g = None
+    if graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            fn()
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        torch.cuda.synchronize()
     out = []
     for _ in range(5):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        for _ in range(reps):
-            fn()
+        if g is not None:
+            g.replay()
+        else:
+            for _ in range(reps):
+                fn()
         e.record()
         torch.cuda.synchronize()
         out.append(s.elapsed_time(e) / reps * 1e3)
@@ -42,6 +60,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
+    ap.add_argument("--eager", action="store_true")
     args = ap.parse_args()
     dev = "cuda"
     N = args.n
@@ -55,7 +74,7 @@ def main():
     def case(name, fn, flops=None, byts=None):
         if args.only and args.only not in name:
             return
-        us = timeit(fn, args.reps)
+        us = timeit(fn, args.reps, graph=not args.eager)
         extra = ""
         if flops:
             extra += f" {flops / us / 1e6:8.1f} TF/s"
@@ -77,10 +96,14 @@ def main():
     case("bmm TN 256^3 x8", lambda: E.bmm([E.bmm_job(X, 1, Z, 0, P, 256, 256, 256)], nbh), f)
     case("bmm 2-job 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
                                               E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh), 2 * f)
+    case("bmm NN 256^3 x8 [bf16x3]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh, 1), f)
+    case("bmm 2-job 256^3 x8 [bf16x3]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
+                                              E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh, 1), 2 * f)
     case("bmm Y=ZW 256x64x256 x8", lambda: E.bmm([E.bmm_job(Z, 0, W, 0, Y, 256, 64, 256)], nbh), f // 4)
     case("torch bmm fp32 256^3 x8", lambda: torch.bmm(X, Z, out=P), f)
     saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=dev)
-    case("pinv_fwd (26 launches)", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, E._p(saved), st()), 24 * f)
+    case("pinv_fwd (26 launches)", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 0, E._p(saved), st()), 24 * f)
+    case("pinv_fwd [bf16x3]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 1, E._p(saved), st()), 24 * f)
     # ---------------- GEMMs ----------------
     pool = E.Pool(dev)
     xn = torch.randn(n, 512, device=dev).to(bf)
@@ -146,6 +169,11 @@ def main():
     case("a1_fwd", lambda: _lib.call("tm_nys_a1_fwd", BF16, E._p(q), E._p(v), E._p(kl_t), E._p(y_t), E._p(wconv),
                                      nbh, 8, n, E._p(merged), E._p(lse1), st()),
          4 * nbh * n * 256 * 64, 3 * n * 512 * 2)
+    for var, nm in ((1, "no conv"), (2, "no MFMA")):
+        _lib.lib().tm_debug_set_variant(1, var)
+        case(f"a1_fwd [{nm}]", lambda: _lib.call("tm_nys_a1_fwd", BF16, E._p(q), E._p(v), E._p(kl_t), E._p(y_t),
+                                                E._p(wconv), nbh, 8, n, E._p(merged), E._p(lse1), st()))
+    _lib.lib().tm_debug_set_variant(1, 0)
     dmerged = torch.randn(1, n, 512, device=dev).to(bf)
     dv = torch.empty(nbh, n, 64, device=dev)
     d1 = torch.empty(nbh, n, device=dev)

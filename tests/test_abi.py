@@ -38,12 +38,14 @@ def test_struct_layouts_match_c(tmp_path):
     """Every field offset of the ctypes mirrors equals the C compiler's offsetof()."""
     import shutil
     import subprocess
-    from transmil_deepgraft_amd._lib import GemmArgs, BmmJob
+    from transmil_deepgraft_amd._lib import GemmArgs, BmmJob, OptimTensor, OptimTable
+    structs = (("tm_gemm_args", GemmArgs), ("tm_bmm_job", BmmJob), ("tm_optim_tensor", OptimTensor),
+               ("tm_optim_table", OptimTable))
     cc = shutil.which("gcc") or shutil.which("cc")
     if cc is None:
         pytest.skip("no C compiler")
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', 'int main(void) {']
-    for cname, cls in (("tm_gemm_args", GemmArgs), ("tm_bmm_job", BmmJob)):
+    for cname, cls in structs:
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
         for fname, _ in cls._fields_:
             lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
@@ -58,7 +60,7 @@ def test_struct_layouts_match_c(tmp_path):
         if line:
             a, b, c = line.split()
             got[(a, b)] = int(c)
-    for cname, cls in (("tm_gemm_args", GemmArgs), ("tm_bmm_job", BmmJob)):
+    for cname, cls in structs:
         assert got[(cname, "size")] == ctypes.sizeof(cls), cname
         for fname, _ in cls._fields_:
             assert got[(cname, fname)] == getattr(cls, fname).offset, (cname, fname)

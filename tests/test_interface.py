@@ -1,0 +1,159 @@
+"""The Lightning-step surface (transmil_deepgraft_amd/interface.py) on CPU, plus the
+fused RAdam+Lookahead kernel and the multi-rank gradient all-reduce.
+
+The Lookahead reference semantics are restated from code/MyOptimizer/lookahead.py
+(update_slow: the first sync copies fast -> slow, then slow += alpha (fast - slow),
+fast = slow; every k-th step of the wrapper)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.nn as nn
+
+
+class RefLookahead:
+    """code/MyOptimizer/lookahead.py step()/update_slow(), per-parameter slow buffers."""
+
+    def __init__(self, base, alpha=0.5, k=6):
+        self.base, self.alpha, self.k, self.n = base, alpha, k, 0
+        self.slow = {}
+
+    @torch.no_grad()
+    def step(self):
+        self.base.step()
+        self.n += 1
+        if self.n % self.k:
+            return
+        for g in self.base.param_groups:
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                if p not in self.slow:
+                    self.slow[p] = p.detach().clone()
+                s = self.slow[p]
+                s.add_(p.detach() - s, alpha=self.alpha)
+                p.copy_(s)
+
+
+def _toy(seed=0, device="cpu"):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Linear(16, 32), nn.GELU(), nn.LayerNorm(32), nn.Linear(32, 3)).to(device)
+
+
+def _grads(model, step):
+    g = torch.Generator().manual_seed(100 + step)
+    for p in model.parameters():
+        p.grad = (torch.randn(p.shape, generator=g) * 0.1).to(p.device)
+
+
+def test_add_weight_decay_groups():
+    from transmil_deepgraft_amd.interface import add_weight_decay
+    m = _toy()
+    groups = add_weight_decay(m, 0.01)
+    nd = {id(p) for p in groups[0]["params"]}
+    dc = {id(p) for p in groups[1]["params"]}
+    assert groups[0]["weight_decay"] == 0.0 and groups[1]["weight_decay"] == 0.01
+    for name, p in m.named_parameters():
+        expect_nd = p.dim() == 1 or name.endswith(".bias")
+        assert (id(p) in nd) == expect_nd and (id(p) in dc) == (not expect_nd), name
+
+
+def test_device_lookahead_matches_reference_semantics():
+    from transmil_deepgraft_amd.interface import Lookahead, add_weight_decay
+    a, b = _toy(1), _toy(1)
+    opt_a = Lookahead(torch.optim.RAdam(add_weight_decay(a, 0.01), lr=2e-3))
+    opt_b = RefLookahead(torch.optim.RAdam(add_weight_decay(b, 0.01), lr=2e-3))
+    for step in range(20):
+        _grads(a, step)
+        _grads(b, step)
+        opt_a.step()
+        opt_b.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=0, atol=1e-7)
+
+
+def test_task_surface_cpu():
+    """training_step(batch) -> loss [1]; configure_optimizers() -> ([opt], [sched dict])."""
+    from transmil_deepgraft_amd.interface import TransMILTask, Lookahead
+
+    class Tiny(nn.Module):
+        n_classes = 3
+
+        def __init__(self):
+            super().__init__()
+            self.fc = nn.Linear(8, 3)
+
+        def forward(self, x):
+            return self.fc(x.mean(1))
+
+    task = TransMILTask(Tiny())
+    loss = task.training_step((torch.rand(2, 5, 8), torch.tensor([0, 2]), (["a", "b"], ["p", "q"])))
+    assert loss.shape == (1,)
+    opts, scheds = task.configure_optimizers()
+    assert isinstance(opts[0], Lookahead)
+    assert scheds[0]["monitor"] == "val_loss" and scheds[0]["frequency"] == 10
+    assert isinstance(scheds[0]["scheduler"], torch.optim.lr_scheduler.ReduceLROnPlateau)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _allreduce_worker(rank, world, port, out):
+    import torch.distributed as dist
+    from transmil_deepgraft_amd.interface import GradAllReduce
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    m = _toy(0)
+    ar = GradAllReduce(m.parameters())
+    _grads(m, rank)
+    ar()
+    out[rank] = [p.grad.clone() for p in m.parameters()]
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_gloo_world2():
+    """Two ranks (gloo, CPU): every rank ends with the mean of the ranks' gradients."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_allreduce_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    m0, m1 = _toy(0), _toy(0)
+    _grads(m0, 0)
+    _grads(m1, 1)
+    for i, (p0, p1) in enumerate(zip(m0.parameters(), m1.parameters())):
+        mean = (p0.grad + p1.grad) / 2
+        torch.testing.assert_close(res[0][i], mean)
+        torch.testing.assert_close(res[1][i], mean)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [6, 0])
+def test_fused_radam_lookahead_matches_torch(k):
+    """tm_radam_lookahead_step vs torch.optim.RAdam (+ reference Lookahead) over 20 steps,
+    covering the un-rectified first steps (rho_t <= 5), two syncs and L2 decay groups."""
+    from transmil_deepgraft_amd.interface import FusedRAdamLookahead, add_weight_decay
+    a, b = _toy(2, "cuda"), _toy(2, "cuda")
+    opt_a = FusedRAdamLookahead(add_weight_decay(a, 0.05), lr=3e-3, lookahead_k=k)
+    base = torch.optim.RAdam(add_weight_decay(b, 0.05), lr=3e-3)
+    opt_b = RefLookahead(base) if k else base
+    for step in range(20):
+        _grads(a, step)
+        _grads(b, step)
+        opt_a.step()
+        opt_b.step()
+    torch.cuda.synchronize()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=2e-5, atol=2e-6)
+    sd = opt_a.state_dict()
+    assert int(sd["fused_counters"][0]) == 20
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        sa, sb = opt_a.state[pa], base.state[pb]
+        torch.testing.assert_close(sa["exp_avg"], sb["exp_avg"], rtol=2e-5, atol=1e-8)
+        torch.testing.assert_close(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=2e-5, atol=1e-10)

@@ -160,7 +160,47 @@ def test_ppeg_fwd_bwd(G):
         assert _rel(p1.grad.cpu(), p2.grad) < 1e-4, n1
 
 
+# ----------------------------------------------------------------------------- bmm
+@pytest.mark.parametrize("prec,tol", [(0, 2e-6), (1, 3e-5)])
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("K", [64, 256])
+def test_bmm_batched_epilogue(prec, tol, ta, tb, K):
+    """C = alpha*op(A) op(B) + diag*I + e1*E1 + e2*E2, fp32 in/out; prec 1 = bf16x3 split."""
+    from transmil_deepgraft_amd.engine import bmm, bmm_job
+    nb, M, N = 3, 256, 64 if K == 256 else 256
+    g = torch.Generator().manual_seed(K + 4 * ta + 2 * tb + prec)
+    A = torch.randn(nb, M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(nb, K, N, generator=g, dtype=torch.float64)
+    E1 = torch.randn(nb, M, N, generator=g, dtype=torch.float64)
+    E2 = torch.randn(nb, M, N, generator=g, dtype=torch.float64)
+    ref = 0.7 * A @ B + 0.5 * E1 - 2.0 * E2
+    ref += 3.0 * torch.eye(M, N, dtype=torch.float64)
+    Ad = (A.transpose(1, 2) if ta else A).contiguous().float().to(DEV)
+    Bd = (B.transpose(1, 2) if tb else B).contiguous().float().to(DEV)
+    out = torch.empty(nb, M, N, device=DEV)
+    bmm([bmm_job(Ad, ta, Bd, tb, out, M, N, K, alpha=0.7, diag=3.0, E1=E1.float().to(DEV), e1=0.5,
+                 E2=E2.float().to(DEV), e2=-2.0)], nb, prec)
+    torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < tol
+
+
 # ----------------------------------------------------------------------------- pinv
+def test_pinv_bf16x3_close_to_exact():
+    """The bench mode's bf16x3 products keep the 6 Newton-Schulz steps within 1e-4."""
+    from transmil_deepgraft_amd import _lib
+    from transmil_deepgraft_amd.engine import _p, _stream
+    nbh = 8
+    g = torch.Generator().manual_seed(8)
+    X = torch.softmax(torch.randn(nbh, 256, 256, generator=g) * 0.3, dim=-1).to(DEV)
+    zs = []
+    for prec in (0, 1):
+        saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=DEV)
+        _lib.call("tm_pinv_fwd", _p(X), nbh, 6, prec, _p(saved), _stream())
+        zs.append(saved[6 * nbh * 65536:7 * nbh * 65536].clone())
+    torch.cuda.synchronize()
+    assert _rel(zs[1].cpu(), zs[0].cpu()) < 1e-4
+
+
 def test_pinv_fwd_bwd_fp32_exact_path():
     """Z = pinv(softmax(s)); compare Z and dL/ds.  dL/dA2 itself is not compared: the
     max(rowsum) term of Z0's scale adds a row-constant gradient that torch gives to
@@ -179,12 +219,12 @@ def test_pinv_fwd_bwd_fp32_exact_path():
     z_ref.backward(gz)
     X = a.float().to(DEV)
     saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=DEV)
-    _lib.call("tm_pinv_fwd", _p(X), nbh, 6, _p(saved), _stream())
+    _lib.call("tm_pinv_fwd", _p(X), nbh, 6, 0, _p(saved), _stream())
     z = saved[6 * nbh * 65536:7 * nbh * 65536].view(nbh, 256, 256)
     dz = gz.float().to(DEV).contiguous()
     work = torch.empty(_lib.query("tm_pinv_bwd_workspace_floats", nbh), device=DEV)
     dX = torch.empty(nbh, 256, 256, device=DEV)
-    _lib.call("tm_pinv_bwd", _p(X), nbh, 6, _p(saved), _p(dz), _p(work), _p(dX), _stream())
+    _lib.call("tm_pinv_bwd", _p(X), nbh, 6, 0, _p(saved), _p(dz), _p(work), _p(dX), _stream())
     ds = torch.empty_like(dX)
     _lib.call("tm_softmax_bwd_rows256", _p(X), _p(dX), _p(ds), nbh * 256, _stream())
     torch.cuda.synchronize()

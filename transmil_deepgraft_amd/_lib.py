@@ -40,6 +40,18 @@ class BmmJob(C.Structure):
                 ("C", P), ("ldc", I), ("sc", L), ("M", I), ("N", I), ("K", I)]
 
 
+OPTIM_MAX_TENSORS = 40
+
+
+class OptimTensor(C.Structure):
+    _fields_ = [("param", P), ("grad", P), ("numel", L), ("lr", Fl), ("weight_decay", Fl)]
+
+
+class OptimTable(C.Structure):
+    _fields_ = [("count", I), ("reserved", I), ("offset", L * (OPTIM_MAX_TENSORS + 1)),
+                ("t", OptimTensor * OPTIM_MAX_TENSORS)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "tm_last_error": (C.c_char_p, []),
@@ -68,11 +80,12 @@ _SIGS = {
     "tm_nys_a3_bwd_workspace": (L, [I, I]),
     "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, P]),
     "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
-    "tm_bmm": (I, [C.POINTER(BmmJob), I, I, P]),
+    "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
+    "tm_debug_set_variant": (None, [I, I]),
     "tm_pinv_saved_floats": (L, [I, I]),
-    "tm_pinv_fwd": (I, [P, I, I, P, P]),
+    "tm_pinv_fwd": (I, [P, I, I, I, P, P]),
     "tm_pinv_bwd_workspace_floats": (L, [I]),
-    "tm_pinv_bwd": (I, [P, I, I, P, P, P, P, P]),
+    "tm_pinv_bwd": (I, [P, I, I, I, P, P, P, P, P]),
     "tm_ppeg_fold": (I, [P, P, P, P, P, P, I, P, P, P]),
     "tm_ppeg_fwd": (I, [P, I, I, I, P, P, P, P]),
     "tm_ppeg_bwd_workspace": (L, [I, I, I]),
@@ -81,6 +94,7 @@ _SIGS = {
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),
+    "tm_radam_lookahead_step": (I, [C.POINTER(OptimTable), P, P, P, P, Fl, Fl, Fl, I, Fl, P]),
 }
 
 EXPORTED = tuple(_SIGS)

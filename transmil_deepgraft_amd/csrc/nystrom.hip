@@ -225,7 +225,11 @@ TM_DEV void stage_values(T* vs, const T* src, int tid) {
 // A1 path forward.  grid (n/128, nbh), block 256 (4 waves x 32 queries).
 //   merged[bag][t][head*64+d] = softmax_j(q_t . kl_j) . Y_j  + sum_tau w[head][tau] v[t+tau-16][d]
 //   lse1[bh][t] saved for backward.
-template <typename T>
+constexpr int A1_VS = 66;  // conv window row stride (floats): a wave's 2 query groups hit distinct banks
+constexpr int A1_WIN_ITEMS = (128 + 2 * HALF) * 8 / 256;
+constexpr size_t A1_EPI_BYTES = (128 * 68 + (128 + 2 * HALF) * A1_VS) * sizeof(float);
+
+template <typename T, int VAR = 0>   // VAR (ablation): 1 = no conv taps, 2 = no MFMA phase
 __global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, const T* __restrict__ v,
                                                      const T* __restrict__ kl_t, const T* __restrict__ y_t,
                                                      const float* __restrict__ wconv, int n, int nh,
@@ -249,9 +253,24 @@ __global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, co
   __syncthreads();
   f32x16 o[2];
   float mx, sum;
-  attn_fwd_wave<T>(ks, vt, qf, o, mx, sum, lane);
+  if constexpr (VAR == 2) {
+    o[0] = (f32x16){}; o[1] = (f32x16){};
+    mx = to_f(qf[0][0]); sum = 1.f + to_f(ks[lane]) + to_f(vt[lane]);
+  } else {
+    attn_fwd_wave<T>(ks, vt, qf, o, mx, sum, lane);
+  }
   if (h == 0) lse1[(size_t)bh * n + qrow] = mx + __logf(sum);
   const float inv = 1.0f / sum;
+  // conv window: v rows [t0 - 16, t0 + 144) of this head, requested now (5 x 16 B per
+  // thread) so the loads overlap the normalisation / LDS round trip below.
+  const T* vb = v + (size_t)bh * n * DH;
+  vec8<T> vwin[A1_WIN_ITEMS];
+#pragma unroll
+  for (int i = 0; i < A1_WIN_ITEMS; ++i) {
+    const int it = tid + 256 * i, row = it >> 3, src = t0 - HALF + row;
+    if (src >= 0 && src < n) vwin[i] = load8(vb + (size_t)src * DH + (it & 7) * 8);
+    else vwin[i] = vec8<T>{};
+  }
   __syncthreads();  // everyone done reading ks/vt
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
@@ -263,29 +282,48 @@ __global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, co
       val[2] = o[dt][4 * g4 + 2] * inv; val[3] = o[dt][4 * g4 + 3] * inv;
       *(f32x4*)(ost + (wave * 32 + r) * 68 + d0) = val;
     }
+  float* vs = ost + 128 * 68;  // [160][A1_VS] fp32 window
+#pragma unroll
+  for (int i = 0; i < A1_WIN_ITEMS; ++i) {
+    const int it = tid + 256 * i, row = it >> 3, dc = (it & 7) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; e += 2)
+      *(float2*)(vs + row * A1_VS + dc + e) = make_float2(to_f(vwin[i][e]), to_f(vwin[i][e + 1]));
+  }
   __syncthreads();
-  // conv residual + coalesced store: item = (query, 8 d)
-  float w[TAPS];
+  // conv residual, register-blocked: thread = (16 consecutive queries, 2 d); every window
+  // row is read once from LDS and feeds up to 16 outputs.
+  if constexpr (VAR != 1) {
+    const int dp = tid & 31, qb = tid >> 5;
+    const float* wc = wconv + head * TAPS;
+    float w[TAPS];
 #pragma unroll
-  for (int tau = 0; tau < TAPS; ++tau) w[tau] = wconv[head * TAPS + tau];
-  const T* vb = v + (size_t)bh * n * DH;
-  for (int it = tid; it < 128 * 8; it += 256) {
-    const int ql = it >> 3, dc = (it & 7) * 8, t = t0 + ql;
-    float acc[8];
+    for (int tau = 0; tau < TAPS; ++tau) w[tau] = wc[tau];
+    float2 acc[16];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = ost[ql * 68 + dc + e];
+    for (int j = 0; j < 16; ++j) acc[j] = *(const float2*)(ost + (qb * 16 + j) * 68 + 2 * dp);
 #pragma unroll
-    for (int tau = 0; tau < TAPS; ++tau) {
-      const int src = t + tau - HALF;
-      if (src >= 0 && src < n) {
-        const vec8<T> vv = load8(vb + (size_t)src * DH + dc);
+    for (int i = 0; i < 16 + 2 * HALF; ++i) {
+      const float2 x = *(const float2*)(vs + (qb * 16 + i) * A1_VS + 2 * dp);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] = fmaf(w[tau], to_f(vv[e]), acc[e]);
+      for (int j = 0; j < 16; ++j) {
+        const int tau = i - j;
+        if (tau >= 0 && tau < TAPS) {
+          acc[j].x = fmaf(w[tau], x.x, acc[j].x);
+          acc[j].y = fmaf(w[tau], x.y, acc[j].y);
+        }
       }
     }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) *(float2*)(ost + (qb * 16 + j) * 68 + 2 * dp) = acc[j];
+    __syncthreads();
+  }
+  // coalesced store: item = (query, 8 d)
+  for (int it = tid; it < 128 * 8; it += 256) {
+    const int ql = it >> 3, dc = (it & 7) * 8, t = t0 + ql;
     vec8<T> outv;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) outv[e] = from_f<T>(acc[e]);
+    for (int e = 0; e < 8; ++e) outv[e] = from_f<T>(ost[ql * 68 + dc + e]);
     store8(merged + ((size_t)bag * n + t) * (nh * DH) + head * DH + dc, outv);
   }
 }
@@ -514,6 +552,7 @@ struct BwdArgs {
 };
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
+int g_nys_variant = 0;
 
 template <typename T> struct BwdLay {
   static constexpr int QT_ROW = 32 + 4;              // Q^T / dO^T chunk [64 d][36]
@@ -746,6 +785,7 @@ __global__ void assemble_dqkv_kernel(const float* __restrict__ dq, const float* 
 }  // namespace
 
 // ============================ C entry points ===============================
+extern "C" void tm_debug_set_nys_variant(int value) { g_nys_variant = value; }
 
 #define TM_DTYPE_DISPATCH(dt, CALL)                               \
   if ((dt) == TM_BF16) { using T = bf16; CALL; }                  \
@@ -804,10 +844,11 @@ extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void
   hipStream_t st = (hipStream_t)stream;
   TM_DTYPE_DISPATCH(dtype, ({
     const size_t sm1 = ((size_t)NL * Lay<T>::KROW + Lay<T>::VELEMS) * sizeof(T);
-    const size_t sm = sm1 > 128 * 68 * 4 ? sm1 : 128 * 68 * 4;
-    tm_allow_smem(a1_fwd_kernel<T>, sm);
-    a1_fwd_kernel<T><<<dim3(n / 128, nbh), 256, sm, st>>>((const T*)q, (const T*)v, (const T*)kl_t,
-                                                          (const T*)y_t, wconv, n, nh, (T*)merged, lse1);
+    const size_t sm = sm1 > A1_EPI_BYTES ? sm1 : A1_EPI_BYTES;
+    auto kern = g_nys_variant == 1 ? a1_fwd_kernel<T, 1> : g_nys_variant == 2 ? a1_fwd_kernel<T, 2> : a1_fwd_kernel<T, 0>;
+    tm_allow_smem(kern, sm);
+    kern<<<dim3(n / 128, nbh), 256, sm, st>>>((const T*)q, (const T*)v, (const T*)kl_t,
+                                              (const T*)y_t, wconv, n, nh, (T*)merged, lse1);
   }));
   TM_CHECK_LAUNCH();
   return 0;

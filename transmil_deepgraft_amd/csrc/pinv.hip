@@ -23,6 +23,8 @@ constexpr int NL = 256;
 
 struct JobPair { tm_bmm_job j[2]; int tiles0; };
 
+
+
 TM_DEV f32x8 frag_a(const float* A, int ta, int lda, int m, int k) {
   if (ta == 0) return load8<float>(A + (size_t)m * lda + k);
   f32x8 r;
@@ -38,8 +40,40 @@ TM_DEV f32x8 frag_b(const float* B, int tb, int ldb, int k, int n) {
   return r;
 }
 
-__global__ __launch_bounds__(256) void bmm_kernel(JobPair jp, int nbatch) {
-  __shared__ float red[4][16][64];
+// One k-step (16 deep) of a 32x32 fp32 product.
+//   PREC 0: exact fp32 (8 x v_mfma_f32_32x32x2_f32, an fmaf chain per element).
+//   PREC 1: "bf16x3": x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (16 significant
+//           bits); hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_bf16 with fp32
+//           accumulation (dropped lo*lo ~ 2^-16 relative).  3 x 32 cycles instead of
+//           8 x 64: used by the bf16 (bench) mode only.
+template <int PREC>
+TM_DEV void mma_f32_step(f32x16& acc, const f32x8& a, const f32x8& b) {
+  if constexpr (PREC == 0) {
+    mma16(acc, a, b);
+  } else {
+    bf16x8 ah, al, bh, bl;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      ah[e] = (bf16)a[e];
+      al[e] = (bf16)(a[e] - (float)ah[e]);
+      bh[e] = (bf16)b[e];
+      bl[e] = (bf16)(b[e] - (float)bh[e]);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc, 0, 0, 0);
+  }
+}
+
+// One workgroup = one 32x32 output tile of one batch entry; its 8 waves take the
+// k-steps round-robin (s = wave, wave + 8, ...; every fragment requested before the
+// first MFMA) and are summed in LDS in a fixed order.  4 waves per SIMD hide the L2
+// latency of the operand loads behind each other's MFMAs.
+constexpr int BMM_WAVES = 8;
+
+template <int PREC>
+__global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
+  __shared__ float red[BMM_WAVES][16][64];
   int b = blockIdx.x;
   const int which = b < jp.tiles0 * nbatch ? 0 : 1;
   if (which) b -= jp.tiles0 * nbatch;
@@ -49,37 +83,35 @@ __global__ __launch_bounds__(256) void bmm_kernel(JobPair jp, int nbatch) {
   const int tm = tile / ntn, tn = tile % ntn;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int nterms = J.A2 ? 2 : 1;
-  const int kchunk = J.K * nterms / 4;
+  const int nsteps = J.K * nterms / 16;
   f32x16 acc = (f32x16){};
-  // all fragments of up to 4 k-steps are requested before the first MFMA, so the
-  // L2 round trips overlap instead of serialising step by step
-  for (int kb = wave * kchunk; kb < (wave + 1) * kchunk; kb += 64) {
-    f32x8 af[4], bf[4];
-    const int nst = min(4, ((wave + 1) * kchunk - kb) / 16);
+  f32x8 af[4], bfr[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (s < nst) {
-        const int kk = kb + 16 * s;
-        const int term = kk / J.K, kl = kk % J.K;
-        const float* A = term ? J.A2 + bh * J.sa2 : J.A + bh * J.sa;
-        const float* B = term ? J.B2 + bh * J.sb2 : J.B + bh * J.sb;
-        const int ta = term ? J.ta2 : J.ta, tb = term ? J.tb2 : J.tb;
-        const int lda = term ? J.lda2 : J.lda, ldb = term ? J.ldb2 : J.ldb;
-        af[s] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
-        bf[s] = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
-      }
+  for (int i = 0; i < 4; ++i) {
+    const int st = wave + BMM_WAVES * i;
+    if (st < nsteps) {
+      const int kk = st * 16;
+      const int term = kk / J.K, kl = kk % J.K;
+      const float* A = term ? J.A2 + bh * J.sa2 : J.A + bh * J.sa;
+      const float* B = term ? J.B2 + bh * J.sb2 : J.B + bh * J.sb;
+      const int ta = term ? J.ta2 : J.ta, tb = term ? J.tb2 : J.tb;
+      const int lda = term ? J.lda2 : J.lda, ldb = term ? J.ldb2 : J.ldb;
+      af[i] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
+      bfr[i] = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
     }
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-      if (s < nst) mma16(acc, af[s], bf[s]);
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (wave + BMM_WAVES * i < nsteps) mma_f32_step<PREC>(acc, af[i], bfr[i]);
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[wave][i][lane] = acc[i];
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int e = tid + 256 * q, reg = e >> 6, ln = e & 63;
-    const float s = ((red[0][reg][ln] + red[1][reg][ln]) + red[2][reg][ln]) + red[3][reg][ln];
+  for (int q = 0; q < 2; ++q) {
+    const int e = tid + 512 * q, reg = e >> 6, ln = e & 63;
+    float s = red[0][reg][ln];
+#pragma unroll
+    for (int w = 1; w < BMM_WAVES; ++w) s += red[w][reg][ln];
     const int row = tm * 32 + acc_row(reg, ln >> 5), col = tn * 32 + (ln & 31);
     const size_t off = (size_t)bh * J.sc + (size_t)row * J.ldc + col;
     float v = J.alpha * s;
@@ -191,7 +223,7 @@ __global__ __launch_bounds__(256) void pinv_init_bwd_kernel(const float* __restr
   }
 }
 
-int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, hipStream_t st) {
+int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, hipStream_t st) {
   TM_REQUIRE(njobs == 1 || njobs == 2, "bmm: njobs must be 1 or 2");
   JobPair jp{};
   int total = 0;
@@ -200,13 +232,14 @@ int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, hipStream_t st) {
     TM_REQUIRE(J.A && J.B && J.C, "bmm: null operand");
     TM_REQUIRE(J.M % 32 == 0 && J.N % 32 == 0, "bmm: M, N must be multiples of 32");
     const int nterms = J.A2 ? 2 : 1;
-    TM_REQUIRE((J.K * nterms) % 64 == 0 && J.K % ((J.K * nterms) / 4) == 0, "bmm: K split must be 16-aligned per wave");
+    TM_REQUIRE(J.K % 16 == 0 && J.K * nterms <= 16 * BMM_WAVES * 4, "bmm: K must be a multiple of 16, K*terms <= 512");
     jp.j[i] = J;
     const int tiles = (J.M / 32) * (J.N / 32);
     if (i == 0) jp.tiles0 = tiles;
     total += tiles * nbatch;
   }
-  bmm_kernel<<<total, 256, 0, st>>>(jp, nbatch);
+  if (prec == 1) bmm_kernel<1><<<total, 512, 0, st>>>(jp, nbatch);
+  else bmm_kernel<0><<<total, 512, 0, st>>>(jp, nbatch);
   TM_CHECK_LAUNCH();
   return 0;
 }
@@ -232,8 +265,15 @@ void add_term(tm_bmm_job& j, const float* A, int ta, const float* B, int tb) {
 
 }  // namespace
 
-extern "C" int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, void* stream) {
-  return launch_bmm(jobs, njobs, nbatch, (hipStream_t)stream);
+// Debug/ablation switch for microbenchmarks only (not part of the supported ABI surface).
+extern "C" void tm_debug_set_nys_variant(int value);
+extern "C" void tm_debug_set_variant(int which, int value) {
+  if (which == 1) tm_debug_set_nys_variant(value);
+}
+
+extern "C" int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream) {
+  TM_REQUIRE(prec == 0 || prec == 1, "bmm: prec must be 0 (fp32) or 1 (bf16x3)");
+  return launch_bmm(jobs, njobs, nbatch, prec, (hipStream_t)stream);
 }
 
 // workspace: Zs[iters+1], Ps[iters], T3s[iters], T5s[iters] (each nbh*256*256 fp32) + sums[2][nbh][256] + stats[8]
@@ -241,7 +281,7 @@ extern "C" long long tm_pinv_saved_floats(int nbh, int iters) {
   return (4LL * iters + 1) * nbh * NL * NL + 2LL * nbh * NL + 8;
 }
 
-extern "C" int tm_pinv_fwd(const float* X, int nbh, int iters, float* saved, void* stream) {
+extern "C" int tm_pinv_fwd(const float* X, int nbh, int iters, int prec, float* saved, void* stream) {
   TM_REQUIRE(X && saved && iters >= 0, "pinv_fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   const size_t mat = (size_t)nbh * NL * NL;
@@ -261,14 +301,14 @@ extern "C" int tm_pinv_fwd(const float* X, int nbh, int iters, float* saved, voi
     float* T3 = T3s + it * mat;
     float* T5 = T5s + it * mat;
     tm_bmm_job j = job(X, 0, Z, 0, P, NL, NL, NL, 1.f);               // P = X Z
-    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+    if (int rc = launch_bmm(&j, 1, nbh, prec, st)) return rc;
     j = job(P, 0, P, 0, T3, NL, NL, NL, 1.f, 15.f);                    // T3 = 15I + P P - 7P
     j.E1 = P; j.e1 = -7.f;
-    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+    if (int rc = launch_bmm(&j, 1, nbh, prec, st)) return rc;
     j = job(P, 0, T3, 0, T5, NL, NL, NL, -1.f, 13.f);                  // T5 = 13I - P T3
-    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+    if (int rc = launch_bmm(&j, 1, nbh, prec, st)) return rc;
     j = job(Z, 0, T5, 0, Zs + (it + 1) * mat, NL, NL, NL, 0.25f);      // Z' = 0.25 Z T5
-    if (int rc = launch_bmm(&j, 1, nbh, st)) return rc;
+    if (int rc = launch_bmm(&j, 1, nbh, prec, st)) return rc;
   }
   return 0;
 }
@@ -279,8 +319,8 @@ extern "C" long long tm_pinv_bwd_workspace_floats(int nbh) {
 }
 
 // dZ (gradient w.r.t. the final Z) is consumed (overwritten).  dX is written (=).
-extern "C" int tm_pinv_bwd(const float* X, int nbh, int iters, const float* saved, float* dZ, float* work, float* dX,
-                           void* stream) {
+extern "C" int tm_pinv_bwd(const float* X, int nbh, int iters, int prec, const float* saved, float* dZ, float* work,
+                           float* dX, void* stream) {
   TM_REQUIRE(X && saved && dZ && work && dX, "pinv_bwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   const size_t mat = (size_t)nbh * NL * NL;
@@ -305,19 +345,19 @@ extern "C" int tm_pinv_bwd(const float* X, int nbh, int iters, const float* save
     tm_bmm_job jb[2];
     jb[0] = job(Z, 1, G, 0, dT5, NL, NL, NL, 0.25f);                    // dT5 = 0.25 Z^T G
     jb[1] = job(G, 0, T5, 1, dZa, NL, NL, NL, 0.25f);                   // dZa = 0.25 G T5^T
-    if (int rc = launch_bmm(jb, 2, nbh, st)) return rc;
+    if (int rc = launch_bmm(jb, 2, nbh, prec, st)) return rc;
     jb[0] = job(dT5, 0, T3, 1, dP, NL, NL, NL, -1.f);                   // dP  = -dT5 T3^T
     jb[1] = job(P, 1, dT5, 0, dT3, NL, NL, NL, -1.f);                   // dT3 = -P^T dT5
-    if (int rc = launch_bmm(jb, 2, nbh, st)) return rc;
+    if (int rc = launch_bmm(jb, 2, nbh, prec, st)) return rc;
     jb[0] = job(dT3, 0, P, 1, dP, NL, NL, NL, 1.f);                     // dP += dT3 P^T + P^T dT3 - 7 dT3
     add_term(jb[0], P, 1, dT3, 0);
     jb[0].E1 = dP; jb[0].e1 = 1.f; jb[0].E2 = dT3; jb[0].e2 = -7.f;
-    if (int rc = launch_bmm(jb, 1, nbh, st)) return rc;
+    if (int rc = launch_bmm(jb, 1, nbh, prec, st)) return rc;
     jb[0] = job(dP, 0, Z, 1, dX, NL, NL, NL, 1.f);                      // dX (+)= dP Z^T
     if (!first) { jb[0].E1 = dX; jb[0].e1 = 1.f; }
     jb[1] = job(X, 1, dP, 0, G, NL, NL, NL, 1.f);                       // G = dZa + X^T dP
     jb[1].E1 = dZa; jb[1].e1 = 1.f;
-    if (int rc = launch_bmm(jb, 2, nbh, st)) return rc;
+    if (int rc = launch_bmm(jb, 2, nbh, prec, st)) return rc;
     first = false;
   }
   if (first) {  // iters == 0: dX starts at zero

@@ -177,9 +177,10 @@ def bmm_job(A, ta, B, tb, Cout, M, N, K, alpha=1.0, diag=0.0, E1=None, e1=0.0, E
     return j
 
 
-def bmm(jobs, nbatch):
+def bmm(jobs, nbatch, prec=0):
+    """prec 0: exact fp32 MFMA (parity mode); 1: bf16x3 split (bench mode)."""
     arr = (BmmJob * len(jobs))(*jobs)
-    _lib.call("tm_bmm", arr, len(jobs), nbatch, _stream())
+    _lib.call("tm_bmm", arr, len(jobs), nbatch, prec, _stream())
 
 
 class Pool:
@@ -206,7 +207,8 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
     a2 = pool(nbh * NL * NL).view(nbh, NL, NL)
     _lib.call("tm_nys_sim2_softmax", _p(ql), _p(kl), nbh, _p(a2), st)
     saved = pool(_lib.query("tm_pinv_saved_floats", nbh, PINV_ITERS))
-    _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, _p(saved), st)
+    prec = 1 if dt_code == BF16 else 0
+    _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, prec, _p(saved), st)
     z = saved[PINV_ITERS * nbh * NL * NL:(PINV_ITERS + 1) * nbh * NL * NL].view(nbh, NL, NL)
     w = pool(nbh * NL * DH).view(nbh, NL, DH)
     lse3 = pool(nbh * NL)
@@ -214,7 +216,7 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
     with probe("a3_fwd"):
         _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
     y = pool(nbh * NL * DH).view(nbh, NL, DH)
-    bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh)
+    bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh, prec)
     y_t = pool(nbh * NL * DH, tdtype)
     _lib.call("tm_cast_f32", dt_code, _p(y), _p(y_t), nbh * NL * DH, st)
     merged = pool(geo.B * n * nh * DH, tdtype).view(geo.B, n, nh * DH)
@@ -234,6 +236,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     q, k, v = qkv[0], qkv[1], qkv[2]
     st = _stream()
     mat = nbh * NL * NL
+    prec = 1 if dt_code == BF16 else 0
     # conv33 backward + D1
     dq = pool(nbh * n * DH)
     dk = pool(nbh * n * DH)
@@ -256,16 +259,17 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     dz = pool(mat).view(nbh, NL, NL)
     dw = pool(nbh * NL * DH).view(nbh, NL, DH)
     bmm([bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH),
-         bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh)
+         bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh, prec)
     # pseudo-inverse backward -> dA2, then softmax backward
     da2 = pool(mat).view(nbh, NL, NL)
     pwork = pool(_lib.query("tm_pinv_bwd_workspace_floats", nbh))
-    _lib.call("tm_pinv_bwd", _p(state["a2"]), nbh, PINV_ITERS, _p(state["pinv"]), _p(dz), _p(pwork), _p(da2), st)
+    _lib.call("tm_pinv_bwd", _p(state["a2"]), nbh, PINV_ITERS, prec, _p(state["pinv"]), _p(dz), _p(pwork),
+              _p(da2), st)
     ds2 = pool(mat).view(nbh, NL, NL)
     _lib.call("tm_softmax_bwd_rows256", _p(state["a2"]), _p(da2), _p(ds2), nbh * NL, st)
     dql = pool(nbh * NL * DH).view(nbh, NL, DH)
     bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL),
-         bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh)
+         bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
     # A3 product backward: dk (=), dv (+=), dql (+=)
     d3 = pool(nbh * NL)
     dw_t = pool(nbh * NL * DH, tdtype)

@@ -10,6 +10,7 @@ it on MI355X:
 * ``add_weight_decay`` / ``create_optimizer`` -- no-decay groups + RAdam, optionally
                            wrapped in Lookahead (code/MyOptimizer/optim_factory.py:25-123)
 * ``Lookahead``         -- k-step slow-weight wrapper (alpha 0.5, k 6; multi-tensor ops)
+* ``FusedRAdamLookahead`` -- RAdam + Lookahead for the GPU as one HIP elementwise launch
 * ``GradAllReduce``     -- the DDP gradient all-reduce (Lightning DDP, code/train.py:178-201):
                            one flat fp32 bucket, averaged over ranks with one RCCL
                            all_reduce over xGMI (the model is 9.64 MB of fp32 grads)
@@ -18,6 +19,7 @@ it on MI355X:
 """
 from __future__ import annotations
 
+import ctypes as C
 from collections import defaultdict
 
 import torch
@@ -97,6 +99,104 @@ class Lookahead(torch.optim.Optimizer):
         self.base_optimizer.zero_grad(set_to_none=set_to_none)
 
 
+class FusedRAdamLookahead(torch.optim.Optimizer):
+    """``Lookahead(torch.optim.RAdam(groups))`` as ONE HIP launch pair per step.
+
+    Same update as ``torch.optim.RAdam`` (L2 weight decay folded into the gradient,
+    ``decoupled_weight_decay=False``; code/MyOptimizer/optim_factory.py:77-79) followed
+    by the reference Lookahead sync every ``k`` steps (code/MyOptimizer/lookahead.py,
+    wrapped at optim_factory.py:118-121; ``lookahead_k=0`` gives plain RAdam).  The
+    moments and slow weights of every parameter live in three flat fp32 buffers, the
+    step counters on the device, and the kernel reads each parameter/gradient through
+    a pointer table passed by value (``tm_radam_lookahead_step``, csrc/optim.hip), so
+    the step is hipGraph-capturable.  ``lr`` / ``weight_decay`` are read per group
+    at each call (a captured graph keeps the values it was captured with, as a
+    capturable torch optimizer does)."""
+
+    def __init__(self, params, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 lookahead_alpha=0.5, lookahead_k=6):
+        if not 0.0 <= lookahead_alpha <= 1.0 or lookahead_k < 0:
+            raise ValueError("Lookahead: alpha in [0,1], k >= 0")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                        lookahead_alpha=lookahead_alpha, lookahead_k=lookahead_k, lookahead_step=0)
+        super().__init__(params, defaults)
+        from . import _lib
+        self._lib = _lib
+        plist = [p for g in self.param_groups for p in g["params"]]
+        if len(plist) > _lib.OPTIM_MAX_TENSORS:
+            raise ValueError(f"fused RAdam: at most {_lib.OPTIM_MAX_TENSORS} parameter tensors")
+        if any(p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous() for p in plist):
+            raise ValueError("fused RAdam: parameters must be contiguous fp32 CUDA tensors")
+        for g in self.param_groups:
+            for key in ("betas", "eps", "lookahead_alpha", "lookahead_k"):
+                if g[key] != self.param_groups[0][key]:
+                    raise ValueError(f"fused RAdam: '{key}' must be equal across groups")
+        self._params = plist
+        total = sum(p.numel() for p in plist)
+        dev = plist[0].device
+        self._flat = torch.zeros(3, total, dtype=torch.float32, device=dev)  # exp_avg, exp_avg_sq, slow
+        self._counters = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._offsets = [0]
+        for p in plist:
+            self._offsets.append(self._offsets[-1] + p.numel())
+        self._bind_state()
+
+    def _bind_state(self):
+        for i, p in enumerate(self._params):
+            a, b = self._offsets[i], self._offsets[i + 1]
+            self.state[p] = {"exp_avg": self._flat[0, a:b].view_as(p),
+                             "exp_avg_sq": self._flat[1, a:b].view_as(p),
+                             "slow_buffer": self._flat[2, a:b].view_as(p)}
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        lib = self._lib
+        tab = lib.OptimTable()
+        tab.count = len(self._params)
+        i = 0
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is None:
+                    raise RuntimeError("fused RAdam: every parameter needs a gradient each step")
+                t = tab.t[i]
+                t.param, t.grad, t.numel = p.data_ptr(), p.grad.data_ptr(), p.numel()
+                t.lr, t.weight_decay = float(g["lr"]), float(g["weight_decay"])
+                tab.offset[i] = self._offsets[i]
+                i += 1
+            g["lookahead_step"] += 1
+        tab.offset[i] = self._offsets[i]
+        g0 = self.param_groups[0]
+        b1, b2 = g0["betas"]
+        lib.call("tm_radam_lookahead_step", C.byref(tab), self._flat[0].data_ptr(), self._flat[1].data_ptr(),
+                 self._flat[2].data_ptr(), self._counters.data_ptr(), float(b1), float(b2), float(g0["eps"]),
+                 int(g0["lookahead_k"]), float(g0["lookahead_alpha"]),
+                 torch.cuda.current_stream(self._flat.device).cuda_stream)
+        return loss
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd["fused_counters"] = self._counters.cpu()
+        return sd
+
+    def load_state_dict(self, state_dict):
+        counters = state_dict.get("fused_counters")
+        super().load_state_dict({k: v for k, v in state_dict.items() if k != "fused_counters"})
+        with torch.no_grad():
+            for i, p in enumerate(self._params):
+                st = self.state[p]
+                a, b = self._offsets[i], self._offsets[i + 1]
+                for row, key in enumerate(("exp_avg", "exp_avg_sq", "slow_buffer")):
+                    if key in st:
+                        self._flat[row, a:b].copy_(st[key].reshape(-1))
+            if counters is not None:
+                self._counters.copy_(counters)
+        self._bind_state()
+
+
 def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float = 2e-4,
                      weight_decay: float = 0.01, eps=None, betas=None):
     """optim_factory.create_optimizer for the optimizers TransMIL configs use (radam / adam / adamw / sgd)."""
@@ -109,6 +209,10 @@ def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float =
     parts = opt.lower().split("_")
     name = parts[-1]
     fused = torch.cuda.is_available()
+    on_gpu = fused and all(p.is_cuda for p in model.parameters())
+    if name == "radam" and on_gpu:
+        la = len(parts) > 1 and parts[0] == "lookahead"
+        return FusedRAdamLookahead(params, lookahead_k=6 if la else 0, **kw)
     if name == "radam":
         base = torch.optim.RAdam(params, foreach=True, capturable=fused, **kw)
     elif name == "adam":
