@@ -118,7 +118,7 @@ int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_
 long long tm_nys_a3_bwd_workspace(int nbh, int n);
 int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
                   const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
-                  float* work, float* dql, void* stream);
+                  float* work, float* dql, int accumulate, void* stream);
 int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const float* dk, const float* dkl,
                          const float* dv, int nbags, int nh, int n, float scale, void* dqkv, void* stream);
 
@@ -138,6 +138,8 @@ typedef struct tm_bmm_job {
 int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream);
 /* microbenchmark ablation switch (which = 0: bmm kernel variant); not for production use */
 void tm_debug_set_variant(int which, int value);
+/* XCD id (HW_REG_XCC_ID) of every block of an nblocks x threads launch -> out[nblocks] (int32) */
+int tm_debug_xcc_map(int* out, int nblocks, int threads, void* stream);
 long long tm_pinv_saved_floats(int nbh, int iters);
 int tm_pinv_fwd(const float* X, int nbh, int iters, int prec, float* saved, void* stream);
 long long tm_pinv_bwd_workspace_floats(int nbh);

@@ -84,6 +84,14 @@ def main():
         print(f"{name:40s} {us:9.2f} us{extra}", flush=True)
 
     st = E._stream
+    if not args.only or args.only == "xcc":
+        for nb, th in ((512, 512), (64, 256), (1024, 256)):
+            xm = torch.zeros(nb, dtype=torch.int32, device=dev)
+            _lib.call("tm_debug_xcc_map", E._p(xm), nb, th, st())
+            torch.cuda.synchronize()
+            v = xm.cpu().tolist()
+            same = sum(1 for b in range(8, nb) if v[b] == v[b - 8]) / max(nb - 8, 1)
+            print(f"xcc map {nb}x{th}: first 24 {v[:24]}  frac(b, b+8 same XCD)={same:.3f}", flush=True)
     # ---------------- bmm (pinv building block) ----------------
     X = torch.softmax(torch.randn(nbh, 256, 256, device=dev), -1)
     Z = torch.randn(nbh, 256, 256, device=dev) * 1e-2
@@ -91,12 +99,23 @@ def main():
     W = torch.randn(nbh, 256, 64, device=dev)
     Y = torch.empty(nbh, 256, 64, device=dev)
     f = 2 * nbh * 256 ** 3
+    Y2 = torch.randn(nbh, 256, 256, device=dev)
+    Z2 = torch.empty_like(Z)
     case("bmm NN 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh), f)
     case("bmm NT 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 1, P, 256, 256, 256)], nbh), f)
     case("bmm TN 256^3 x8", lambda: E.bmm([E.bmm_job(X, 1, Z, 0, P, 256, 256, 256)], nbh), f)
     case("bmm 2-job 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
                                               E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh), 2 * f)
     case("bmm NN 256^3 x8 [bf16x3]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh, 1), f)
+    for var, nm in ((1, "no loads/MFMA"), (2, "loads only"), (3, "no E terms"), (4, "store only")):
+        _lib.lib().tm_debug_set_variant(0, var)
+        case(f"bmm NN+E1 bf16x3 [{nm}]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256, E1=Y2, e1=1.0)],
+                                                         nbh, 1), f)
+    _lib.lib().tm_debug_set_variant(0, 0)
+    case("bmm dependent pair bf16x3 (per bmm)", lambda: (E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh, 1),
+                                                        E.bmm([E.bmm_job(X, 0, P, 0, Z2, 256, 256, 256)], nbh, 1)), 2 * f)
+    _lib.lib().tm_debug_set_variant(0, 0)
+    case("bmm NN+E1 bf16x3", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256, E1=Y2, e1=1.0)], nbh, 1), f)
     case("bmm 2-job 256^3 x8 [bf16x3]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
                                               E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh, 1), 2 * f)
     case("bmm Y=ZW 256x64x256 x8", lambda: E.bmm([E.bmm_job(Z, 0, W, 0, Y, 256, 64, 256)], nbh), f // 4)
@@ -198,7 +217,7 @@ def main():
     lse3.uniform_(8, 9)
     case("a3_bwd (+reduce)", lambda: _lib.call("tm_nys_a3_bwd", BF16, E._p(ql_t), E._p(dw_t), E._p(k), E._p(v),
                                                E._p(lse3), E._p(d3), nbh, 8, n, E._p(dk), E._p(dv), E._p(a3bw),
-                                               E._p(dql), st()), 10 * nbh * n * 256 * 64)
+                                               E._p(dql), 1, st()), 10 * nbh * n * 256 * 64)
     # ---------------- PPEG ----------------
     x = torch.randn(1, S, 512, device=dev)
     wf = torch.randn(512 * 49, device=dev) * 0.1

@@ -78,10 +78,11 @@ _SIGS = {
     "tm_nys_a1_bwd_workspace": (L, [I, I, I]),
     "tm_nys_a1_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P, P, P, P, I, P]),
     "tm_nys_a3_bwd_workspace": (L, [I, I]),
-    "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, P]),
+    "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, I, P]),
     "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
     "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
     "tm_debug_set_variant": (None, [I, I]),
+    "tm_debug_xcc_map": (I, [P, I, I, P]),
     "tm_pinv_saved_floats": (L, [I, I]),
     "tm_pinv_fwd": (I, [P, I, I, I, P, P]),
     "tm_pinv_bwd_workspace_floats": (L, [I]),

@@ -928,7 +928,7 @@ extern "C" long long tm_nys_a3_bwd_workspace(int nbh, int n) {
 
 extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
                              const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
-                             float* work, float* dql, void* stream) {
+                             float* work, float* dql, int accumulate, void* stream) {
   TM_REQUIRE(n % NL == 0, "a3_bwd: n must be a multiple of 256");
   const int nkb = n / NL;
   BwdArgs a{};
@@ -946,7 +946,7 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
   TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A3>, bwd_smem_bytes<T>()),
                             attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
   TM_CHECK_LAUNCH();
-  return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, 1, stream);
+  return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, accumulate, stream);
 }
 
 extern "C" int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const float* dk, const float* dkl,

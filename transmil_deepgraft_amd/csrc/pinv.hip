@@ -70,8 +70,9 @@ TM_DEV void mma_f32_step(f32x16& acc, const f32x8& a, const f32x8& b) {
 // first MFMA) and are summed in LDS in a fixed order.  4 waves per SIMD hide the L2
 // latency of the operand loads behind each other's MFMAs.
 constexpr int BMM_WAVES = 8;
+int g_bmm_variant = 0;
 
-template <int PREC>
+template <int PREC, int VAR = 0>  // VAR (ablation): 1 no loads/MFMA, 2 loads only, 3 no E terms, 4 store only
 __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
   __shared__ float red[BMM_WAVES][16][64];
   int b = blockIdx.x;
@@ -85,11 +86,16 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
   const int nterms = J.A2 ? 2 : 1;
   const int nsteps = J.K * nterms / 16;
   f32x16 acc = (f32x16){};
+  if constexpr (VAR == 4) {
+    const int row = tm * 32 + (tid >> 5) % 32, col = tn * 32 + (tid & 31);
+    if (tid < 1024) J.C[(size_t)bh * J.sc + (size_t)row * J.ldc + col] = 0.f;
+    return;
+  }
   f32x8 af[4], bfr[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int st = wave + BMM_WAVES * i;
-    if (st < nsteps) {
+    if (VAR != 1 && st < nsteps) {
       const int kk = st * 16;
       const int term = kk / J.K, kl = kk % J.K;
       const float* A = term ? J.A2 + bh * J.sa2 : J.A + bh * J.sa;
@@ -102,7 +108,13 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (wave + BMM_WAVES * i < nsteps) mma_f32_step<PREC>(acc, af[i], bfr[i]);
+    if (wave + BMM_WAVES * i < nsteps) {
+      if constexpr (VAR == 0 || VAR == 3) mma_f32_step<PREC>(acc, af[i], bfr[i]);
+      if constexpr (VAR == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += af[i][e] * bfr[i][e];
+      }
+    }
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[wave][i][lane] = acc[i];
   __syncthreads();
@@ -116,8 +128,8 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
     const size_t off = (size_t)bh * J.sc + (size_t)row * J.ldc + col;
     float v = J.alpha * s;
     if (row == col) v += J.diag;
-    if (J.E1) v += J.e1 * J.E1[off];
-    if (J.E2) v += J.e2 * J.E2[off];
+    if (VAR != 3 && J.E1) v += J.e1 * J.E1[off];
+    if (VAR != 3 && J.E2) v += J.e2 * J.E2[off];
     J.C[off] = v;
   }
 }
@@ -238,8 +250,17 @@ int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, hipStrea
     if (i == 0) jp.tiles0 = tiles;
     total += tiles * nbatch;
   }
-  if (prec == 1) bmm_kernel<1><<<total, 512, 0, st>>>(jp, nbatch);
-  else bmm_kernel<0><<<total, 512, 0, st>>>(jp, nbatch);
+  if (prec == 1) {
+    switch (g_bmm_variant) {
+      case 1: bmm_kernel<1, 1><<<total, 512, 0, st>>>(jp, nbatch); break;
+      case 2: bmm_kernel<1, 2><<<total, 512, 0, st>>>(jp, nbatch); break;
+      case 3: bmm_kernel<1, 3><<<total, 512, 0, st>>>(jp, nbatch); break;
+      case 4: bmm_kernel<1, 4><<<total, 512, 0, st>>>(jp, nbatch); break;
+      default: bmm_kernel<1><<<total, 512, 0, st>>>(jp, nbatch);
+    }
+  } else {
+    bmm_kernel<0><<<total, 512, 0, st>>>(jp, nbatch);
+  }
   TM_CHECK_LAUNCH();
   return 0;
 }
@@ -266,8 +287,21 @@ void add_term(tm_bmm_job& j, const float* A, int ta, const float* B, int tb) {
 }  // namespace
 
 // Debug/ablation switch for microbenchmarks only (not part of the supported ABI surface).
+__global__ void xcc_map_kernel(int* out) {
+  if (threadIdx.x == 0) out[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+}
+
+// which XCD (0-7) each block of a `nblocks` x `threads` launch ran on (dispatch-placement probe)
+extern "C" int tm_debug_xcc_map(int* out, int nblocks, int threads, void* stream) {
+  TM_REQUIRE(out && nblocks > 0 && threads > 0 && threads <= 1024, "xcc_map: bad args");
+  xcc_map_kernel<<<nblocks, threads, 0, (hipStream_t)stream>>>(out);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" void tm_debug_set_nys_variant(int value);
 extern "C" void tm_debug_set_variant(int which, int value) {
+  if (which == 0) g_bmm_variant = value;
   if (which == 1) tm_debug_set_nys_variant(value);
 }
 

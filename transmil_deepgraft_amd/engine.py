@@ -205,16 +205,18 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
     kl_t = pool(nbh * NL * DH, tdtype).view(nbh, NL, DH)
     _lib.call("tm_nys_landmarks", dt_code, _p(q), _p(k), nbh, n, _p(ql), _p(kl), _p(ql_t), _p(kl_t), st)
     a2 = pool(nbh * NL * NL).view(nbh, NL, NL)
-    _lib.call("tm_nys_sim2_softmax", _p(ql), _p(kl), nbh, _p(a2), st)
     saved = pool(_lib.query("tm_pinv_saved_floats", nbh, PINV_ITERS))
-    prec = 1 if dt_code == BF16 else 0
-    _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, prec, _p(saved), st)
-    z = saved[PINV_ITERS * nbh * NL * NL:(PINV_ITERS + 1) * nbh * NL * NL].view(nbh, NL, NL)
     w = pool(nbh * NL * DH).view(nbh, NL, DH)
     lse3 = pool(nbh * NL)
     work = pool(_lib.query("tm_nys_a3_workspace", nbh, n) // 4)
+    # (measured: running A3 V on a second stream beside the pseudo-inverse chain slowed
+    #  the step -- the chain's launches then wait for CUs -- so the path stays serial)
     with probe("a3_fwd"):
         _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
+    _lib.call("tm_nys_sim2_softmax", _p(ql), _p(kl), nbh, _p(a2), st)
+    prec = 1 if dt_code == BF16 else 0
+    _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, prec, _p(saved), st)
+    z = saved[PINV_ITERS * nbh * NL * NL:(PINV_ITERS + 1) * nbh * NL * NL].view(nbh, NL, NL)
     y = pool(nbh * NL * DH).view(nbh, NL, DH)
     bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh, prec)
     y_t = pool(nbh * NL * DH, tdtype)
@@ -260,6 +262,15 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     dw = pool(nbh * NL * DH).view(nbh, NL, DH)
     bmm([bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH),
          bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh, prec)
+    # A3 product backward: dk (=), dv (+=), dql3 (=)
+    d3 = pool(nbh * NL)
+    dw_t = pool(nbh * NL * DH, tdtype)
+    dql3 = pool(nbh * NL * DH).view(nbh, NL, DH)
+    work3 = pool(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4)
+    _lib.call("tm_nys_rowdot_cast", dt_code, _p(dw), _p(state["w"]), nbh * NL, _p(d3), _p(dw_t), st)
+    with probe("a3_bwd"):
+        _lib.call("tm_nys_a3_bwd", dt_code, _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]),
+                  _p(d3), nbh, nh, n, _p(dk), _p(dv), _p(work3), _p(dql3), 0, st)
     # pseudo-inverse backward -> dA2, then softmax backward
     da2 = pool(mat).view(nbh, NL, NL)
     pwork = pool(_lib.query("tm_pinv_bwd_workspace_floats", nbh))
@@ -268,16 +279,8 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     ds2 = pool(mat).view(nbh, NL, NL)
     _lib.call("tm_softmax_bwd_rows256", _p(state["a2"]), _p(da2), _p(ds2), nbh * NL, st)
     dql = pool(nbh * NL * DH).view(nbh, NL, DH)
-    bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL),
+    bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL, E1=dql3, e1=1.0),
          bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
-    # A3 product backward: dk (=), dv (+=), dql (+=)
-    d3 = pool(nbh * NL)
-    dw_t = pool(nbh * NL * DH, tdtype)
-    _lib.call("tm_nys_rowdot_cast", dt_code, _p(dw), _p(state["w"]), nbh * NL, _p(d3), _p(dw_t), st)
-    work = pool(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4)
-    with probe("a3_bwd"):
-        _lib.call("tm_nys_a3_bwd", dt_code, _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]), _p(d3),
-                  nbh, nh, n, _p(dk), _p(dv), _p(work), _p(dql), st)
     dqkv = pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH)
     _lib.call("tm_nys_assemble_dqkv", dt_code, _p(dq), _p(dql), _p(dk), _p(dkl), _p(dv), geo.B, nh, n,
               C.c_float(scale), _p(dqkv), st)
