@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--gemm-ab", action="store_true", help="also time the GEMMs on the register-staged loop")
     args = ap.parse_args()
     dev = "cuda"
     N = args.n
@@ -71,7 +72,10 @@ def main():
     bf = torch.bfloat16
     res = {}
 
+    tag = [""]
+
     def case(name, fn, flops=None, byts=None):
+        name = tag[0] + name
         if args.only and args.only not in name:
             return
         us = timeit(fn, args.reps, graph=not args.eager)
@@ -123,49 +127,58 @@ def main():
     saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=dev)
     case("pinv_fwd (26 launches)", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 0, E._p(saved), st()), 24 * f)
     case("pinv_fwd [bf16x3]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 1, E._p(saved), st()), 24 * f)
-    # ---------------- GEMMs ----------------
-    pool = E.Pool(dev)
-    xn = torch.randn(n, 512, device=dev).to(bf)
-    wqkv = (torch.randn(1536, 512, device=dev) * 0.05).to(bf)
-    qkv = torch.empty(3, nbh, n, 64, device=dev, dtype=bf)
-    case("gemm qkv (NT, scatter)", lambda: E.gemm(xn, wqkv, qkv, n, 1536, 512, lda=512, ldb=512, ldc=0, dtype=BF16,
-                                                  qkv=(1, 8, 64, n, 0.125)), 2 * n * 1536 * 512)
-    slabq = torch.empty(n, 1536, device=dev)
+    for gv in ((0, 1) if args.gemm_ab else (0,)):
+        _lib.lib().tm_debug_set_variant(2, gv)
+        tag[0] = "[old loop] " if gv else ""
+        # ---------------- GEMMs ----------------
+        pool = E.Pool(dev)
+        xn = torch.randn(n, 512, device=dev).to(bf)
+        wqkv = (torch.randn(1536, 512, device=dev) * 0.05).to(bf)
+        qkv = torch.empty(3, nbh, n, 64, device=dev, dtype=bf)
+        case("gemm qkv (NT, scatter)", lambda: E.gemm(xn, wqkv, qkv, n, 1536, 512, lda=512, ldb=512, ldc=0, dtype=BF16,
+                                                      qkv=(1, 8, 64, n, 0.125)), 2 * n * 1536 * 512)
+        slabq = torch.empty(n, 1536, device=dev)
 
-    def plain_gemm(K_):
-        g = _lib.GemmArgs()
-        g.M, g.N, g.K = n, 1536, K_
-        g.lda, g.ldb, g.ldc = 512, 512, 1536
-        g.ab_dtype, g.c_dtype = BF16, F32
-        g.splits, g.k_per_split = 1, 512
-        g.mode = _lib.EPI_SPLITK
-        g.alpha = 1.0
-        _lib.call("tm_gemm", E._p(xn), E._p(wqkv), E._p(slabq), C.byref(g), st())
-    case("gemm qkv shape, plain fp32 store", lambda: plain_gemm(512), 2 * n * 1536 * 512)
-    case("gemm qkv shape, K=64 plain store", lambda: plain_gemm(64), 2 * n * 1536 * 64)
-    outb = torch.empty(n, 1536, device=dev, dtype=bf)
-    case("torch.matmul bf16 (hipBLASLt) qkv", lambda: torch.matmul(xn, wqkv.t(), out=outb), 2 * n * 1536 * 512)
-    H = torch.randn(S, 512, device=dev)
-    Ho = torch.empty_like(H)
-    wo = (torch.randn(512, 512, device=dev) * 0.05).to(bf)
-    bo = torch.randn(512, device=dev)
-    case("gemm to_out (NT, drop+resid)", lambda: E.gemm(xn, wo, Ho, n, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16,
-                                                        c_dtype=F32, bias=bo, drop_p=0.7, seed=3, resid=H,
-                                                        rowmap=(n, n - S, S, 0, 0, 0)), 2 * n * 512 * 512)
-    dq = torch.randn(n, 1536, device=dev).to(bf)
-    dx = torch.empty(n, 512, device=dev, dtype=bf)
-    case("gemm dxn (B k-strided)", lambda: E.gemm(dq, wqkv, dx, n, 512, 1536, lda=1536, ldb=512, ldc=512, b_kn=1,
-                                                  dtype=BF16), 2 * n * 1536 * 512)
-    dW = torch.empty(1536, 512, device=dev)
-    case("wgrad dWqkv (split-K + reduce)", lambda: E.weight_grad(dq, xn, dW, 1536, 512, n, ldy=1536, ldx=512,
-                                                                 dtype=BF16, work_pool=pool), 2 * n * 1536 * 512)
-    slab = torch.randn(8, 1536 * 512, device=dev)
-    case("splitk_reduce 8 x 786K", lambda: _lib.call("tm_splitk_reduce", E._p(slab), E._p(dW), 8, 1536 * 512,
-                                                     C.c_float(1.0), 0, st()), byts=9 * 1536 * 512 * 4)
-    slab2 = torch.randn(33, 512, device=dev)
-    ob = torch.empty(512, device=dev)
-    case("splitk_reduce 33 x 512", lambda: _lib.call("tm_splitk_reduce", E._p(slab2), E._p(ob), 33, 512,
-                                                     C.c_float(1.0), 0, st()))
+        def plain_gemm(K_):
+            g = _lib.GemmArgs()
+            g.M, g.N, g.K = n, 1536, K_
+            g.lda, g.ldb, g.ldc = 512, 512, 1536
+            g.ab_dtype, g.c_dtype = BF16, F32
+            g.splits, g.k_per_split = 1, 512
+            g.mode = _lib.EPI_SPLITK
+            g.alpha = 1.0
+            _lib.call("tm_gemm", E._p(xn), E._p(wqkv), E._p(slabq), C.byref(g), st())
+        case("gemm qkv shape, plain fp32 store", lambda: plain_gemm(512), 2 * n * 1536 * 512)
+        case("gemm qkv shape, K=64 plain store", lambda: plain_gemm(64), 2 * n * 1536 * 64)
+        outb = torch.empty(n, 1536, device=dev, dtype=bf)
+        case("torch.matmul bf16 (hipBLASLt) qkv", lambda: torch.matmul(xn, wqkv.t(), out=outb), 2 * n * 1536 * 512)
+        H = torch.randn(S, 512, device=dev)
+        Ho = torch.empty_like(H)
+        wo = (torch.randn(512, 512, device=dev) * 0.05).to(bf)
+        bo = torch.randn(512, device=dev)
+        case("gemm to_out (NT, drop+resid)", lambda: E.gemm(xn, wo, Ho, n, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16,
+                                                            c_dtype=F32, bias=bo, drop_p=0.7, seed=3, resid=H,
+                                                            rowmap=(n, n - S, S, 0, 0, 0)), 2 * n * 512 * 512)
+        case("gemm to_out shape, bias only", lambda: E.gemm(xn, wo, Ho, n, 512, 512, lda=512, ldb=512, ldc=512,
+                                                            dtype=BF16, c_dtype=F32, bias=bo), 2 * n * 512 * 512)
+        case("torch.matmul bf16 to_out shape", lambda: torch.matmul(xn, wo.t(), out=outb[:, :512]), 2 * n * 512 * 512)
+        dq = torch.randn(n, 1536, device=dev).to(bf)
+        dx = torch.empty(n, 512, device=dev, dtype=bf)
+        case("gemm dxn (B k-strided)", lambda: E.gemm(dq, wqkv, dx, n, 512, 1536, lda=1536, ldb=512, ldc=512, b_kn=1,
+                                                      dtype=BF16), 2 * n * 1536 * 512)
+        dW = torch.empty(1536, 512, device=dev)
+        case("wgrad dWqkv (split-K + reduce)", lambda: E.weight_grad(dq, xn, dW, 1536, 512, n, ldy=1536, ldx=512,
+                                                                     dtype=BF16, work_pool=pool), 2 * n * 1536 * 512)
+        slab = torch.randn(8, 1536 * 512, device=dev)
+        case("splitk_reduce 8 x 786K", lambda: _lib.call("tm_splitk_reduce", E._p(slab), E._p(dW), 8, 1536 * 512,
+                                                         C.c_float(1.0), 0, st()), byts=9 * 1536 * 512 * 4)
+        slab2 = torch.randn(33, 512, device=dev)
+        ob = torch.empty(512, device=dev)
+        case("splitk_reduce 33 x 512", lambda: _lib.call("tm_splitk_reduce", E._p(slab2), E._p(ob), 33, 512,
+                                                         C.c_float(1.0), 0, st()))
+    _lib.lib().tm_debug_set_variant(2, 0)
+    tag[0] = ""
+
     # ---------------- NystromAttention core ----------------
     q = (torch.randn(nbh, n, 64, device=dev) * 0.3).to(bf)
     k = (torch.randn(nbh, n, 64, device=dev) * 0.3).to(bf)

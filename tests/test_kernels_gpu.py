@@ -24,11 +24,13 @@ def _rel(a, b):
 # ----------------------------------------------------------------------------- GEMM
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("a_trans,b_kn", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_gemm_layouts(dtype, a_trans, b_kn):
+@pytest.mark.parametrize("K", [168, 320])
+def test_gemm_layouts(dtype, a_trans, b_kn, K):
+    """K = 168: register-staged loop; K = 320 (bf16): the global_load_lds ring."""
     from transmil_deepgraft_amd.engine import gemm
     from transmil_deepgraft_amd._lib import BF16, F32
     code = BF16 if dtype == torch.bfloat16 else F32
-    M, N, K = 296, 256, 168   # M: not a tile multiple, but 16-B rows when stored transposed
+    M, N = 296, 264   # not tile multiples, but 16-B rows when stored transposed
     g = torch.Generator(device="cpu").manual_seed(1)
     A = torch.randn(M, K, generator=g).to(dtype)
     B = torch.randn(K, N, generator=g).to(dtype)
@@ -92,6 +94,20 @@ def test_gemm_dropout_residual_and_splitk():
     X = torch.randn(4000, 160, generator=g)
     res = torch.empty(96, 160, device=DEV)
     weight_grad(dY.to(DEV), X.to(DEV), res, 96, 160, 4000, ldy=96, ldx=160, dtype=F32, work_pool=Pool(DEV))
+    torch.cuda.synchronize()
+    assert _rel(res.cpu(), dY.double().t() @ X.double()) < 1e-5
+
+
+def test_gemm_ring_splitk_weight_grad_bf16():
+    """bf16 split-K weight gradient through the global_load_lds ring (K = 33 x 256)."""
+    from transmil_deepgraft_amd.engine import weight_grad, Pool
+    from transmil_deepgraft_amd._lib import BF16
+    g = torch.Generator().manual_seed(5)
+    K = 33 * 256
+    dY = torch.randn(K, 192, generator=g).bfloat16()
+    X = torch.randn(K, 136, generator=g).bfloat16()
+    res = torch.empty(192, 136, device=DEV)
+    weight_grad(dY.to(DEV), X.to(DEV), res, 192, 136, K, ldy=192, ldx=136, dtype=BF16, work_pool=Pool(DEV))
     torch.cuda.synchronize()
     assert _rel(res.cpu(), dY.double().t() @ X.double()) < 1e-5
 

@@ -27,6 +27,7 @@
 namespace {
 
 constexpr int BM = 128, BN = 128;
+constexpr int EP_ROW = BN + 8;  // epilogue image row (floats): the two lane halves (rows r, r+4) on distinct banks
 
 template <typename T> struct Tile {
   static constexpr int E = 16 / sizeof(T);             // elements per 16-B chunk
@@ -130,8 +131,136 @@ constexpr int tile_elems() {
   return (TRANS && sizeof(T) == 2) ? Tile<T>::BK * Tile<T>::TROW : BM * Tile<T>::KROW;
 }
 
+// Epilogue shared by both main loops: the 2x2 (32x32) accumulators of each of the 4 waves
+// (2x2 waves of 64x64) -> LDS [128][EP_ROW] fp32, then 8-column row chunks with 16-B
+// loads/stores: bias, pre-activation store, GELU, dropout, residual, accumulate, and the
+// TransMIL row maps (grid duplication, QKV head-major scatter, split-K slabs).
+// The caller guarantees every wave is past its last read of the staging buffers.
 template <typename OutT>
-TM_DEV void put(OutT* p, float v) { *p = from_f<OutT>(v); }
+TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0);
+
+// accumulator tile (32x32 at rows rb, cols cb of the block tile) -> epilogue image
+TM_DEV void stage_acc(float* ep, const f32x16& acc, int rb, int cb, int lane) {
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) ep[(rb + acc_row(r, h)) * EP_ROW + cb + l32] = acc[r];
+}
+
+template <typename OutT>
+TM_DEV void gemm_epilogue(const f32x16 (&acc)[2][2], char* smem, OutT* __restrict__ C, const tm_gemm_args& g,
+                          int m0, int n0) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  float* ep = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) stage_acc(ep, acc[i][j], wm * 64 + i * 32, wn * 64 + j * 32, lane);
+  __syncthreads();
+  gemm_epilogue_rows<OutT>(smem, C, g, m0, n0);
+}
+
+// the chunk phase: every thread of the block walks 8-column row chunks of the staged tile
+template <typename OutT>
+TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0) {
+  const int tid = threadIdx.x;
+  const float* ep = (const float*)smem;
+  const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
+  const size_t slab = (size_t)blockIdx.z * g.M * g.N;
+  for (int c = tid; c < BM * (BN / 8); c += blockDim.x) {
+    const int lr = c >> 4, lc = (c & 15) * 8;
+    const int m = m0 + lr, n = n0 + lc;
+    if (m >= g.M || n >= g.N) continue;
+    float v[8];
+    {
+      const f32x4 lo = *(const f32x4*)(ep + lr * EP_ROW + lc), hi = *(const f32x4*)(ep + lr * EP_ROW + lc + 4);
+      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    }
+    const int ne = min(8, g.N - n);  // valid columns in this chunk
+    if (g.mode == TM_EPI_SPLITK) {
+      float* dst = (float*)C + slab + (size_t)m * g.N + n;
+      if (ne == 8 && g.N % 4 == 0) {
+        *(f32x4*)dst = (f32x4){v[0], v[1], v[2], v[3]};
+        *(f32x4*)(dst + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+      } else {
+        for (int e = 0; e < ne; ++e) dst[e] = v[e];
+      }
+      continue;
+    }
+    if (g.mode == TM_EPI_QKV) {  // 8 columns never straddle a head (dh % 8 == 0, checked on the host)
+      const int bag = m / g.seq, t = m - bag * g.seq;
+      const int inner = g.nh * g.dh;
+      const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
+      OutT* dst = C + (((long long)which * g.nbags + bag) * g.nh + hh) * g.seq * g.dh + (long long)t * g.dh + d;
+      const float qs = which == 0 ? g.qscale : 1.f;
+      vec8<OutT> o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = from_f<OutT>((v[e] * g.alpha + (g.bias ? g.bias[n + e] : 0.f)) * qs);
+      store8<OutT>(dst, o);
+      continue;
+    }
+    int row = m, dup_row = -1;
+    if (g.grp_in > 0) {
+      const int bag = m / g.grp_in, t = m - bag * g.grp_in - g.skip;
+      if (t < 0) continue;
+      row = bag * g.grp_out + g.out_off + t;
+      if (t < g.dup_n) dup_row = bag * g.grp_out + g.dup_off + t;
+    }
+    const size_t off = (size_t)row * g.ldc + n;
+    const bool vec = ne == 8 && g.ldc % 8 == 0 && (!g.pre || g.ld_pre % 8 == 0);
+    float bv[8], rv[8], cv[8];
+    if (vec) {
+      if (g.bias) { const f32x8 t8 = load8<float>(g.bias + n); for (int e = 0; e < 8; ++e) bv[e] = t8[e]; }
+      if (g.resid) { const f32x8 t8 = load8<float>(g.resid + off); for (int e = 0; e < 8; ++e) rv[e] = t8[e]; }
+      if (g.accumulate) { const vec8<OutT> t8 = load8<OutT>(C + off); for (int e = 0; e < 8; ++e) cv[e] = to_f(t8[e]); }
+    } else {
+      for (int e = 0; e < ne; ++e) {
+        bv[e] = g.bias ? g.bias[n + e] : 0.f;
+        rv[e] = g.resid ? g.resid[off + e] : 0.f;
+        cv[e] = g.accumulate ? to_f(C[off + e]) : 0.f;
+      }
+    }
+    vec8<OutT> pre8, out8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = v[e] * g.alpha + (g.bias ? bv[e] : 0.f);
+      pre8[e] = from_f<OutT>(x);
+      if (g.gelu) x = gelu_erf(x);
+      if (g.drop_p > 0.f) {
+        const float u = dropout_u01(seed, (uint32_t)row, (uint32_t)(n + e));
+        x = (u >= g.drop_p) ? x * g.drop_scale : 0.f;
+      }
+      if (g.resid) x += rv[e];
+      if (g.accumulate) x += cv[e];
+      out8[e] = from_f<OutT>(x);
+    }
+    if (vec) {
+      if (g.pre) store8<OutT>((OutT*)g.pre + (size_t)m * g.ld_pre + n, pre8);
+      store8<OutT>(C + off, out8);
+      if (dup_row >= 0) store8<OutT>(C + (size_t)dup_row * g.ldc + n, out8);
+    } else {
+      for (int e = 0; e < ne; ++e) {
+        if (g.pre) ((OutT*)g.pre)[(size_t)m * g.ld_pre + n + e] = pre8[e];
+        C[off + e] = out8[e];
+        if (dup_row >= 0) C[(size_t)dup_row * g.ldc + n + e] = out8[e];
+      }
+    }
+  }
+}
+
+
+
+// XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so renumber them
+// so that each XCD gets a contiguous run of row-major tiles (its row panels of A stay in
+// its own L2).  Bijective for any grid size.
+TM_DEV void tile_of_block(int& m0, int& n0) {
+  const int ntx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int orig = blockIdx.y * ntx + blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  m0 = (id / ntx) * BM;
+  n0 = (id % ntx) * BN;
+}
 
 template <typename T, typename OutT, bool A_T, bool B_KN>
 __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
@@ -144,8 +273,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
   T* Bs0 = As0 + 2 * AE;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, h = lane >> 5, l32 = lane & 31;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int wm = wave >> 1, wn = wave & 1;
+  int m0, n0;
+  tile_of_block(m0, n0);
   const int kbeg = blockIdx.z * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
@@ -194,87 +324,163 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
     __syncthreads();
   }
 
-  // ---------------- epilogue: row / column bookkeeping hoisted out of the element loop ----------------
-  int ncol[2];
-  float bcol[2];
-  long long cpart[2];   // QKV: column part of the scatter offset
-  bool qcol[2];
+  gemm_epilogue<OutT>(acc, smem, C, g, m0, n0);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 main loop v2: a 4-stage ring of LDS tiles filled by global_load_lds (16 B per
+// lane, no VGPR round trip), so three 64-deep k-tiles are in flight while one is
+// multiplied.  Per stage: A and B 128 x 64 bf16 images of 16 KB each (128 KB ring,
+// one workgroup per CU).  Sync per k-tile: counted `s_waitcnt vmcnt` (never 0 in
+// steady state) + raw s_barrier, which also retires the buffer the next prefetch
+// overwrites (read in the previous iteration).
+// LDS images (bank-clean reads, swizzle applied on the global source address):
+//   k-contiguous operand [128 rows][64 k]: 16-B chunk c of row r at slot c ^ ((r >> 1) & 7)
+//     -> fragment = one ds_read_b128 per lane (16 consecutive rows hit 16 distinct bank groups)
+//   k-strided operand [64 k][128 rows]: chunk c of k-row k at slot c ^ (2 * (k & 3))
+//     -> fragment = two ds_read_b64_tr_b16 (4 k-rows x 2 chunks per 16-lane group all distinct)
+constexpr int NSTAGE = 4;
+constexpr int STAGE_BYTES = 2 * 128 * 64 * 2;  // A + B images
+constexpr int RING_BYTES = NSTAGE * STAGE_BYTES;
+
+// One operand image of one stage: 16 wave-instructions of 1 KB, 2 per wave (8 waves).
+template <bool KSTRIDED>
+TM_DEV void glds_tile(char* img, const bf16* X, int ld, int r0, int rmax, int k0, int wave, int lane) {
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + j * 32 + l32;
-    ncol[j] = n;
-    bcol[j] = (g.bias && n < g.N) ? g.bias[n] : 0.f;
-    if (g.mode == TM_EPI_QKV) {
-      const int inner = g.nh * g.dh;
-      const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
-      cpart[j] = ((long long)which * g.nbags * g.nh + hh) * g.seq * g.dh + d;
-      qcol[j] = which == 0;
-    } else {
-      cpart[j] = 0;
-      qcol[j] = false;
+  for (int i = 0; i < 2; ++i) {
+    const int j = wave * 2 + i;  // 1-KB piece of the image
+    const bf16* src;
+    if constexpr (!KSTRIDED) {   // rows r0.., 8 rows x 128 B per piece
+      const int r = j * 8 + (lane >> 3), slot = lane & 7;
+      const int c = slot ^ ((r >> 1) & 7);
+      const int gr = min(r0 + r, rmax - 1);
+      src = X + (size_t)gr * ld + k0 + c * 8;
+    } else {                     // k-rows k0.., 4 rows x 256 B per piece
+      const int k = j * 4 + (lane >> 4), slot = lane & 15;
+      const int c = slot ^ (2 * (k & 3));
+      const int gm = min(r0 + c * 8, rmax - 8);
+      src = X + (size_t)(k0 + k) * ld + gm;
+    }
+    __builtin_amdgcn_global_load_lds((glb_t*)src, (lds_t*)(img + j * 1024), 16, 0, 0);
+  }
+}
+
+// fragment of 32 rows (rb..rb+31) x 8 k (kb + 8h ..) from a k-contiguous image
+TM_DEV bf16x8 frag_rows_sw(const char* img, int rb, int kb, int lane) {
+  const int r = rb + (lane & 31), c = (kb >> 3) + (lane >> 5);
+  return *(const bf16x8*)(img + r * 128 + ((c ^ ((r >> 1) & 7)) << 4));
+}
+// same fragment from a k-strided image via transposing reads
+TM_DEV bf16x8 frag_kstr_sw(const char* img, int mb, int kb, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int m = mb + (g & 1) * 16 + 4 * p;
+  const int k = kb + 8 * (g >> 1) + q;
+  const int c = m >> 3, half = (m >> 2) & 1;
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_v4*)(img + k * 256 + ((c ^ (2 * (k & 3))) << 4) + half * 8));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (lds_v4*)(img + (k + 4) * 256 + ((c ^ (2 * ((k + 4) & 3))) << 4) + half * 8));
+  return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int N>
+TM_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <typename OutT, bool A_T, bool B_KN>
+__global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                        OutT* __restrict__ C, tm_gemm_args g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 4 (M) x 2 (N) waves of 32 x 64
+  int m0, n0;
+  tile_of_block(m0, n0);
+  const int kbeg = blockIdx.z * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg) / 64 : 0;  // host guarantees 64 | (kend - kbeg)
+
+  f32x16 acc[2];
+  acc[0] = (f32x16){};
+  acc[1] = (f32x16){};
+
+  auto issue = [&](int kt) {
+    char* st = smem + (kt % NSTAGE) * STAGE_BYTES;
+    const int k0 = kbeg + kt * 64;
+    glds_tile<A_T>(st, A, g.lda, m0, g.M, k0, wave, lane);
+    glds_tile<B_KN>(st + STAGE_BYTES / 2, B, g.ldb, n0, g.N, k0, wave, lane);
+  };
+#pragma unroll
+  for (int t = 0; t < NSTAGE - 1; ++t)
+    if (t < nk) issue(t);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's pieces of tile kt have landed once at most (tiles issued after kt) x 4 loads remain
+    const int ahead = min(NSTAGE - 2, nk - 1 - kt);
+    if (ahead >= 2) wait_vm<8>(); else if (ahead == 1) wait_vm<4>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave done reading tile kt-1
+    asm volatile("" ::: "memory");
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1);  // overwrites tile kt-1's buffer
+    const char* sa = smem + (kt % NSTAGE) * STAGE_BYTES;
+    const char* sb = sa + STAGE_BYTES / 2;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 af = A_T ? frag_kstr_sw(sa, wm * 32, s * 16, lane) : frag_rows_sw(sa, wm * 32, s * 16, lane);
+      bf16x8 bfr[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = B_KN ? frag_kstr_sw(sb, wn * 64 + j * 32, s * 16, lane) : frag_rows_sw(sb, wn * 64 + j * 32, s * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) mma16(acc[j], af, bfr[j]);
     }
   }
-  const size_t slab = (size_t)blockIdx.z * g.M * g.N;
-  const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
+  __syncthreads();  // all fragment reads done before the epilogue reuses the ring
+  float* ep = (float*)smem;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm * 64 + i * 32 + acc_row(r, h);
-      if (m >= g.M) continue;
-      if (g.mode == TM_EPI_SPLITK) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          if (ncol[j] < g.N) ((float*)C)[slab + (size_t)m * g.N + ncol[j]] = acc[i][j][r];
-        continue;
-      }
-      if (g.mode == TM_EPI_QKV) {
-        const int bag = m / g.seq, t = m - bag * g.seq;
-        const long long rpart = ((long long)bag * g.nh * g.seq + t) * g.dh;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (ncol[j] >= g.N) continue;
-          float v = acc[i][j][r] * g.alpha + bcol[j];
-          if (qcol[j]) v *= g.qscale;
-          put(C + rpart + cpart[j], v);
-        }
-        continue;
-      }
-      int row = m, dup_row = -1;
-      if (g.grp_in > 0) {
-        const int bag = m / g.grp_in, t = m - bag * g.grp_in - g.skip;
-        if (t < 0) continue;
-        row = bag * g.grp_out + g.out_off + t;
-        if (t < g.dup_n) dup_row = bag * g.grp_out + g.dup_off + t;
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = ncol[j];
-        if (n >= g.N) continue;
-        float v = acc[i][j][r] * g.alpha + bcol[j];
-        if (g.pre) put((OutT*)g.pre + (size_t)m * g.ld_pre + n, v);
-        if (g.gelu) v = gelu_erf(v);
-        if (g.drop_p > 0.f) {
-          const float u = dropout_u01(seed, (uint32_t)row, (uint32_t)n);
-          v = (u >= g.drop_p) ? v * g.drop_scale : 0.f;
-        }
-        const size_t off = (size_t)row * g.ldc + n;
-        if (g.resid) v += g.resid[off];
-        if (g.accumulate) v += to_f(C[off]);
-        put(C + off, v);
-        if (dup_row >= 0) put(C + (size_t)dup_row * g.ldc + n, v);
-      }
-    }
+  for (int j = 0; j < 2; ++j) stage_acc(ep, acc[j], wm * 32, wn * 64 + j * 32, lane);
+  __syncthreads();
+  gemm_epilogue_rows<OutT>(smem, C, g, m0, n0);
 }
 
 template <typename T, bool A_T, bool B_KN>
 constexpr size_t gemm_smem() {
-  return 2 * (tile_elems<T, A_T>() + tile_elems<T, B_KN>()) * sizeof(T);
+  constexpr size_t main = 2 * (tile_elems<T, A_T>() + tile_elems<T, B_KN>()) * sizeof(T);
+  constexpr size_t epi = (size_t)BM * EP_ROW * sizeof(float);
+  return main > epi ? main : epi;
+}
+
+int g_gemm_variant = 0;  // debug: 1 = always the register-staged loop
+
+template <typename OutT>
+bool ring_ok(const tm_gemm_args& g) {
+  if (g_gemm_variant == 1) return false;
+  // whole 64-deep k-tiles in every split; k-strided operands need >= 8 rows/cols (clamped 16-B pieces)
+  if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
+  if ((g.a_trans && g.M < 8) || (g.b_kn && g.N < 8)) return false;
+  if (g.a_trans && g.M % 8 != 0) return false;
+  if (g.b_kn && g.N % 8 != 0) return false;
+  return true;
 }
 
 template <typename T, typename OutT>
 int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.splits);
+  if constexpr (sizeof(T) == 2) {
+    if (ring_ok<OutT>(g)) {
+      constexpr size_t epi = (size_t)BM * EP_ROW * sizeof(float);
+      constexpr size_t sm = RING_BYTES > epi ? RING_BYTES : epi;
+#define TM_RING_CASE(AT, BKN)                                                                   \
+      if (g.a_trans == AT && g.b_kn == BKN) {                                                   \
+        tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN>, sm);                                     \
+        gemm_ring_kernel<OutT, AT, BKN><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        TM_CHECK_LAUNCH();                                                                      \
+        return 0;                                                                               \
+      }
+      TM_RING_CASE(0, 0) TM_RING_CASE(0, 1) TM_RING_CASE(1, 0) TM_RING_CASE(1, 1)
+#undef TM_RING_CASE
+    }
+  }
   const T* a = (const T*)A;
   const T* b = (const T*)B;
   OutT* c = (OutT*)C;
@@ -341,6 +547,7 @@ extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args
   TM_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "gemm: operands must be 16-B aligned");
   const int E = g->ab_dtype == TM_BF16 ? 8 : 4;
   TM_REQUIRE(g->lda % E == 0 && g->ldb % E == 0, "gemm: leading dimensions must be multiples of 16 B");
+  TM_REQUIRE(g->mode != TM_EPI_QKV || (g->dh % 8 == 0 && g->N % 8 == 0), "gemm: QKV scatter needs dh % 8 == 0");
   if (g->M == 0 || g->N == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   if (g->ab_dtype == TM_BF16) {
@@ -353,6 +560,8 @@ extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args
   if (g->c_dtype == TM_BF16) return launch_t<float, bf16>(A, B, C, *g, st);
   return launch_t<float, float>(A, B, C, *g, st);
 }
+
+extern "C" void tm_debug_set_gemm_variant(int value) { g_gemm_variant = value; }
 
 extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
                                 int accumulate, void* stream) {

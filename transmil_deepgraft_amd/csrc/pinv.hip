@@ -300,9 +300,11 @@ extern "C" int tm_debug_xcc_map(int* out, int nblocks, int threads, void* stream
 }
 
 extern "C" void tm_debug_set_nys_variant(int value);
+extern "C" void tm_debug_set_gemm_variant(int value);
 extern "C" void tm_debug_set_variant(int which, int value) {
   if (which == 0) g_bmm_variant = value;
   if (which == 1) tm_debug_set_nys_variant(value);
+  if (which == 2) tm_debug_set_gemm_variant(value);
 }
 
 extern "C" int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream) {
