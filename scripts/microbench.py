@@ -111,11 +111,15 @@ def main():
     case("bmm 2-job 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
                                               E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh), 2 * f)
     case("bmm NN 256^3 x8 [bf16x3]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh, 1), f)
-    for var, nm in ((1, "no loads/MFMA"), (2, "loads only"), (3, "no E terms"), (4, "store only")):
+    for var, nm in ((1, "no loads/MFMA"), (2, "loads only"), (4, "store only"), (5, "A loads only"),
+                    (6, "B loads only"), (7, "tiny footprint"), (8, "B as NT")):
         _lib.lib().tm_debug_set_variant(0, var)
         case(f"bmm NN+E1 bf16x3 [{nm}]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256, E1=Y2, e1=1.0)],
                                                          nbh, 1), f)
     _lib.lib().tm_debug_set_variant(0, 0)
+    case("bmm NT bf16x3", lambda: E.bmm([E.bmm_job(X, 0, Z, 1, P, 256, 256, 256)], nbh, 1), f)
+    case("bmm TN bf16x3", lambda: E.bmm([E.bmm_job(X, 1, Z, 0, P, 256, 256, 256)], nbh, 1), f)
+    case("bmm Y=ZW bf16x3", lambda: E.bmm([E.bmm_job(Z, 0, W, 0, Y, 256, 64, 256)], nbh, 1), f // 4)
     case("bmm dependent pair bf16x3 (per bmm)", lambda: (E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh, 1),
                                                         E.bmm([E.bmm_job(X, 0, P, 0, Z2, 256, 256, 256)], nbh, 1)), 2 * f)
     _lib.lib().tm_debug_set_variant(0, 0)
@@ -127,9 +131,9 @@ def main():
     saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=dev)
     case("pinv_fwd (26 launches)", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 0, E._p(saved), st()), 24 * f)
     case("pinv_fwd [bf16x3]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 1, E._p(saved), st()), 24 * f)
-    for gv in ((0, 1) if args.gemm_ab else (0,)):
+    for gv in ((0, 1, 2) if args.gemm_ab else (0,)):
         _lib.lib().tm_debug_set_variant(2, gv)
-        tag[0] = "[old loop] " if gv else ""
+        tag[0] = ("", "[2 LDS buf] ", "[glds ring] ")[gv]
         # ---------------- GEMMs ----------------
         pool = E.Pool(dev)
         xn = torch.randn(n, 512, device=dev).to(bf)
@@ -174,7 +178,10 @@ def main():
                                                          C.c_float(1.0), 0, st()), byts=9 * 1536 * 512 * 4)
         slab2 = torch.randn(33, 512, device=dev)
         ob = torch.empty(512, device=dev)
-        case("splitk_reduce 33 x 512", lambda: _lib.call("tm_splitk_reduce", E._p(slab2), E._p(ob), 33, 512,
+        nf = torch.empty(n * 1536, device=dev)
+    case("torch fill 52 MB fp32", lambda: nf.fill_(1.0), byts=n * 1536 * 4)
+    case("torch copy 52 MB fp32", lambda: slabq.view(-1).copy_(nf), byts=2 * n * 1536 * 4)
+    case("splitk_reduce 33 x 512", lambda: _lib.call("tm_splitk_reduce", E._p(slab2), E._p(ob), 33, 512,
                                                          C.c_float(1.0), 0, st()))
     _lib.lib().tm_debug_set_variant(2, 0)
     tag[0] = ""

@@ -22,10 +22,19 @@ def _rel(a, b):
 
 
 # ----------------------------------------------------------------------------- GEMM
+@pytest.fixture(params=[0, 1, 2], ids=["1buf", "2buf", "ring"])
+def gemm_variant(request):
+    """Every GEMM main loop (register-staged 1 / 2 LDS buffers, global_load_lds ring)."""
+    from transmil_deepgraft_amd import _lib
+    _lib.lib().tm_debug_set_variant(2, request.param)
+    yield request.param
+    _lib.lib().tm_debug_set_variant(2, 0)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("a_trans,b_kn", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("K", [168, 320])
-def test_gemm_layouts(dtype, a_trans, b_kn, K):
+def test_gemm_layouts(dtype, a_trans, b_kn, K, gemm_variant):
     """K = 168: register-staged loop; K = 320 (bf16): the global_load_lds ring."""
     from transmil_deepgraft_amd.engine import gemm
     from transmil_deepgraft_amd._lib import BF16, F32
@@ -45,7 +54,7 @@ def test_gemm_layouts(dtype, a_trans, b_kn, K):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_epilogue_bias_gelu_rowmap_dup(dtype):
+def test_gemm_epilogue_bias_gelu_rowmap_dup(dtype, gemm_variant):
     from transmil_deepgraft_amd.engine import gemm
     from transmil_deepgraft_amd._lib import BF16, F32
     code = BF16 if dtype == torch.bfloat16 else F32
@@ -98,7 +107,7 @@ def test_gemm_dropout_residual_and_splitk():
     assert _rel(res.cpu(), dY.double().t() @ X.double()) < 1e-5
 
 
-def test_gemm_ring_splitk_weight_grad_bf16():
+def test_gemm_ring_splitk_weight_grad_bf16(gemm_variant):
     """bf16 split-K weight gradient through the global_load_lds ring (K = 33 x 256)."""
     from transmil_deepgraft_amd.engine import weight_grad, Pool
     from transmil_deepgraft_amd._lib import BF16
@@ -113,7 +122,7 @@ def test_gemm_ring_splitk_weight_grad_bf16():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_qkv_scatter(dtype):
+def test_gemm_qkv_scatter(dtype, gemm_variant):
     from transmil_deepgraft_amd.engine import gemm
     from transmil_deepgraft_amd._lib import BF16, F32
     code = BF16 if dtype == torch.bfloat16 else F32

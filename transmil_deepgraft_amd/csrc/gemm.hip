@@ -137,7 +137,7 @@ constexpr int tile_elems() {
 // TransMIL row maps (grid duplication, QKV head-major scatter, split-K slabs).
 // The caller guarantees every wave is past its last read of the staging buffers.
 template <typename OutT>
-TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0);
+TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows);
 
 // accumulator tile (32x32 at rows rb, cols cb of the block tile) -> epilogue image
 TM_DEV void stage_acc(float* ep, const f32x16& acc, int rb, int cb, int lane) {
@@ -152,22 +152,29 @@ TM_DEV void gemm_epilogue(const f32x16 (&acc)[2][2], char* smem, OutT* __restric
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   float* ep = (float*)smem;
+  // two passes of 64 rows (the image is 64 x EP_ROW fp32 = 34.8 KB)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) stage_acc(ep, acc[i][j], wm * 64 + i * 32, wn * 64 + j * 32, lane);
-  __syncthreads();
-  gemm_epilogue_rows<OutT>(smem, C, g, m0, n0);
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) stage_acc(ep, acc[i][j], i * 32, wn * 64 + j * 32, lane);
+    }
+    __syncthreads();
+    gemm_epilogue_rows<OutT>(smem, C, g, m0 + half * 64, n0, 64);
+    __syncthreads();
+  }
 }
 
 // the chunk phase: every thread of the block walks 8-column row chunks of the staged tile
 template <typename OutT>
-TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0) {
+TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows) {
   const int tid = threadIdx.x;
   const float* ep = (const float*)smem;
   const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
   const size_t slab = (size_t)blockIdx.z * g.M * g.N;
-  for (int c = tid; c < BM * (BN / 8); c += blockDim.x) {
+  for (int c = tid; c < rows * (BN / 8); c += blockDim.x) {
     const int lr = c >> 4, lc = (c & 15) * 8;
     const int m = m0 + lr, n = n0 + lc;
     if (m >= g.M || n >= g.N) continue;
@@ -262,7 +269,9 @@ TM_DEV void tile_of_block(int& m0, int& n0) {
   n0 = (id % ntx) * BN;
 }
 
-template <typename T, typename OutT, bool A_T, bool B_KN>
+// NBUF = 2: double-buffered LDS (one barrier per k-tile); NBUF = 1: one LDS buffer, two
+// barriers per k-tile, half the LDS -> twice the resident workgroups per CU.
+template <typename T, typename OutT, bool A_T, bool B_KN, int NBUF = 2>
 __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, const T* __restrict__ B,
                                                    OutT* __restrict__ C, tm_gemm_args g) {
   using TT = Tile<T>;
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
   constexpr int AE = tile_elems<T, A_T>(), BE = tile_elems<T, B_KN>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* As0 = (T*)smem;
-  T* Bs0 = As0 + 2 * AE;
+  T* Bs0 = As0 + NBUF * AE;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -298,13 +307,21 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
     if constexpr (B_KN) store_cols(Bs0 + buf * BE, sb, tid); else store_rows(Bs0 + buf * BE, sb, tid);
   };
 
-  if (nk > 0) {
-    gload(kbeg);
-    lstore(0);
+  if constexpr (NBUF == 1) {
+    if (nk > 0) gload(kbeg);
+  } else {
+    if (nk > 0) {
+      gload(kbeg);
+      lstore(0);
+    }
+    __syncthreads();
   }
-  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = NBUF == 1 ? 0 : (kt & 1);
+    if constexpr (NBUF == 1) {
+      lstore(0);
+      __syncthreads();
+    }
     if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
     const T* as = As0 + cur * AE;
     const T* bs = Bs0 + cur * BE;
@@ -320,7 +337,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
 #pragma unroll
         for (int j = 0; j < 2; ++j) mma16(acc[i][j], af[i], bfr[j]);
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+    if (NBUF == 2 && kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();
   }
 
@@ -440,21 +457,21 @@ __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__
 #pragma unroll
   for (int j = 0; j < 2; ++j) stage_acc(ep, acc[j], wm * 32, wn * 64 + j * 32, lane);
   __syncthreads();
-  gemm_epilogue_rows<OutT>(smem, C, g, m0, n0);
+  gemm_epilogue_rows<OutT>(smem, C, g, m0, n0, BM);
 }
 
-template <typename T, bool A_T, bool B_KN>
+template <typename T, bool A_T, bool B_KN, int NBUF = 2>
 constexpr size_t gemm_smem() {
-  constexpr size_t main = 2 * (tile_elems<T, A_T>() + tile_elems<T, B_KN>()) * sizeof(T);
-  constexpr size_t epi = (size_t)BM * EP_ROW * sizeof(float);
+  constexpr size_t main = NBUF * (tile_elems<T, A_T>() + tile_elems<T, B_KN>()) * sizeof(T);
+  constexpr size_t epi = (size_t)(BM / 2) * EP_ROW * sizeof(float);
   return main > epi ? main : epi;
 }
 
-int g_gemm_variant = 0;  // debug: 1 = always the register-staged loop
+int g_gemm_variant = 0;  // debug: 0/1 = register-staged loop (1 / 2 LDS buffers), 2 = global_load_lds ring
 
 template <typename OutT>
 bool ring_ok(const tm_gemm_args& g) {
-  if (g_gemm_variant == 1) return false;
+  if (g_gemm_variant != 2) return false;
   // whole 64-deep k-tiles in every split; k-strided operands need >= 8 rows/cols (clamped 16-B pieces)
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if ((g.a_trans && g.M < 8) || (g.b_kn && g.N < 8)) return false;
@@ -486,9 +503,15 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
   OutT* c = (OutT*)C;
 #define TM_GEMM_CASE(AT, BKN)                                                       \
   if (g.a_trans == AT && g.b_kn == BKN) {                                           \
-    constexpr size_t sm = gemm_smem<T, AT, BKN>();                                  \
-    tm_allow_smem(gemm_kernel<T, OutT, AT, BKN>, sm);                               \
-    gemm_kernel<T, OutT, AT, BKN><<<grid, 256, sm, st>>>(a, b, c, g);               \
+    if (g_gemm_variant != 1) {                                                      \
+      constexpr size_t sm = gemm_smem<T, AT, BKN, 1>();                             \
+      tm_allow_smem(gemm_kernel<T, OutT, AT, BKN, 1>, sm);                          \
+      gemm_kernel<T, OutT, AT, BKN, 1><<<grid, 256, sm, st>>>(a, b, c, g);          \
+    } else {                                                                        \
+      constexpr size_t sm = gemm_smem<T, AT, BKN>();                                \
+      tm_allow_smem(gemm_kernel<T, OutT, AT, BKN>, sm);                             \
+      gemm_kernel<T, OutT, AT, BKN><<<grid, 256, sm, st>>>(a, b, c, g);             \
+    }                                                                               \
     TM_CHECK_LAUNCH();                                                              \
     return 0;                                                                       \
   }

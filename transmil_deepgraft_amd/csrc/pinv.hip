@@ -102,14 +102,24 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
       const float* B = term ? J.B2 + bh * J.sb2 : J.B + bh * J.sb;
       const int ta = term ? J.ta2 : J.ta, tb = term ? J.tb2 : J.tb;
       const int lda = term ? J.lda2 : J.lda, ldb = term ? J.ldb2 : J.ldb;
-      af[i] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
-      bfr[i] = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
+      if constexpr (VAR == 7) {  // tiny footprint: every block reads tile (0,0) of batch 0
+        af[i] = frag_a(J.A, ta, lda, r, kl + 8 * h);
+        bfr[i] = frag_b(J.B, tb, ldb, kl + 8 * h, r);
+      } else if constexpr (VAR == 8) {  // B read as if stored transposed (contiguous 32 B per lane)
+        af[i] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
+        bfr[i] = frag_b(B, 1, ldb, kl + 8 * h, tn * 32 + r);
+      } else {
+        if constexpr (VAR != 6) af[i] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
+        else af[i] = (f32x8){(float)lane, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+        if constexpr (VAR != 5) bfr[i] = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
+        else bfr[i] = (f32x8){(float)lane, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+      }
     }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     if (wave + BMM_WAVES * i < nsteps) {
-      if constexpr (VAR == 0 || VAR == 3) mma_f32_step<PREC>(acc, af[i], bfr[i]);
+      if constexpr (VAR == 0 || VAR == 3 || VAR >= 5) mma_f32_step<PREC>(acc, af[i], bfr[i]);
       if constexpr (VAR == 2) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += af[i][e] * bfr[i][e];
@@ -256,6 +266,10 @@ int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, hipStrea
       case 2: bmm_kernel<1, 2><<<total, 512, 0, st>>>(jp, nbatch); break;
       case 3: bmm_kernel<1, 3><<<total, 512, 0, st>>>(jp, nbatch); break;
       case 4: bmm_kernel<1, 4><<<total, 512, 0, st>>>(jp, nbatch); break;
+      case 5: bmm_kernel<1, 5><<<total, 512, 0, st>>>(jp, nbatch); break;
+      case 6: bmm_kernel<1, 6><<<total, 512, 0, st>>>(jp, nbatch); break;
+      case 7: bmm_kernel<1, 7><<<total, 512, 0, st>>>(jp, nbatch); break;
+      case 8: bmm_kernel<1, 8><<<total, 512, 0, st>>>(jp, nbatch); break;
       default: bmm_kernel<1><<<total, 512, 0, st>>>(jp, nbatch);
     }
   } else {
