@@ -245,6 +245,129 @@ __global__ __launch_bounds__(256) void pinv_init_bwd_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// Layout-specialised bmm.  The generic kernel above selects layouts and terms at run
+// time; hipcc then branches around the fragment loads and waits for each group
+// (s_waitcnt vmcnt between them) and reads the job fields with dependent loads from a
+// dynamically indexed kernel argument: several serial memory round trips per launch.
+// Here every job's layout, term count and k-slots are template constants, so each wave
+// issues all of its fragment loads back to back and waits once.
+// Layout code C: bit0 ta, bit1 tb, bit2 two terms (K = 256 each), bit3 ta2, bit4 tb2,
+// bits5-6 slots per wave: 0 -> 2 (K = 256), 1 -> 1 (K <= 128), 2 -> 4 (two terms).
+template <int TA>
+TM_DEV f32x8 fa(const float* A, int lda, int m, int k) {
+  if constexpr (TA == 0) return load8<float>(A + (size_t)m * lda + k);
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = A[(size_t)(k + e) * lda + m];
+  return r;
+}
+template <int TB>
+TM_DEV f32x8 fb(const float* B, int ldb, int k, int n) {
+  if constexpr (TB == 1) return load8<float>(B + (size_t)n * ldb + k);
+  f32x8 r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = B[(size_t)(k + e) * ldb + n];
+  return r;
+}
+
+template <int PREC, int C>
+TM_DEV void bmm_tile(const tm_bmm_job& J, int bh, int tile, float (*red)[16][64]) {
+  constexpr int TA = C & 1, TB = (C >> 1) & 1, TWO = (C >> 2) & 1, TA2 = (C >> 3) & 1, TB2 = (C >> 4) & 1;
+  constexpr int SK = (C >> 5) & 3;
+  constexpr int NSLOT = SK == 0 ? 2 : (SK == 1 ? 1 : 4);
+  const int ntn = J.N / 32;
+  const int m0 = (tile / ntn) * 32, n0 = (tile % ntn) * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  // epilogue operands first, so their latency overlaps the fragment loads
+  float ev1[2] = {0.f, 0.f}, ev2[2] = {0.f, 0.f};
+  size_t off[2];
+  int row[2], col[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = tid + 512 * q, reg = e >> 6, ln = e & 63;
+    row[q] = m0 + acc_row(reg, ln >> 5);
+    col[q] = n0 + (ln & 31);
+    off[q] = (size_t)bh * J.sc + (size_t)row[q] * J.ldc + col[q];
+  }
+  if (J.E1) { ev1[0] = J.E1[off[0]]; ev1[1] = J.E1[off[1]]; }
+  if (J.E2) { ev2[0] = J.E2[off[0]]; ev2[1] = J.E2[off[1]]; }
+  f32x16 acc = (f32x16){};
+  if (NSLOT > 1 || wave * 16 < J.K) {
+    const float* A = J.A + bh * J.sa;
+    const float* B = J.B + bh * J.sb;
+    f32x8 af[NSLOT], bf[NSLOT];
+#pragma unroll
+    for (int i = 0; i < NSLOT; ++i) {
+      const int kk = (wave + 8 * i) * 16 + 8 * h;
+      if constexpr (TWO) {
+        if (i >= 2) {
+          af[i] = fa<TA2>(J.A2 + bh * J.sa2, J.lda2, m0 + r, kk - 256);
+          bf[i] = fb<TB2>(J.B2 + bh * J.sb2, J.ldb2, kk - 256, n0 + r);
+          continue;
+        }
+      }
+      af[i] = fa<TA>(A, J.lda, m0 + r, kk);
+      bf[i] = fb<TB>(B, J.ldb, kk, n0 + r);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every fragment load is issued before the first MFMA waits
+#pragma unroll
+    for (int i = 0; i < NSLOT; ++i) mma_f32_step<PREC>(acc, af[i], bf[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[wave][i][lane] = acc[i];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int e = tid + 512 * q, reg = e >> 6, ln = e & 63;
+    float sum = red[0][reg][ln];
+#pragma unroll
+    for (int w = 1; w < BMM_WAVES; ++w) sum += red[w][reg][ln];
+    float v = J.alpha * sum;
+    if (row[q] == col[q]) v += J.diag;
+    v += J.e1 * ev1[q] + J.e2 * ev2[q];
+    J.C[off[q]] = v;
+  }
+}
+
+template <int PREC, int C0, int C1>
+__global__ __launch_bounds__(512) void bmm_spec_kernel(JobPair jp, int nbatch) {
+  __shared__ float red[BMM_WAVES][16][64];
+  const int b = blockIdx.x;
+  if (C1 < 0 || b < jp.tiles0 * nbatch) {
+    bmm_tile<PREC, C0>(jp.j[0], b % nbatch, b / nbatch, red);
+  } else {
+    const int b1 = b - jp.tiles0 * nbatch;
+    bmm_tile<PREC, (C1 < 0 ? 0 : C1)>(jp.j[1], b1 % nbatch, b1 / nbatch, red);
+  }
+}
+
+int bmm_code(const tm_bmm_job& J) {
+  if (J.A2) {
+    if (J.K != 256) return -1;
+    return (J.ta & 1) | (J.tb & 1) << 1 | 4 | (J.ta2 & 1) << 3 | (J.tb2 & 1) << 4 | 2 << 5;
+  }
+  if (J.K == 256) return (J.ta & 1) | (J.tb & 1) << 1;
+  if (J.K <= 128 && J.K % 16 == 0) return (J.ta & 1) | (J.tb & 1) << 1 | 1 << 5;
+  return -1;
+}
+
+template <int PREC>
+bool launch_spec(const JobPair& jp, int c0, int c1, int total, int nbatch, hipStream_t st) {
+#define TM_SPEC(A, B)                                                                  \
+  if (c0 == A && c1 == B) {                                                            \
+    bmm_spec_kernel<PREC, A, B><<<total, 512, 0, st>>>(jp, nbatch);                    \
+    return true;                                                                       \
+  }
+  // single jobs: every layout at K = 256 and K <= 128, and the two-term dP update
+  TM_SPEC(0, -1) TM_SPEC(1, -1) TM_SPEC(2, -1) TM_SPEC(3, -1)
+  TM_SPEC(32, -1) TM_SPEC(33, -1) TM_SPEC(34, -1) TM_SPEC(35, -1) TM_SPEC(78, -1)
+  // the job pairs of the pseudo-inverse backward and the landmark gradients
+  TM_SPEC(1, 2) TM_SPEC(2, 1) TM_SPEC(34, 1) TM_SPEC(0, 1) TM_SPEC(0, 2) TM_SPEC(0, 0)
+#undef TM_SPEC
+  return false;
+}
+
 int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, hipStream_t st) {
   TM_REQUIRE(njobs == 1 || njobs == 2, "bmm: njobs must be 1 or 2");
   JobPair jp{};
@@ -259,6 +382,17 @@ int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, hipStrea
     const int tiles = (J.M / 32) * (J.N / 32);
     if (i == 0) jp.tiles0 = tiles;
     total += tiles * nbatch;
+  }
+  if (g_bmm_variant == 0) {
+    const int c0 = bmm_code(jobs[0]), c1 = njobs > 1 ? bmm_code(jobs[1]) : -1;
+    if (c0 >= 0 && (njobs == 1 || c1 >= 0)) {
+      const bool ok = prec == 1 ? launch_spec<1>(jp, c0, c1, total, nbatch, st)
+                                : launch_spec<0>(jp, c0, c1, total, nbatch, st);
+      if (ok) {
+        TM_CHECK_LAUNCH();
+        return 0;
+      }
+    }
   }
   if (prec == 1) {
     switch (g_bmm_variant) {
