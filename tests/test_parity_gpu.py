@@ -92,6 +92,42 @@ def test_bf16_mode_close_to_oracle(N):
     np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=5e-2)
 
 
+@pytest.mark.parametrize("N", [1000, 4000])
+def test_bf16_mode_grads_close_to_oracle(N):
+    """Bench-mode (bf16 operands) gradients against the fp64 oracle: every parameter's
+    gradient within 6e-2 of its max magnitude (bf16 operands carry ~3 significant digits)."""
+    ref, ours = _pair(2, dtype=torch.bfloat16)
+    x = torch.from_numpy(bag_input(N, 512, 99 + N))
+    lr, gr = _ref_forward_backward(ref, x, 1, 2)
+    lo, go = _ours_forward_backward(ours, x, 1, 2)
+    np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=5e-2)
+    bad = []
+    for name, g in gr.items():
+        err = ((go[name].double() - g).abs().max() / g.abs().max().clamp_min(1e-12)).item()
+        if err > 6e-2:
+            bad.append((name, err))
+    assert not bad, bad
+
+
+def test_bf16_staged_attention_backward_is_bitwise_the_per_chunk_one():
+    """The once-staged bf16 attention backward (default) and the per-chunk-staged one
+    (variant 3) compute the same sums in the same order: gradients bitwise equal."""
+    from transmil_deepgraft_amd import _lib
+    ref, ours = _pair(2, dtype=torch.bfloat16)
+    x = torch.from_numpy(bag_input(3000, 512, 7))
+    grads = []
+    for variant in (0, 3):
+        _lib.lib().tm_debug_set_variant(1, variant)
+        try:
+            ours.zero_grad(set_to_none=True)
+            _, g = _ours_forward_backward(ours, x, 0, 2)
+        finally:
+            _lib.lib().tm_debug_set_variant(1, 0)
+        grads.append(g)
+    for name in grads[0]:
+        assert torch.equal(grads[0][name], grads[1][name]), name
+
+
 def test_return_attn_contract():
     """(logits, (attn [B,8,n',n'], padding)) with the class token at row `padding` (:209-210)."""
     ref, ours = _pair(2)

@@ -40,6 +40,28 @@ template <typename T> struct Tile {
 
 template <typename T> union Chunk { f32x4 raw; T e[16 / sizeof(T)]; };
 
+// Interior tiles (every row and k of the tile in range: a workgroup-uniform test) load
+// with no per-chunk bounds branches, so all chunk loads issue back to back and retire
+// with one wait; hipcc otherwise branches around each guarded load and waits for it.
+template <typename T>
+TM_DEV void load_rows_full(Chunk<T> (&st)[Tile<T>::CHUNKS], const T* X, int ld, int r0, int k0, int tid) {
+  constexpr int E = Tile<T>::E, CPR = Tile<T>::BK / E;
+#pragma unroll
+  for (int i = 0; i < Tile<T>::CHUNKS; ++i) {
+    const int c = tid + 256 * i;
+    st[i].raw = *(const f32x4*)(X + (size_t)(r0 + c / CPR) * ld + k0 + (c % CPR) * E);
+  }
+}
+template <typename T>
+TM_DEV void load_cols_full(Chunk<T> (&st)[Tile<T>::CHUNKS], const T* X, int ld, int m0, int k0, int tid) {
+  constexpr int E = Tile<T>::E, CPR = BM / E;
+#pragma unroll
+  for (int i = 0; i < Tile<T>::CHUNKS; ++i) {
+    const int c = tid + 256 * i;
+    st[i].raw = *(const f32x4*)(X + (size_t)(k0 + c / CPR) * ld + m0 + (c % CPR) * E);
+  }
+}
+
 // k-contiguous operand rows r0.. : chunk c -> row c / (BK/E), col (c % (BK/E)) * E
 template <typename T>
 TM_DEV void load_rows(Chunk<T> (&st)[Tile<T>::CHUNKS], const T* X, int ld, int r0, int rmax, int k0, int kend,
@@ -296,11 +318,19 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x16){};
 
   Chunk<T> sa[TT::CHUNKS], sb[TT::CHUNKS];
+  const bool rows_full = m0 + BM <= g.M && n0 + BN <= g.N;
   auto gload = [&](int k0) {
-    if constexpr (A_T) load_cols(sa, A, g.lda, m0, g.M, k0, kend, tid);
-    else load_rows(sa, A, g.lda, m0, g.M, k0, kend, tid);
-    if constexpr (B_KN) load_cols(sb, B, g.ldb, n0, g.N, k0, kend, tid);
-    else load_rows(sb, B, g.ldb, n0, g.N, k0, kend, tid);
+    if (rows_full && k0 + BK <= kend) {
+      if constexpr (A_T) load_cols_full(sa, A, g.lda, m0, k0, tid);
+      else load_rows_full(sa, A, g.lda, m0, k0, tid);
+      if constexpr (B_KN) load_cols_full(sb, B, g.ldb, n0, k0, tid);
+      else load_rows_full(sb, B, g.ldb, n0, k0, tid);
+    } else {
+      if constexpr (A_T) load_cols(sa, A, g.lda, m0, g.M, k0, kend, tid);
+      else load_rows(sa, A, g.lda, m0, g.M, k0, kend, tid);
+      if constexpr (B_KN) load_cols(sb, B, g.ldb, n0, g.N, k0, kend, tid);
+      else load_rows(sb, B, g.ldb, n0, g.N, k0, kend, tid);
+    }
   };
   auto lstore = [&](int buf) {
     if constexpr (A_T) store_cols(As0 + buf * AE, sa, tid); else store_rows(As0 + buf * AE, sa, tid);

@@ -752,6 +752,198 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 attention backward with every operand of the workgroup staged ONCE: the
+// workgroup's <= 256 query rows of Q and dO ([q][72] row-major images), their lse / D,
+// K^T and the wave's K / V fragments are all requested in one burst before the query
+// walk, so the walk itself issues no global loads (the per-chunk version paid two
+// dependent HBM round trips per 32-query chunk).  dV/dK operands come from the same
+// row-major images through transposing reads (acc_as_operand k order).
+struct BwdLay16 {
+  static constexpr int KT_ROW = NL + 8, DS_ROW = NL + 8, QROW = DH + 8;
+  static constexpr size_t KT_OFF = 0;
+  static constexpr size_t DS_OFF = KT_OFF + DH * KT_ROW * 2;
+  static constexpr size_t QS_OFF = DS_OFF + 32 * DS_ROW * 2;
+  static constexpr size_t OS_OFF = QS_OFF + NL * QROW * 2;
+  static constexpr size_t XC_OFF = OS_OFF + NL * QROW * 2;  // fp32 [3][2][1024]
+  static constexpr size_t LS_OFF = XC_OFF + 6 * 1024 * 4;   // fp32 lse[256], D[256]
+  static constexpr size_t MAIN = LS_OFF + 2 * NL * 4;
+  static constexpr size_t EPI = (size_t)NL * 68 * 4;
+  static constexpr size_t BYTES = MAIN > EPI ? MAIN : EPI;
+};
+
+// A-operand fragment (rows m = mb + l32, 8 k in acc_as_operand order) of a row-major
+// [k][QROW] bf16 image: element j of lane half h <-> k = kb + 8 (j >> 2) + 4 h + (j & 3)
+TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) {
+  constexpr int R = BwdLay16::QROW;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int m = mb + (g & 1) * 16 + 4 * p;
+  const int k = kb + 4 * (g >> 1) + q;
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(S + k * R + m));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(S + (k + 8) * R + m));
+  return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
+  using LY = BwdLay16;
+  constexpr int KT_ROW = LY::KT_ROW, DS_ROW = LY::DS_ROW, QROW = LY::QROW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* kt_s = (bf16*)(smem + LY::KT_OFF);
+  bf16* ds_s = (bf16*)(smem + LY::DS_OFF);
+  bf16* qs = (bf16*)(smem + LY::QS_OFF);
+  bf16* os = (bf16*)(smem + LY::OS_OFF);
+  float* xch = (float*)(smem + LY::XC_OFF);
+  float* lse_s = (float*)(smem + LY::LS_OFF);
+  float* dd_s = lse_s + NL;
+  float* stage = (float*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int blk = blockIdx.x, bh = blockIdx.y, nh = a.nh;
+  const int key0 = (MODE == MODE_A3) ? blk * NL : 0;
+  const int q_begin = (MODE == MODE_A1) ? blk * a.n_queries_per_wg : 0;
+  const int q_count = a.n_queries_per_wg;  // <= 256, a multiple of 32 (host-checked)
+
+  const bf16* Q = (const bf16*)a.q + hoff(bh, nh, a.q_bag, a.q_head) + (size_t)q_begin * a.q_row;
+  const bf16* dO = (const bf16*)a.dO + hoff(bh, nh, a.o_bag, a.o_head) + (size_t)q_begin * a.o_row;
+  const bf16* K = (const bf16*)a.k + hoff(bh, nh, a.k_bag, a.k_head) + (size_t)key0 * DH;
+  const bf16* V = (const bf16*)a.v + hoff(bh, nh, a.v_bag, a.v_head) + (size_t)key0 * DH;
+  const float* lse = a.lse + bh * a.lse_bh + q_begin;
+  const float* dd = a.dd + bh * a.dd_bh + q_begin;
+
+  // ---- one burst of loads: K rows (for K^T), Q / dO rows, K / V fragments, lse / D ----
+  const int mykey = wave * 32;
+  bf16x8 kr[4], qr[4], orow[4], kf[4], vf[4];
+  float lsev = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = tid + 512 * j;  // 16-B piece: row c >> 3, d0 = (c & 7) * 8
+    kr[j] = load8(K + (size_t)(c >> 3) * DH + (c & 7) * 8);
+    const int qq = min(c >> 3, q_count - 1);
+    qr[j] = load8(Q + (size_t)qq * a.q_row + (c & 7) * 8);
+    orow[j] = load8(dO + (size_t)qq * a.o_row + (c & 7) * 8);
+  }
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    kf[st] = load8(K + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
+    vf[st] = load8(V + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
+  }
+  {
+    const int qq = min(tid & (NL - 1), q_count - 1);
+    lsev = tid < NL ? lse[qq] : dd[qq];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = tid + 512 * j, row = c >> 3, d0 = (c & 7) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) kt_s[(d0 + e) * KT_ROW + row] = kr[j][e];
+    *(bf16x8*)(qs + row * QROW + d0) = qr[j];
+    *(bf16x8*)(os + row * QROW + d0) = orow[j];
+  }
+  (tid < NL ? lse_s : dd_s)[tid & (NL - 1)] = lsev;
+  __syncthreads();
+
+  f32x16 dvt[2], dkt[2];  // [d tile], cols = this wave's 32 keys
+#pragma unroll
+  for (int i = 0; i < 2; ++i) { dvt[i] = (f32x16){}; dkt[i] = (f32x16){}; }
+
+  const int dt_q = wave & 1, kq = wave >> 1;  // dQ role: d tile, key quarter
+#pragma unroll 1
+  for (int c0 = 0; c0 < q_count; c0 += 32) {
+    // S = Q K^T, dP = dO V^T: rows = queries (registers), cols = this wave's keys (lanes)
+    f32x16 s = (f32x16){}, dp = (f32x16){};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const bf16x8 qa_f = *(const bf16x8*)(qs + (c0 + r) * QROW + st * 16 + 8 * h);
+      const bf16x8 oa_f = *(const bf16x8*)(os + (c0 + r) * QROW + st * 16 + 8 * h);
+      mma16(s, qa_f, kf[st]);
+      mma16(dp, oa_f, vf[st]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int qq = c0 + acc_row(i, h);
+      const float p = __expf(s[i] - lse_s[qq]);
+      s[i] = p;
+      dp[i] = p * (dp[i] - dd_s[qq]);
+    }
+    // dV^T += dO^T P ; dK^T += Q^T dS
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      const bf16x8 bp = acc_as_operand<bf16>(s, sp);
+      const bf16x8 bs = acc_as_operand<bf16>(dp, sp);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const bf16x8 ao = frag_tr_acc(os + c0 * QROW, dt * 32, 16 * sp, lane);
+        const bf16x8 aq = frag_tr_acc(qs + c0 * QROW, dt * 32, 16 * sp, lane);
+        mma16(dvt[dt], ao, bp);
+        mma16(dkt[dt], aq, bs);
+      }
+    }
+    __syncthreads();  // previous chunk's dQ reads of ds_s / xch are done
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + r] = from_f<bf16>(dp[i]);
+    __syncthreads();
+    // dQ chunk [32 q x 64 d] = dS [32 x 256] . K [256 x 64]: this wave: d tile dt_q, keys 64*kq..+63
+    {
+      f32x16 acc = (f32x16){};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int kk = kq * 64 + st * 16 + 8 * h;
+        mma16(acc, load8(ds_s + r * DS_ROW + kk), load8(kt_s + (dt_q * 32 + r) * KT_ROW + kk));
+      }
+      if (kq > 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xch[((kq - 1) * 2 + dt_q) * 1024 + i * 64 + lane] = acc[i];
+      }
+      __syncthreads();
+      if (kq == 0) {
+        float* dst;
+        if (MODE == MODE_A1) dst = a.dq + bh * a.dq_bh;
+        else dst = a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qq = q_begin + c0 + acc_row(i, h);
+          const float v = ((acc[i] + xch[(0 * 2 + dt_q) * 1024 + i * 64 + lane]) +
+                           xch[(1 * 2 + dt_q) * 1024 + i * 64 + lane]) + xch[(2 * 2 + dt_q) * 1024 + i * 64 + lane];
+          dst[(size_t)qq * DH + dt_q * 32 + r] = v;
+        }
+      }
+    }
+  }
+  // ---- key-side epilogue through LDS (transpose to [key][d]) ----
+  __syncthreads();
+#pragma unroll
+  for (int which = 0; which < 2; ++which) {
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const f32x16& accv = which == 0 ? dvt[dt] : dkt[dt];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        *(f32x4*)(stage + (mykey + r) * 68 + dt * 32 + 8 * g4 + 4 * h) =
+            (f32x4){accv[4 * g4], accv[4 * g4 + 1], accv[4 * g4 + 2], accv[4 * g4 + 3]};
+    }
+    __syncthreads();
+    float* dst;
+    bool add = false;
+    if (MODE == MODE_A3) {
+      dst = (which == 0 ? a.dv + bh * a.dv_bh : a.dk + bh * a.dk_bh) + (size_t)key0 * DH;
+      add = (which == 0);
+    } else {
+      dst = (which == 0 ? a.dv : a.dk) + (size_t)blk * a.slab_stride + bh * (which == 0 ? a.dv_bh : a.dk_bh);
+    }
+    for (int i = tid; i < NL * DH / 4; i += 512) {
+      const int key = i >> 4, d4 = (i & 15) * 4;
+      f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
+      float* p = dst + (size_t)key * DH + d4;
+      if (add) val += *(const f32x4*)p;
+      *(f32x4*)p = val;
+    }
+    __syncthreads();
+  }
+}
+
 template <typename T>
 constexpr size_t bwd_smem_bytes() {
   return BwdLay<T>::BYTES;
@@ -911,8 +1103,13 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
   a.slab_stride = (long long)nbh * NL * DH;
   a.nh = nh; a.n_queries_per_wg = queries_per_wg; a.n_key_rows = NL;
   hipStream_t st = (hipStream_t)stream;
-  TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A1>, bwd_smem_bytes<T>()),
-                            attn_bwd_kernel<T, MODE_A1><<<dim3(nqc, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
+  if (dtype == TM_BF16 && queries_per_wg <= NL && g_nys_variant != 3) {
+    tm_allow_smem(attn_bwd_bf16_kernel<MODE_A1>, BwdLay16::BYTES);
+    attn_bwd_bf16_kernel<MODE_A1><<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
+  } else {
+    TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A1>, bwd_smem_bytes<T>()),
+                              attn_bwd_kernel<T, MODE_A1><<<dim3(nqc, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
+  }
   TM_CHECK_LAUNCH();
   const long long cnt = (long long)nbh * NL * DH;
   int rc = tm_splitk_reduce(slab_k, dkl, nqc, cnt, 1.0f, accumulate, stream);
@@ -943,8 +1140,13 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
   a.dv = dv; a.dv_bh = (long long)n * DH;
   a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
   hipStream_t st = (hipStream_t)stream;
-  TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A3>, bwd_smem_bytes<T>()),
-                            attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
+  if (dtype == TM_BF16 && g_nys_variant != 3) {
+    tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3>, BwdLay16::BYTES);
+    attn_bwd_bf16_kernel<MODE_A3><<<dim3(nkb, nbh), 512, BwdLay16::BYTES, st>>>(a);
+  } else {
+    TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A3>, bwd_smem_bytes<T>()),
+                              attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
+  }
   TM_CHECK_LAUNCH();
   return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, accumulate, stream);
 }
