@@ -165,6 +165,18 @@ int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, int pad, int
 int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
                     void* dpre, float* dcls, void* stream);
 
+/* fp32 -> dtype copies of up to 8 tensors (per-step bf16 GEMM weight operands) in one launch;
+ * offset[] = prefix sums of the element counts, offset[0] = 0 */
+#define TM_CAST_MAX 8
+typedef struct tm_cast_table {
+  int count;
+  int reserved;
+  const float* src[TM_CAST_MAX];
+  void* dst[TM_CAST_MAX];
+  long long offset[TM_CAST_MAX + 1];
+} tm_cast_table;
+int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* stream);
+
 /* ---- optimizer step (optim.hip) ----------------------------------------
  * torch.optim.RAdam (L2 decay, code/MyOptimizer/optim_factory.py:77-79) + the
  * Lookahead sync (code/MyOptimizer/lookahead.py, wrapped at optim_factory.py:118-121)

@@ -38,9 +38,9 @@ def test_struct_layouts_match_c(tmp_path):
     """Every field offset of the ctypes mirrors equals the C compiler's offsetof()."""
     import shutil
     import subprocess
-    from transmil_deepgraft_amd._lib import GemmArgs, BmmJob, OptimTensor, OptimTable
+    from transmil_deepgraft_amd._lib import GemmArgs, BmmJob, OptimTensor, OptimTable, CastTable
     structs = (("tm_gemm_args", GemmArgs), ("tm_bmm_job", BmmJob), ("tm_optim_tensor", OptimTensor),
-               ("tm_optim_table", OptimTable))
+               ("tm_optim_table", OptimTable), ("tm_cast_table", CastTable))
     cc = shutil.which("gcc") or shutil.which("cc")
     if cc is None:
         pytest.skip("no C compiler")

@@ -52,6 +52,14 @@ class OptimTable(C.Structure):
                 ("t", OptimTensor * OPTIM_MAX_TENSORS)]
 
 
+CAST_MAX = 8
+
+
+class CastTable(C.Structure):
+    _fields_ = [("count", I), ("reserved", I), ("src", P * CAST_MAX), ("dst", P * CAST_MAX),
+                ("offset", L * (CAST_MAX + 1))]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "tm_last_error": (C.c_char_p, []),
@@ -95,6 +103,7 @@ _SIGS = {
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),
+    "tm_cast_f32_many": (I, [I, C.POINTER(CastTable), P]),
     "tm_radam_lookahead_step": (I, [C.POINTER(OptimTable), P, P, P, P, Fl, Fl, Fl, I, Fl, P]),
 }
 

@@ -551,24 +551,34 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
   return 1;
 }
 
-__global__ void splitk_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out, int splits,
-                                     size_t count, float alpha, int accumulate) {
-  const size_t i4 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i4 * 4 >= count) return;
-  if (i4 * 4 + 4 <= count) {
-    f32x4 s = *(const f32x4*)(slab + i4 * 4);
-#pragma unroll 8
-    for (int z = 1; z < splits; ++z) s += *(const f32x4*)(slab + (size_t)z * count + i4 * 4);
+// out = alpha * sum_z slab[z] (+ out): the splits are summed in index order (bitwise
+// reproducible).  U loads per thread are issued together (indices clamped, masked by
+// select, no branches), so a 33-way reduce is one memory round trip, not five.
+template <int U, int VEC>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                            int splits, size_t count, float alpha, int accumulate) {
+  typedef float vf __attribute__((ext_vector_type(VEC)));
+  const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (iv * VEC >= count) return;
+  if (iv * VEC + VEC <= count) {
+    vf s = (vf)0.f;
+    for (int z0 = 0; z0 < splits; z0 += U) {
+      vf v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = *(const vf*)(slab + (size_t)min(z0 + u, splits - 1) * count + iv * VEC);
+#pragma unroll
+      for (int u = 0; u < U; ++u) s += (z0 + u < splits) ? v[u] : (vf)0.f;
+    }
     s *= alpha;
-    if (accumulate) s += *(f32x4*)(out + i4 * 4);
-    *(f32x4*)(out + i4 * 4) = s;
+    if (accumulate) s += *(const vf*)(out + iv * VEC);
+    *(vf*)(out + iv * VEC) = s;
   } else {
-    for (size_t i = i4 * 4; i < count; ++i) {
-      float s = slab[i];
-      for (int z = 1; z < splits; ++z) s += slab[(size_t)z * count + i];
-      s *= alpha;
-      if (accumulate) s += out[i];
-      out[i] = s;
+    for (size_t i = iv * VEC; i < count; ++i) {
+      float t = slab[i];
+      for (int z = 1; z < splits; ++z) t += slab[(size_t)z * count + i];
+      t *= alpha;
+      if (accumulate) t += out[i];
+      out[i] = t;
     }
   }
 }
@@ -582,8 +592,17 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, int rows, int col
   const int r0 = blockIdx.y * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
   __shared__ float red[4][64];
   float s = 0.f;
-  if (c < cols)
-    for (int r = r0 + sub; r < r1; r += 4) s += to_f(X[(size_t)r * ld + c]);
+  if (c < cols) {
+    // 8 independent partial sums per thread: eight row loads in flight at once
+    float p8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int r = r0 + sub;
+    for (; r + 28 < r1; r += 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) p8[j] += to_f(X[(size_t)(r + 4 * j) * ld + c]);
+    }
+    for (; r < r1; r += 4) p8[0] += to_f(X[(size_t)r * ld + c]);
+    s = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
+  }
   red[sub][threadIdx.x & 63] = s;
   __syncthreads();
   if (sub == 0 && c < cols)
@@ -620,9 +639,21 @@ extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long 
                                 int accumulate, void* stream) {
   TM_REQUIRE(slab && out && splits >= 1 && count >= 0, "splitk_reduce: bad args");
   if (count == 0) return 0;
-  const size_t n4 = ((size_t)count + 3) / 4;
-  splitk_reduce_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, (hipStream_t)stream>>>(slab, out, splits, (size_t)count,
-                                                                                    alpha, accumulate);
+  hipStream_t st = (hipStream_t)stream;
+  // float4 per thread only when that still gives >= 1024 workgroups' worth of threads
+  const bool vec4 = count % 4 == 0 && count / 4 >= 256LL * 1024;
+  const size_t nthreads = vec4 ? (size_t)count / 4 : (size_t)count;
+  const unsigned blocks = (unsigned)((nthreads + 255) / 256);
+  if (splits <= 8) {
+    if (vec4) splitk_reduce_kernel<8, 4><<<blocks, 256, 0, st>>>(slab, out, splits, (size_t)count, alpha, accumulate);
+    else splitk_reduce_kernel<8, 1><<<blocks, 256, 0, st>>>(slab, out, splits, (size_t)count, alpha, accumulate);
+  } else if (splits <= 16) {
+    if (vec4) splitk_reduce_kernel<16, 4><<<blocks, 256, 0, st>>>(slab, out, splits, (size_t)count, alpha, accumulate);
+    else splitk_reduce_kernel<16, 1><<<blocks, 256, 0, st>>>(slab, out, splits, (size_t)count, alpha, accumulate);
+  } else {
+    if (vec4) splitk_reduce_kernel<36, 4><<<blocks, 256, 0, st>>>(slab, out, splits, (size_t)count, alpha, accumulate);
+    else splitk_reduce_kernel<36, 1><<<blocks, 256, 0, st>>>(slab, out, splits, (size_t)count, alpha, accumulate);
+  }
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -7,6 +7,19 @@
 
 namespace {
 
+// fp32 -> T copies of up to 8 tensors in one launch (the per-step GEMM weight operands)
+template <typename T>
+__global__ void cast_many_kernel(tm_cast_table tab) {
+  const long long i4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= tab.offset[tab.count]) return;
+  int t = 0;
+  while (i4 >= tab.offset[t + 1]) ++t;
+  const long long j = i4 - tab.offset[t], n = tab.offset[t + 1] - tab.offset[t];
+  const float* src = tab.src[t];
+  T* dst = (T*)tab.dst[t];
+  for (int e = 0; e < 4 && j + e < n; ++e) dst[j + e] = from_f<T>(src[j + e]);
+}
+
 // H[b*S + 0][:] = cls[:]; grid (B), block 256
 __global__ void put_cls_kernel(const float* __restrict__ cls, int S, int D, float* __restrict__ H) {
   for (int c = threadIdx.x; c < D; c += blockDim.x) H[(size_t)blockIdx.x * S * D + c] = cls[c];
@@ -106,6 +119,22 @@ extern "C" int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int
                                                                                (T*)dpre)));
   TM_CHECK_LAUNCH();
   cls_grad_kernel<<<1, 256, 0, st>>>(dH, B, S, D, dcls);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* stream) {
+  TM_REQUIRE(table && table->count >= 1 && table->count <= TM_CAST_MAX, "cast_many: 1..8 tensors");
+  long long off = 0;
+  for (int i = 0; i < table->count; ++i) {
+    TM_REQUIRE(table->src[i] && table->dst[i], "cast_many: null tensor");
+    TM_REQUIRE(table->offset[i] == off && table->offset[i + 1] >= off, "cast_many: offsets must be a prefix sum");
+    off = table->offset[i + 1];
+  }
+  if (off == 0) return 0;
+  const long long threads = (off + 3) / 4;
+  TM_DTYPE_DISPATCH(dtype, (cast_many_kernel<T><<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+                               *table)));
   TM_CHECK_LAUNCH();
   return 0;
 }

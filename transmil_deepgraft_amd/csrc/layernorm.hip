@@ -27,8 +27,14 @@ TM_DEV void load_row(float (&v)[VPL], const float* p, int lane) {
 
 template <typename T, int VPL>
 TM_DEV void load_row_t(float (&v)[VPL], const T* p, int lane) {
+  if constexpr (VPL == 8) {
+    const vec8<T> t = load8(p + lane * VPL);
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) v[i] = to_f(p[lane * VPL + i]);
+    for (int i = 0; i < 8; ++i) v[i] = to_f(t[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) v[i] = to_f(p[lane * VPL + i]);
+  }
 }
 
 // rows: B*S input rows (fp32 residual stream); out row = (r / S) * n_pad + pad + r % S
@@ -88,12 +94,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 #pragma unroll
   for (int i = 0; i < VPL; ++i) { dg[i] = 0.f; db[i] = 0.f; gm[i] = gamma[lane * VPL + i]; }
   const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-  for (int r = r0 + wave; r < r1; r += 4) {
-    const int b = r / S, t = r % S;
-    float g[VPL], xv[VPL];
+  // software pipeline: the next row's dy, x, mean/rstd and dx_accum are requested before
+  // this row is processed (one HBM round trip in flight instead of one per row)
+  auto fetch = [&](int r, float (&g)[VPL], float (&xv)[VPL], float (&acc)[VPL], float& mu, float& rs) {
+    const int rr = min(r, rows - 1);
+    const int b = rr / S, t = rr % S;
     load_row_t<T, VPL>(g, dy + ((size_t)b * n_pad + pad + t) * D, lane);
-    load_row<VPL>(xv, x + (size_t)r * D, lane);
-    const float mu = mean[r], rs = rstd[r];
+    load_row<VPL>(xv, x + (size_t)rr * D, lane);
+    load_row<VPL>(acc, dx_accum + (size_t)rr * D, lane);
+    mu = mean[rr];
+    rs = rstd[rr];
+  };
+  float g[VPL], xv[VPL], dacc[VPL], mu, rs;
+  int r = r0 + wave;
+  if (r < r1) fetch(r, g, xv, dacc, mu, rs);
+  for (; r < r1; r += 4) {
+    float g2[VPL], xv2[VPL], dacc2[VPL], mu2 = 0.f, rs2 = 0.f;
+    const bool more = r + 4 < r1;
+    if (more) fetch(r + 4, g2, xv2, dacc2, mu2, rs2);
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
@@ -109,8 +127,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     s1 = wave_sum(s1) * (1.0f / D);
     s2 = wave_sum(s2) * (1.0f / D);
     float* dst = dx_accum + (size_t)r * D;
+    if constexpr (VPL % 4 == 0) {
 #pragma unroll
-    for (int i = 0; i < VPL; ++i) dst[lane * VPL + i] += rs * (g[i] - s1 - xv[i] * s2);
+      for (int i = 0; i < VPL; i += 4)
+        *(f32x4*)(dst + lane * VPL + i) =
+            (f32x4){dacc[i] + rs * (g[i] - s1 - xv[i] * s2), dacc[i + 1] + rs * (g[i + 1] - s1 - xv[i + 1] * s2),
+                    dacc[i + 2] + rs * (g[i + 2] - s1 - xv[i + 2] * s2), dacc[i + 3] + rs * (g[i + 3] - s1 - xv[i + 3] * s2)};
+    } else {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) dst[lane * VPL + i] = dacc[i] + rs * (g[i] - s1 - xv[i] * s2);
+    }
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) { g[i] = g2[i]; xv[i] = xv2[i]; dacc[i] = dacc2[i]; }
+      mu = mu2;
+      rs = rs2;
+    }
   }
   __shared__ float red[2][4][D];
 #pragma unroll

@@ -374,8 +374,10 @@ __global__ void a3_combine_kernel(const float* __restrict__ part_o, const float*
                                   float* __restrict__ lse3) {
   const int bh = blockIdx.x, qi = blockIdx.y * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
   float M = -INFINITY;
+#pragma unroll 8
   for (int kb = 0; kb < nkb; ++kb) M = fmaxf(M, part_m[((size_t)kb * nbh + bh) * NL + qi]);
   float L = 0.f, acc = 0.f;
+#pragma unroll 8
   for (int kb = 0; kb < nkb; ++kb) {
     const size_t pidx = ((size_t)kb * nbh + bh) * NL + qi;
     const float sc = __expf(part_m[pidx] - M);
@@ -402,8 +404,12 @@ __global__ void rowdot_cast_kernel(const float* __restrict__ dw, const float* __
 // T copy of an fp32 [rows][64] matrix
 template <typename T>
 __global__ void cast_rows_kernel(const float* __restrict__ x, T* __restrict__ y, long long count) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i < count) y[i] = from_f<T>(x[i]);
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i + 8 <= count) {
+    store8<T>(y + i, cvt8<T>(x + i));
+  } else {
+    for (long long j = i; j < count; ++j) y[j] = from_f<T>(x[j]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1056,7 +1062,8 @@ extern "C" int tm_nys_rowdot_cast(int dtype, const float* dw, const float* w, in
 
 extern "C" int tm_cast_f32(int dtype, const float* x, void* y, long long count, void* stream) {
   if (count == 0) return 0;
-  TM_DTYPE_DISPATCH(dtype, (cast_rows_kernel<T><<<(unsigned)((count + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+  TM_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0, "cast_f32: 16-B aligned buffers");
+  TM_DTYPE_DISPATCH(dtype, (cast_rows_kernel<T><<<(unsigned)((count + 2047) / 2048), 256, 0, (hipStream_t)stream>>>(
                                x, (T*)y, count)));
   TM_CHECK_LAUNCH();
   return 0;

@@ -331,7 +331,7 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
     dxn = pool(B * n * D, tdtype).view(B, n, D)
     gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     # LayerNorm backward, accumulated into dH (residual branch already there)
-    rpb = 64
+    rpb = 32
     work = pool(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4)
     _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
               _p(saved["rstd"]), B * S, D, S, n, pad, rpb, _p(dH), _p(work), _p(grads["norm_w"]),
@@ -357,19 +357,40 @@ class TransMILEngine:
         _lib.call("tm_cast_f32", self.dt_code, _p(w.contiguous()), _p(out), w.numel(), _stream())
         return out.view(w.shape)
 
+    def _cast_many(self, ws, pool):
+        """T copies of several fp32 weights in one launch (fp32 mode: the weights themselves)."""
+        ws = [w.contiguous() for w in ws]
+        if self.dt_code == F32:
+            return ws
+        tab = _lib.CastTable()
+        tab.count = len(ws)
+        outs = []
+        off = 0
+        for i, w in enumerate(ws):
+            o = pool(w.numel(), self.tdtype).view(w.shape)
+            tab.src[i], tab.dst[i], tab.offset[i] = w.data_ptr(), o.data_ptr(), off
+            off += w.numel()
+            outs.append(o)
+        tab.offset[len(ws)] = off
+        _lib.call("tm_cast_f32_many", self.dt_code, C.byref(tab), _stream())
+        return outs
+
     def prepare(self, params, pool):
         """fp32 master parameters -> the per-call operand set (T copies of GEMM weights)."""
         D = params["norm.weight"].shape[0]
         p = {"D": D}
-        p["w1"] = self._cast(params["_fc1.0.weight"], pool)
+        w1, wqkv1, wo1, wqkv2, wo2 = self._cast_many(
+            [params["_fc1.0.weight"], params["layer1.attn.to_qkv.weight"], params["layer1.attn.to_out.0.weight"],
+             params["layer2.attn.to_qkv.weight"], params["layer2.attn.to_out.0.weight"]], pool)
+        p["w1"] = w1
         p["b1"] = params["_fc1.0.bias"]
         p["cls"] = params["cls_token"]
-        for li in (1, 2):
+        for li, (wqkv, wo) in ((1, (wqkv1, wo1)), (2, (wqkv2, wo2))):
             pre = f"layer{li}."
             p[li] = {
                 "norm_w": params[pre + "norm.weight"], "norm_b": params[pre + "norm.bias"],
-                "wqkv": self._cast(params[pre + "attn.to_qkv.weight"], pool),
-                "wo": self._cast(params[pre + "attn.to_out.0.weight"], pool),
+                "wqkv": wqkv,
+                "wo": wo,
                 "bo": params[pre + "attn.to_out.0.bias"],
                 "wconv": params[pre + "attn.res_conv.weight"].contiguous(),
             }
