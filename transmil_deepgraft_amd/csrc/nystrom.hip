@@ -196,29 +196,59 @@ TM_DEV void attn_fwd_wave(const T* ks, const T* vt, const vec8<T> (&qf)[4], f32x
   }
 }
 
+// A [256][64] T tile (row stride 64) held in registers between its global loads and its
+// LDS writes: a compile-time count of 16-B pieces per thread, so every load of the tile is
+// issued before the first wait (a runtime-bounded `for (i = tid; ...)` loop let the compiler
+// pipeline only the first few and serialise the rest, one HBM/L2 round trip each).
+template <typename T>
+struct TileRegs {
+  static constexpr int E = 16 / sizeof(T), PER_ROW = DH / E, PER = NL * PER_ROW / 256;
+  f32x4 r[PER];
+  TM_DEV void load(const T* src, int tid) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 256 * j;
+      r[j] = *(const f32x4*)(src + (size_t)(i / PER_ROW) * DH + (i % PER_ROW) * E);
+    }
+  }
+  // keys: ks[key][KROW]
+  TM_DEV void store_keys(T* ks, int tid) const {
+    constexpr int KROW = Lay<T>::KROW;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 256 * j;
+      *(f32x4*)(ks + (i / PER_ROW) * KROW + (i % PER_ROW) * E) = r[j];
+    }
+  }
+  // values in the layout of Lay<T> (bf16 natural [key][VROW], fp32 transposed [d][VROW])
+  TM_DEV void store_values(T* vs, int tid) const {
+    constexpr int VROW = Lay<T>::VROW;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 256 * j, key = i / PER_ROW, d0 = (i % PER_ROW) * E;
+      if constexpr (sizeof(T) == 2) {
+        *(f32x4*)(vs + key * VROW + d0) = r[j];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) vs[(d0 + e) * VROW + key] = r[j][e];
+      }
+    }
+  }
+};
+
 // stage T rows [256][64] (row stride 64) into ks[key][KROW]
 template <typename T>
 TM_DEV void stage_keys_t(T* ks, const T* src, int tid) {
-  constexpr int KROW = Lay<T>::KROW, E = 16 / sizeof(T);
-  for (int i = tid; i < NL * DH / E; i += 256) {
-    const int row = i / (DH / E), c = (i % (DH / E)) * E;
-    *(f32x4*)(ks + row * KROW + c) = *(const f32x4*)(src + (size_t)row * DH + c);
-  }
+  TileRegs<T> t;
+  t.load(src, tid);
+  t.store_keys(ks, tid);
 }
 // stage values [256 keys][64] (T rows, stride 64) into the value layout of Lay<T>
 template <typename T>
 TM_DEV void stage_values(T* vs, const T* src, int tid) {
-  constexpr int VROW = Lay<T>::VROW, E = 16 / sizeof(T);
-  for (int i = tid; i < NL * DH / E; i += 256) {
-    const int key = i / (DH / E), d0 = (i % (DH / E)) * E;
-    if constexpr (sizeof(T) == 2) {
-      *(f32x4*)(vs + key * VROW + d0) = *(const f32x4*)(src + (size_t)key * DH + d0);
-    } else {
-      const f32x4 v4 = *(const f32x4*)(src + (size_t)key * DH + d0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) vs[(d0 + e) * VROW + key] = v4[e];
-    }
-  }
+  TileRegs<T> t;
+  t.load(src, tid);
+  t.store_values(vs, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -230,7 +260,7 @@ constexpr int A1_WIN_ITEMS = (128 + 2 * HALF) * 8 / 256;
 constexpr size_t A1_EPI_BYTES = (128 * 68 + (128 + 2 * HALF) * A1_VS) * sizeof(float);
 
 template <typename T, int VAR = 0>   // VAR (ablation): 1 = no conv taps, 2 = no MFMA phase
-__global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, const T* __restrict__ v,
+__global__ __launch_bounds__(256, 2) void a1_fwd_kernel(const T* __restrict__ q, const T* __restrict__ v,
                                                      const T* __restrict__ kl_t, const T* __restrict__ y_t,
                                                      const float* __restrict__ wconv, int n, int nh,
                                                      T* __restrict__ merged, float* __restrict__ lse1) {
@@ -243,13 +273,36 @@ __global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, co
   const int r = lane & 31, h = lane >> 5;
   const int head = bh % nh, bag = bh / nh;
   const int t0 = blockIdx.x * 128;
-  stage_keys_t<T>(ks, kl_t + (size_t)bh * NL * DH, tid);
-  stage_values<T>(vt, y_t + (size_t)bh * NL * DH, tid);
   const T* qb = q + (size_t)bh * n * DH;
+  const T* vb = v + (size_t)bh * n * DH;
   vec8<T> qf[4];
   const int qrow = t0 + wave * 32 + r;
+  // conv window: v rows [t0 - 16, t0 + 144) of this head (5 x 16 B per thread)
+  vec8<T> vwin[A1_WIN_ITEMS];
+  auto load_window = [&]() {
 #pragma unroll
-  for (int st = 0; st < 4; ++st) qf[st] = load8(qb + (size_t)qrow * DH + st * 16 + 8 * h);
+    for (int i = 0; i < A1_WIN_ITEMS; ++i) {
+      const int it = tid + 256 * i, row = it >> 3, src = t0 - HALF + row;
+      if (src >= 0 && src < n) vwin[i] = load8(vb + (size_t)src * DH + (it & 7) * 8);
+      else vwin[i] = vec8<T>{};
+    }
+  };
+  if constexpr (sizeof(T) == 2) {
+    // one burst: landmark keys, Y and this wave's query fragments (the conv window is
+    // requested after the MFMA phase: held across it, it would cost the second wave per SIMD)
+    TileRegs<T> kr, yr;
+    kr.load(kl_t + (size_t)bh * NL * DH, tid);
+    yr.load(y_t + (size_t)bh * NL * DH, tid);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) qf[st] = load8(qb + (size_t)qrow * DH + st * 16 + 8 * h);
+    kr.store_keys(ks, tid);
+    yr.store_values(vt, tid);
+  } else {
+    stage_keys_t<T>(ks, kl_t + (size_t)bh * NL * DH, tid);
+    stage_values<T>(vt, y_t + (size_t)bh * NL * DH, tid);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) qf[st] = load8(qb + (size_t)qrow * DH + st * 16 + 8 * h);
+  }
   __syncthreads();
   f32x16 o[2];
   float mx, sum;
@@ -261,16 +314,8 @@ __global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, co
   }
   if (h == 0) lse1[(size_t)bh * n + qrow] = mx + __logf(sum);
   const float inv = 1.0f / sum;
-  // conv window: v rows [t0 - 16, t0 + 144) of this head, requested now (5 x 16 B per
-  // thread) so the loads overlap the normalisation / LDS round trip below.
-  const T* vb = v + (size_t)bh * n * DH;
-  vec8<T> vwin[A1_WIN_ITEMS];
-#pragma unroll
-  for (int i = 0; i < A1_WIN_ITEMS; ++i) {
-    const int it = tid + 256 * i, row = it >> 3, src = t0 - HALF + row;
-    if (src >= 0 && src < n) vwin[i] = load8(vb + (size_t)src * DH + (it & 7) * 8);
-    else vwin[i] = vec8<T>{};
-  }
+  // the conv window is requested now, overlapping the normalisation / LDS round trip below
+  load_window();
   __syncthreads();  // everyone done reading ks/vt
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
@@ -333,7 +378,7 @@ __global__ __launch_bounds__(256) void a1_fwd_kernel(const T* __restrict__ q, co
 // grid (n/256, nbh, 2), block 256.
 //   part_o[kb][bh][q][d] = sum_{keys in kb} exp(s - m_kb) v ; part_ml[kb][bh][q] = (m, l)
 template <typename T>
-__global__ __launch_bounds__(256) void a3_fwd_kernel(const float* __restrict__ ql, const T* __restrict__ k,
+__global__ __launch_bounds__(256, 2) void a3_fwd_kernel(const float* __restrict__ ql, const T* __restrict__ k,
                                                      const T* __restrict__ v, int n, float* __restrict__ part_o,
                                                      float* __restrict__ part_m, float* __restrict__ part_l) {
   constexpr int KROW = Lay<T>::KROW;
@@ -343,14 +388,24 @@ __global__ __launch_bounds__(256) void a3_fwd_kernel(const float* __restrict__ q
   const int kb = blockIdx.x, bh = blockIdx.y, nbh = gridDim.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const size_t kv_off = ((size_t)bh * n + (size_t)kb * NL) * DH;
-  stage_keys_t<T>(ks, k + kv_off, tid);
-  stage_values<T>(vt, v + kv_off, tid);
-  __syncthreads();
-  {
-    const int qi = blockIdx.z * 128 + wave * 32 + r;  // query half per workgroup
-    vec8<T> qf[4];
+  const int qi = blockIdx.z * 128 + wave * 32 + r;  // query half per workgroup
+  vec8<T> qf[4];
+  if constexpr (sizeof(T) == 2) {
+    TileRegs<T> kr, vr;  // one burst: keys, values, query fragments
+    kr.load(k + kv_off, tid);
+    vr.load(v + kv_off, tid);
 #pragma unroll
     for (int st = 0; st < 4; ++st) qf[st] = cvt8<T>(ql + ((size_t)bh * NL + qi) * DH + st * 16 + 8 * h);
+    kr.store_keys(ks, tid);
+    vr.store_values(vt, tid);
+  } else {
+    stage_keys_t<T>(ks, k + kv_off, tid);
+    stage_values<T>(vt, v + kv_off, tid);
+#pragma unroll
+    for (int st = 0; st < 4; ++st) qf[st] = cvt8<T>(ql + ((size_t)bh * NL + qi) * DH + st * 16 + 8 * h);
+  }
+  __syncthreads();
+  {
     f32x16 o[2];
     float mx, sum;
     attn_fwd_wave<T>(ks, vt, qf, o, mx, sum, lane);
@@ -439,21 +494,37 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_kernel(const T* __restrict__ 
   const T* ob = merged + (size_t)bag * n * ld + head * DH;
   const T* vb = v + (size_t)bh * n * DH;
   constexpr int E = 16 / sizeof(T);
-  for (int i = tid; i < HR * DH / E; i += 256) {
-    const int rr = i / (DH / E), d0 = (i % (DH / E)) * E, t = t0 - HALF + rr;
-    const bool ok = t >= 0 && t < n;
-    Chunk16<T> a, b;
-    if (ok) {
-      a.raw = *(const f32x4*)(dob + (size_t)t * ld + d0);
-      b.raw = *(const f32x4*)(vb + (size_t)t * DH + d0);
-    }
+  constexpr int PER = HR * DH / E / 256;  // 16-B pieces per thread and tensor
+  // one burst: the dO / v windows, this thread's quarter row of O and the conv taps
+  Chunk16<T> ca[PER], cb[PER], co[16 / E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      dos[rr][d0 + e] = ok ? to_f(a.e[e]) : 0.f;
-      vs[rr][d0 + e] = ok ? to_f(b.e[e]) : 0.f;
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + 256 * j, rr = i / (DH / E), d0 = (i % (DH / E)) * E, t = t0 - HALF + rr;
+    if (t >= 0 && t < n) {
+      ca[j].raw = *(const f32x4*)(dob + (size_t)t * ld + d0);
+      cb[j].raw = *(const f32x4*)(vb + (size_t)t * DH + d0);
+    } else {
+      ca[j].raw = (f32x4){};
+      cb[j].raw = (f32x4){};
     }
   }
-  if (tid < TAPS) ws[tid] = wconv[head * TAPS + tid];
+  {
+    const int t = t0 + (tid >> 2), dq0 = (tid & 3) * 16;
+#pragma unroll
+    for (int part = 0; part < 16 / E; ++part)
+      co[part].raw = t < n ? *(const f32x4*)(ob + (size_t)t * ld + dq0 + part * E) : (f32x4){};
+  }
+  const float wtap = tid < TAPS ? wconv[head * TAPS + tid] : 0.f;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + 256 * j, rr = i / (DH / E), d0 = (i % (DH / E)) * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      dos[rr][d0 + e] = to_f(ca[j].e[e]);
+      vs[rr][d0 + e] = to_f(cb[j].e[e]);
+    }
+  }
+  if (tid < TAPS) ws[tid] = wtap;
   __syncthreads();
   // part A: thread (row rl, tap phase qq): taps qq, qq+4, ...
   {
@@ -482,14 +553,11 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_kernel(const T* __restrict__ 
           }
         }
       }
-      if (dc / 16 == qq && t < n) {  // this thread's quarter of dO . O
+      if (dc / 16 == qq) {  // this thread's quarter of dO . O (co is zero past n)
 #pragma unroll
-        for (int part = 0; part < 16 / E; ++part) {
-          Chunk16<T> o;
-          o.raw = *(const f32x4*)(ob + (size_t)t * ld + dc + part * E);
+        for (int part = 0; part < 16 / E; ++part)
 #pragma unroll
-          for (int e = 0; e < E; ++e) dd = fmaf(g[part * E + e], to_f(o.e[e]), dd);
-        }
+          for (int e = 0; e < E; ++e) dd = fmaf(g[part * E + e], to_f(co[part].e[e]), dd);
       }
     }
     float wc = 0.f;
@@ -963,21 +1031,35 @@ __global__ void assemble_dqkv_kernel(const float* __restrict__ dq, const float* 
                                      const float* __restrict__ dk, const float* __restrict__ dkl,
                                      const float* __restrict__ dv, int n, int l, int nh, float scale,
                                      T* __restrict__ dqkv) {
-  // grid (n, nbh/?): one block per (bag, t) row, threads over 3*nh*64 columns
-  const int t = blockIdx.x, bag = blockIdx.y;
-  const int inner = nh * DH;
+  // item = (t, 8 consecutive columns of the 3*nh*64-wide row) of bag blockIdx.y;
+  // grid (ceil(n * 3*nh*8 / 256), nbags), block 256.
+  const int inner = nh * DH, per_row = 3 * inner / 8;
+  const long long item = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (item >= (long long)n * per_row) return;
+  const int c = (int)(item % per_row) * 8;
+  const int t = (int)(item / per_row), bag = blockIdx.y;
+  const int which = c / inner, head = (c % inner) / DH, d = c % DH;
+  const size_t bh = (size_t)bag * nh + head;
+  const size_t row = (bh * n + t) * DH + d;
+  const size_t lrow = (bh * NL + t / l) * DH + d;
   const float inv_l = 1.0f / (float)l;
-  for (int c = threadIdx.x; c < 3 * inner; c += blockDim.x) {
-    const int which = c / inner, head = (c % inner) / DH, d = c % DH;
-    const size_t bh = (size_t)bag * nh + head;
-    const size_t row = (bh * n + t) * DH + d;
-    const size_t lrow = (bh * NL + t / l) * DH + d;
+  const float* src = which == 0 ? dq : which == 1 ? dk : dv;
+  const float* lsrc = which == 0 ? dql : dkl;
+  const f32x4 a0 = *(const f32x4*)(src + row), a1 = *(const f32x4*)(src + row + 4);
+  f32x4 b0 = (f32x4){}, b1 = (f32x4){};
+  if (which < 2) { b0 = *(const f32x4*)(lsrc + lrow); b1 = *(const f32x4*)(lsrc + lrow + 4); }
+  const float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+  const float b[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  vec8<T> out;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
     float val;
-    if (which == 0) val = scale * (dq[row] + dql[lrow] * inv_l);
-    else if (which == 1) val = dk[row] + dkl[lrow] * inv_l;
-    else val = dv[row];
-    dqkv[((size_t)bag * n + t) * (3 * inner) + c] = from_f<T>(val);
+    if (which == 0) val = scale * (a[e] + b[e] * inv_l);
+    else if (which == 1) val = a[e] + b[e] * inv_l;
+    else val = a[e];
+    out[e] = from_f<T>(val);
   }
+  store8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c, out);
 }
 
 }  // namespace
@@ -1162,7 +1244,9 @@ extern "C" int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql
                                     const float* dv, int nbags, int nh, int n, float scale, void* dqkv,
                                     void* stream) {
   TM_REQUIRE(n % NL == 0, "assemble_dqkv: n must be a multiple of 256");
-  TM_DTYPE_DISPATCH(dtype, (assemble_dqkv_kernel<T><<<dim3(n, nbags), 256, 0, (hipStream_t)stream>>>(
+  const long long items = (long long)n * 3 * nh * DH / 8;
+  TM_DTYPE_DISPATCH(dtype, (assemble_dqkv_kernel<T><<<dim3((unsigned)((items + 255) / 256), nbags), 256, 0,
+                                                       (hipStream_t)stream>>>(
                                dq, dql, dk, dkl, dv, n, n / NL, nh, scale, (T*)dqkv)));
   TM_CHECK_LAUNCH();
   return 0;
