@@ -76,6 +76,21 @@ def roofline_model(site, n_patches, dtype_bytes):
     raise ValueError(site)
 
 
+def measured_traffic(site, n_patches, dtype):
+    """HBM bytes per launch of `site` from the committed rocprofv3 PMC passes
+    (profiles/traffic.json, written by scripts/gpu_traffic.sh + scripts/traffic_summary.py):
+    FETCH_SIZE (doubled for the gfx950 half-count) + WRITE_SIZE.  None when that file does not
+    hold a measurement of this call site at this workload."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        rec = json.load(open(path))["sites"][site]
+    except (OSError, KeyError, ValueError):
+        return None
+    if rec.get("n") != n_patches or rec.get("dtype") != dtype:
+        return None
+    return rec.get("traffic_bytes")
+
+
 def cpu_baseline(n_patches, ncls, steps):
     """fp32 CPU oracle, logits path (no unused n'xn' attention product), timed on this host."""
     from oracle.transmil_ref import TransMIL as RefTransMIL, TransLayer
@@ -226,10 +241,10 @@ def main():
         peak_fl = BF16_PEAK_TFS if args.dtype == "bf16" else 157.3
         hbm_bound = rm["flops"] / rm["bytes"] < peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
         roof = (dict(bound="hbm", achieved=round(ach_bw, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                     frac=round(ach_bw / HBM_PEAK_GBS, 4), traffic=None)
+                     frac=round(ach_bw / HBM_PEAK_GBS, 4), traffic=measured_traffic(args.probe, args.n, args.dtype))
                 if hbm_bound else
                 dict(bound="mfma", achieved=round(ach_fl, 2), peak=peak_fl, unit="TFLOP/s",
-                     frac=round(ach_fl / peak_fl, 4), traffic=None))
+                     frac=round(ach_fl / peak_fl, 4), traffic=measured_traffic(args.probe, args.n, args.dtype)))
         roof.update(kernel=args.probe, kernel_ms=round(kernel_ms, 5), launches=len(kernel_ms_samples),
                     algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])
         out = {

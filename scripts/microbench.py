@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--only", default="")
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="a1_fwd in-kernel s_memtime stamps")
     ap.add_argument("--gemm-ab", action="store_true", help="also time the GEMMs on the register-staged loop")
     args = ap.parse_args()
     dev = "cuda"
@@ -208,10 +209,32 @@ def main():
     case("a1_fwd", lambda: _lib.call("tm_nys_a1_fwd", BF16, E._p(q), E._p(v), E._p(kl_t), E._p(y_t), E._p(wconv),
                                      nbh, 8, n, E._p(merged), E._p(lse1), st()),
          4 * nbh * n * 256 * 64, 3 * n * 512 * 2)
-    for var, nm in ((1, "no conv"), (2, "no MFMA")):
+    for var, nm in ((11, "no conv"), (12, "no attention"), (13, "prologue only"),
+                    (14, "legacy 128-query kernel")):
         _lib.lib().tm_debug_set_variant(1, var)
         case(f"a1_fwd [{nm}]", lambda: _lib.call("tm_nys_a1_fwd", BF16, E._p(q), E._p(v), E._p(kl_t), E._p(y_t),
                                                 E._p(wconv), nbh, 8, n, E._p(merged), E._p(lse1), st()))
+    if args.stamps:
+        _lib.lib().tm_debug_set_variant(1, 19)
+        _lib.call("tm_nys_a1_fwd", BF16, E._p(q), E._p(v), E._p(kl_t), E._p(y_t), E._p(wconv), nbh, 8, n,
+                  E._p(merged), E._p(lse1), st())
+        torch.cuda.synchronize()
+        import numpy as np
+        buf = (C.c_ulonglong * (256 * 64))()
+        _lib.call("tm_debug_a1_stamps", buf, 256 * 64)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(256, 8, 8).astype(np.int64)[:, :4]
+        t0 = a[:, :, 0].min()
+        print("a1_fwd stamps (cycles from first start): slot medians / maxima over waves")
+        names = ["start", "prologue", "attn1", "window", "conv1", "stores1", "end"]
+        for slot in range(7):
+            rel = a[:, :, slot] - a[:, :, 0]   # per wave, from its own start (XCD clocks differ)
+            ok = a[:, :, slot] > 0
+            vals = rel[ok]
+            if vals.size:
+                print(f"  {slot} {names[slot]:9s} median {int(np.median(vals)):7d} max {int(vals.max()):7d}")
+        d = a[:, :, 6] - a[:, :, 0]
+        print(f"  wave lifetime median {int(np.median(d))} max {int(d.max())}; "
+              f"last end - first start {int(a[:, :, 6].max() - t0)}")
     _lib.lib().tm_debug_set_variant(1, 0)
     dmerged = torch.randn(1, n, 512, device=dev).to(bf)
     dv = torch.empty(nbh, n, 64, device=dev)

@@ -311,3 +311,52 @@ def test_return_attn_matrix():
         _, attn = ours(x.float().to(DEV), return_attn=True)
     assert attn.shape == attn_ref.shape
     assert _rel(attn.cpu(), attn_ref) < 1e-3
+
+
+# ----------------------------------------------------------------------------- A1 forward (bf16 kernels)
+def _a1_ref(q, v, kl, y, wconv, nh):
+    """fp64 restatement: merged[bag][t][head*64 + d] = softmax(q kl^T) y + conv33(v); lse."""
+    nbh, n, dh = q.shape
+    s = q.double() @ kl.double().transpose(1, 2)
+    lse = torch.logsumexp(s, -1)
+    o = torch.softmax(s, -1) @ y.double()
+    vp = torch.nn.functional.pad(v.double(), (0, 0, 16, 16))
+    w = wconv.double().view(-1, 33)
+    for tau in range(33):
+        o += w[torch.arange(nbh) % nh, tau].view(nbh, 1, 1) * vp[:, tau:tau + n]
+    merged = o.view(nbh // nh, nh, n, dh).permute(0, 2, 1, 3).reshape(nbh // nh, n, nh * dh)
+    return merged, lse
+
+
+@pytest.mark.parametrize("nbh,n", [(8, 256), (8, 1280), (32, 512), (8, 8448), (8, 33280)])
+def test_a1_fwd_bf16_kernels(nbh, n):
+    """The per-CU chunk-walking bf16 A1 kernel (MFMA conv, LDS-DMA windows) and the legacy
+    128-query kernel (variant 4) against fp64; and against each other."""
+    L = _lib()
+    from transmil_deepgraft_amd._lib import BF16
+    from transmil_deepgraft_amd.engine import _p, _stream
+    g = torch.Generator(device="cpu").manual_seed(n + nbh)
+    nh = 8
+    q = (torch.randn(nbh, n, 64, generator=g) * 0.3).to(torch.bfloat16)
+    v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16)
+    kl = (torch.randn(nbh, 256, 64, generator=g) * 0.3).to(torch.bfloat16)
+    y = torch.randn(nbh, 256, 64, generator=g).to(torch.bfloat16)
+    wconv = torch.randn(nh, 33, generator=g) * 0.1
+    ref_m, ref_l = _a1_ref(q, v, kl, y, wconv, nh)
+    outs = []
+    for variant in (0, 14):
+        L.lib().tm_debug_set_variant(1, variant)
+        try:
+            merged = torch.full((nbh // nh, n, nh * 64), float("nan"), dtype=torch.bfloat16, device=DEV)
+            lse = torch.full((nbh, n), float("nan"), device=DEV)
+            qd, vd, kd, yd, wd = (t.to(DEV).contiguous() for t in (q, v, kl, y, wconv))
+            L.call("tm_nys_a1_fwd", BF16, _p(qd), _p(vd), _p(kd), _p(yd), _p(wd), nbh, nh, n, _p(merged), _p(lse),
+                   _stream())
+            torch.cuda.synchronize()
+        finally:
+            L.lib().tm_debug_set_variant(1, 0)
+        assert torch.isfinite(merged.float()).all() and torch.isfinite(lse).all()
+        assert _rel(merged.cpu(), ref_m) < 2e-2, variant
+        assert (lse.cpu().double() - ref_l).abs().max().item() < 1e-4, variant
+        outs.append(merged.cpu().float())
+    assert _rel(outs[0], outs[1].double()) < 2e-2

@@ -23,6 +23,7 @@
 //   conv_bwd         conv33 backward + D1 = rowsum(dO * O_att)
 //   attn_bwd<MODE>   shared flash-style backward for the A1 and A3 products
 //   assemble_dqkv    dq, dk, dv + landmark terms -> [B][n][3*h*64]
+#include <algorithm>
 #include "common.h"
 #include "../../include/transmil_hip.h"
 
@@ -152,6 +153,27 @@ template <> TM_DEV f32x8 value_frag<float>(const float* vt, int dt, int kb, int 
 // Shared forward block: one wave, 32 queries (B-operand fragments qf), 256 keys in
 // LDS (ks[key][KROW]), values^T in LDS (vt[d][VROW]).  Returns unnormalised O^T
 // (2 tiles: d 0-31, 32-63; col = query) plus per-query max and sum.
+constexpr float LOG2E = 1.4426950408889634f;
+
+// 16-element max as v_max3_f32 triples (8 instructions instead of 15)
+TM_DEV float max3f(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
+TM_DEV float tree_max16(const f32x16& x) {
+  const float m0 = max3f(x[0], x[1], x[2]), m1 = max3f(x[3], x[4], x[5]), m2 = max3f(x[6], x[7], x[8]);
+  const float m3 = max3f(x[9], x[10], x[11]), m4 = max3f(x[12], x[13], x[14]);
+  return __builtin_fmaxf(max3f(m0, m1, m2), max3f(m3, m4, x[15]));
+}
+// 16-element sum with packed adds (v_pk_add_f32: two lanes of the tree per instruction)
+TM_DEV float tree_sum16(const f32x16& x) {
+  f32x2 a[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    a[i] = (f32x2){x[2 * i], x[2 * i + 1]} + (f32x2){x[2 * i + 8], x[2 * i + 9]};
+  a[0] += a[2];
+  a[1] += a[3];
+  a[0] += a[1];
+  return a[0][0] + a[0][1];
+}
+
 template <typename T>
 TM_DEV void attn_fwd_wave(const T* ks, const T* vt, const vec8<T> (&qf)[4], f32x16 (&o)[2], float& mx, float& sum,
                           int lane) {
@@ -167,21 +189,22 @@ TM_DEV void attn_fwd_wave(const T* ks, const T* vt, const vec8<T> (&qf)[4], f32x
       mma16(s[kt], a, qf[st]);
     }
   }
-  float m = -INFINITY;
+  // row max and sum as balanced trees (a 128-long dependent fmaxf / add chain per lane
+  // costs its full latency), exp as exp2 of one fma: p = 2^(s log2e - m log2e)
+  float mk[8];
 #pragma unroll
-  for (int kt = 0; kt < 8; ++kt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) m = fmaxf(m, s[kt][i]);
+  for (int kt = 0; kt < 8; ++kt) mk[kt] = tree_max16(s[kt]);
+  float m = fmaxf(fmaxf(fmaxf(mk[0], mk[1]), fmaxf(mk[2], mk[3])), fmaxf(fmaxf(mk[4], mk[5]), fmaxf(mk[6], mk[7])));
   m = fmaxf(m, __shfl_xor(m, 32, 64));
-  float l = 0.f;
+  const float ml = m * LOG2E;
+  float lk[8];
 #pragma unroll
-  for (int kt = 0; kt < 8; ++kt)
+  for (int kt = 0; kt < 8; ++kt) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const float p = __expf(s[kt][i] - m);
-      s[kt][i] = p;
-      l += p;
-    }
+    for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(fmaf(s[kt][i], LOG2E, -ml));
+    lk[kt] = tree_sum16(s[kt]);
+  }
+  float l = ((lk[0] + lk[1]) + (lk[2] + lk[3])) + ((lk[4] + lk[5]) + (lk[6] + lk[7]));
   l += __shfl_xor(l, 32, 64);
   mx = m;
   sum = l;
@@ -200,14 +223,14 @@ TM_DEV void attn_fwd_wave(const T* ks, const T* vt, const vec8<T> (&qf)[4], f32x
 // LDS writes: a compile-time count of 16-B pieces per thread, so every load of the tile is
 // issued before the first wait (a runtime-bounded `for (i = tid; ...)` loop let the compiler
 // pipeline only the first few and serialise the rest, one HBM/L2 round trip each).
-template <typename T>
+template <typename T, int NT = 256>
 struct TileRegs {
-  static constexpr int E = 16 / sizeof(T), PER_ROW = DH / E, PER = NL * PER_ROW / 256;
+  static constexpr int E = 16 / sizeof(T), PER_ROW = DH / E, PER = NL * PER_ROW / NT;
   f32x4 r[PER];
   TM_DEV void load(const T* src, int tid) {
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int i = tid + 256 * j;
+      const int i = tid + NT * j;
       r[j] = *(const f32x4*)(src + (size_t)(i / PER_ROW) * DH + (i % PER_ROW) * E);
     }
   }
@@ -216,7 +239,7 @@ struct TileRegs {
     constexpr int KROW = Lay<T>::KROW;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int i = tid + 256 * j;
+      const int i = tid + NT * j;
       *(f32x4*)(ks + (i / PER_ROW) * KROW + (i % PER_ROW) * E) = r[j];
     }
   }
@@ -225,7 +248,7 @@ struct TileRegs {
     constexpr int VROW = Lay<T>::VROW;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
-      const int i = tid + 256 * j, key = i / PER_ROW, d0 = (i % PER_ROW) * E;
+      const int i = tid + NT * j, key = i / PER_ROW, d0 = (i % PER_ROW) * E;
       if constexpr (sizeof(T) == 2) {
         *(f32x4*)(vs + key * VROW + d0) = r[j];
       } else {
@@ -371,6 +394,262 @@ __global__ __launch_bounds__(256, 2) void a1_fwd_kernel(const T* __restrict__ q,
     for (int e = 0; e < 8; ++e) outv[e] = from_f<T>(ost[ql * 68 + dc + e]);
     store8(merged + ((size_t)bag * n + t) * (nh * DH) + head * DH + dc, outv);
   }
+}
+
+// ---------------------------------------------------------------------------
+// A1 path forward, bf16 (bench mode): one workgroup of 8 waves per CU; the landmark keys
+// and Y are staged ONCE per workgroup and each wave walks 32-query chunks of its head.
+// grid = (W, nbh) with W = min(256 / nbh, n / 32) workgroups per head and the head's n / 32
+// chunks split evenly over them, so at N = 8192 every CU holds one workgroup (the
+// 128-query-per-workgroup form launched 528 blocks on 512 slots: a second round for 16).
+// The 33-tap residual conv runs on the MFMA: per chunk (queries t0..t0+31)
+//   O^T[d][q] += sum_j V[t0 - 16 + j][d] * band[j][q],  band[j][q] = w[j - q] (0 <= j - q < 33)
+// over the workgroup's v window: rows [32 c_begin - 16, 32 c_end + 16) copied HBM -> LDS by
+// LDS-DMA (global_load_lds, no VGPRs) in the prologue and left in flight through the first
+// attention phase (v is read 1.1-1.2x, not the 2x of per-chunk windows).  Rows outside
+// [0, n) are fetched clamped and masked in the band instead.  The band fragments of
+// interior chunks are one shared LDS table; the first / last chunk of a head build theirs.
+// LDS: keys [256][72] + Y [256][80] + window [<=320][64] + 4 output stages [32][72] + band
+// table + taps = 140 KB.  One wave per SIMD (512 registers): the wave overlaps its own MFMA
+// and VALU work instead of two waves running the same phases in lockstep.
+constexpr int A1P_WAVES = 4;                                            // one wave per SIMD: 512 registers
+constexpr int A1P_MAXCH = 9;                                            // chunks per workgroup (host-checked)
+constexpr int A1P_WROWS = A1P_MAXCH * 32 + 32;                          // 320 window rows
+constexpr int A1P_OROW = DH + 8;                                        // output stage row (bf16): 144 B
+constexpr size_t A1P_KS = (size_t)NL * Lay<bf16>::KROW * 2;             // 36864
+constexpr size_t A1P_VT = (size_t)NL * Lay<bf16>::VROW * 2;             // 40960
+constexpr size_t A1P_WIN = (size_t)A1P_WROWS * DH * 2;                  // 40960
+constexpr size_t A1P_OST = (size_t)32 * A1P_OROW * 2;                   // 4608 per wave
+constexpr size_t A1P_WIN_OFF = A1P_KS + A1P_VT;
+constexpr size_t A1P_OST_OFF = A1P_WIN_OFF + A1P_WIN;
+constexpr size_t A1P_BAND_OFF = A1P_OST_OFF + A1P_WAVES * A1P_OST;      // [4][64] x 16 B
+constexpr size_t A1P_TAPS_OFF = A1P_BAND_OFF + 4 * 64 * 16;
+constexpr size_t A1P_BYTES = A1P_TAPS_OFF + 128 * sizeof(float);        // 162304
+
+// diagnostic stamps (VAR 9 build only): [block][wave][slot] s_memtime, read by tm_debug_a1_stamps
+__device__ unsigned long long g_a1_stamps[512 * 8 * 8];
+template <int VAR>
+TM_DEV void a1p_stamp(int slot, int wave) {
+  if constexpr (VAR == 9) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if ((threadIdx.x & 63) == 0)
+      g_a1_stamps[((blockIdx.y * gridDim.x + blockIdx.x) * 8 + wave) * 8 + slot] = t;
+  }
+}
+
+TM_DEV void wave_lds_fence() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// A operand of the conv product: window rows kb.. (acc_k_index order, as value_frag)
+TM_DEV bf16x8 a1p_window_frag(const bf16* win, int dt, int kb, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int d = dt * 32 + (g & 1) * 16 + 4 * p;
+  const int key = kb + 4 * (g >> 1) + q;
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(win + key * DH + d));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(win + (key + 8) * DH + d));
+  return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// attn_fwd_wave with the per-tile work interleaved for the scheduler: the max tree of score
+// tile kt beside the MFMAs of tile kt + 1, the exp / sum / bf16 packing of tile kt beside its
+// P.V MFMAs (the two-phase form ran the MFMA and VALU phases back to back).
+TM_DEV void attn_fwd_wave_il(const bf16* ks, const bf16* vt, const bf16x8 (&qf)[4], f32x16 (&o)[2], float& mx,
+                             float& sum, int lane) {
+  constexpr int KROW = Lay<bf16>::KROW;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 s[8];
+  float mk[8];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    s[kt] = (f32x16){};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) mma16(s[kt], load8(ks + (kt * 32 + r) * KROW + st * 16 + 8 * h), qf[st]);
+    mk[kt] = tree_max16(s[kt]);
+  }
+  float m = fmaxf(fmaxf(fmaxf(mk[0], mk[1]), fmaxf(mk[2], mk[3])), fmaxf(fmaxf(mk[4], mk[5]), fmaxf(mk[6], mk[7])));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  const float ml = m * LOG2E;
+  o[0] = (f32x16){};
+  o[1] = (f32x16){};
+  float lk[8];
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(fmaf(s[kt][i], LOG2E, -ml));
+    lk[kt] = tree_sum16(s[kt]);
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      const bf16x8 p = acc_as_operand<bf16>(s[kt], sp);
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) mma16(o[dt], value_frag<bf16>(vt, dt, kt * 32 + 16 * sp, lane), p);
+    }
+  }
+  float l = ((lk[0] + lk[1]) + (lk[2] + lk[3])) + ((lk[4] + lk[5]) + (lk[6] + lk[7]));
+  l += __shfl_xor(l, 32, 64);
+  mx = m;
+  sum = l;
+}
+
+template <int VAR = 0>  // ablation: 1 no conv MFMAs, 2 no attention phase, 3 prologue only, 9 stamps
+__global__ __launch_bounds__(256) void a1_fwd_bf16_kernel(const bf16* __restrict__ q, const bf16* __restrict__ v,
+                                                          const bf16* __restrict__ kl_t, const bf16* __restrict__ y_t,
+                                                          const float* __restrict__ wconv, int n, int nh, int wpg,
+                                                          bf16* __restrict__ merged, float* __restrict__ lse1) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* ks = (bf16*)smem;
+  bf16* vt = (bf16*)(smem + A1P_KS);
+  bf16* win = (bf16*)(smem + A1P_WIN_OFF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  bf16* ost = (bf16*)(smem + A1P_OST_OFF + wave * A1P_OST);
+  bf16x8* band_tab = (bf16x8*)(smem + A1P_BAND_OFF);
+  float* taps = (float*)(smem + A1P_TAPS_OFF);
+  const int bh = blockIdx.y, gi = blockIdx.x;
+  const int head = bh % nh, bag = bh / nh;
+  const int cph = n / 32;                          // 32-query chunks of this head
+  const int c_begin = (int)((long long)gi * cph / wpg), c_end = (int)((long long)(gi + 1) * cph / wpg);
+  const int w0 = c_begin * 32 - HALF;              // sequence row of window row 0
+  const int wrows = (c_end - c_begin) * 32 + 2 * HALF;
+  const bf16* qb = q + (size_t)bh * n * DH;
+  const bf16* vb = v + (size_t)bh * n * DH;
+  const int ld = nh * DH;
+  a1p_stamp<VAR>(0, wave);
+
+  // ---- prologue: keys, Y, taps and this wave's first query fragments through registers;
+  //      the v window by LDS-DMA, left in flight through the first attention phase ----
+  int c = c_begin + wave;
+  bf16x8 qf[4];
+  if (c < c_end) {
+#pragma unroll
+    for (int st = 0; st < 4; ++st) qf[st] = load8(qb + (size_t)(c * 32 + r) * DH + st * 16 + 8 * h);
+  }
+  TileRegs<bf16, 256> kr, yr;
+  kr.load(kl_t + (size_t)bh * NL * DH, tid);
+  yr.load(y_t + (size_t)bh * NL * DH, tid);
+  float tapv = 0.f;
+  if (tid < 128) {
+    const int tau = tid - 32;  // taps[k] = w[k - 32], zero outside the filter
+    if (tau >= 0 && tau < TAPS) tapv = wconv[head * TAPS + tau];
+  }
+  {
+    typedef __attribute__((address_space(3))) void lds_t;
+    typedef __attribute__((address_space(1))) void glb_t;
+#pragma unroll
+    for (int i = 0; i < A1P_WROWS * 8 / 256; ++i) {
+      const int pc = i * 256 + tid, row = pc >> 3;  // 16-B piece pc of the window image
+      if (i * 32 < wrows) {                         // wave-uniform: 8 rows per wave-instruction
+        const int src = min(max(w0 + row, 0), n - 1);
+        __builtin_amdgcn_global_load_lds((glb_t*)(vb + (size_t)src * DH + (pc & 7) * 8),
+                                         (lds_t*)(win + (size_t)(i * 256 + wave * 64) * 8), 16, 0, 0);
+      }
+    }
+  }
+  kr.store_keys(ks, tid);
+  yr.store_values(vt, tid);
+  if (tid < 128) taps[tid] = tapv;
+  __syncthreads();  // taps visible
+  {  // interior band fragments: element jj of lane (rr, hh), k-step s = wave
+    const int s = tid >> 6, ln = tid & 63, rr = ln & 31, hh = ln >> 5;
+    bf16x8 b;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) b[jj] = (bf16)taps[16 * s + 8 * (jj >> 2) + 4 * hh + (jj & 3) - rr + 32];
+    band_tab[s * 64 + ln] = b;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // keys / Y / band table in LDS; the window DMA may still be in flight
+  a1p_stamp<VAR>(1, wave);
+  if constexpr (VAR == 3) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (c < c_end && lane == 0) lse1[(size_t)bh * n + c * 32] = to_f(ks[tid]) + to_f(vt[tid]) + to_f(qf[0][0]);
+    return;
+  }
+
+  bool first = true;
+  for (;;) {
+    const bool active = c < c_end;
+    const int t0 = c * 32;
+    f32x16 o[2];
+    float mx = 0.f, sum = 1.f;
+    if (active) {
+      if constexpr (VAR == 2) {
+        o[0] = (f32x16){}; o[1] = (f32x16){};
+        mx = to_f(qf[0][0]);
+      } else {
+        attn_fwd_wave_il(ks, vt, qf, o, mx, sum, lane);
+      }
+    }
+    if (first) a1p_stamp<VAR>(2, wave);
+    const int cn = c + A1P_WAVES;
+    if (cn < c_end) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st) qf[st] = load8(qb + (size_t)(cn * 32 + r) * DH + st * 16 + 8 * h);
+    }
+    if (first) {
+      // every wave's window pieces have landed (the next chunk's 4 query loads may not)
+      if (cn < c_end) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      first = false;
+      a1p_stamp<VAR>(3, wave);
+    }
+    if (!active) break;
+    // band fragments from the shared table.  At the sequence ends the window rows outside
+    // [0, n) are exactly one k-step: rows j < 16 (k-step 0) for t0 = 0, rows j >= 48 (k-step 3)
+    // for the last chunk -- those fragments are zeroed.
+    bf16x8 band[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) band[s] = band_tab[s * 64 + lane];
+    if (t0 == 0) band[0] = bf16x8{};
+    if (t0 + 32 == n) band[3] = bf16x8{};
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) o[dt][i] *= inv;
+    if constexpr (VAR != 1) {
+      const bf16* wc = win + (size_t)(t0 - HALF - w0) * DH;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) mma16(o[dt], a1p_window_frag(wc, dt, 16 * s, lane), band[s]);
+    }
+    if (c == c_begin + wave) a1p_stamp<VAR>(4, wave);
+    if (h == 0) lse1[(size_t)bh * n + t0 + r] = mx + __logf(sum);
+    // O^T registers -> [32 q][72] bf16 wave stage -> full 128-B row stores, 16 B per lane
+    // (row-per-lane 8-B stores are store-issue bound)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        bf16x4 pk;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pk[e] = (bf16)o[dt][4 * g4 + e];
+        *(bf16x4*)(ost + r * A1P_OROW + dt * 32 + 8 * g4 + 4 * h) = pk;
+      }
+    wave_lds_fence();
+    f32x4 ov[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = lane + 64 * i;
+      ov[i] = *(const f32x4*)(ost + (p >> 3) * A1P_OROW + (p & 7) * 8);
+    }
+    bf16* dst = merged + ((size_t)bag * n + t0) * ld + head * DH;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = lane + 64 * i;
+      *(f32x4*)(dst + (size_t)(p >> 3) * ld + (p & 7) * 8) = ov[i];
+    }
+    wave_lds_fence();  // stage read back before the next chunk rewrites it
+    if (c == c_begin + wave) a1p_stamp<VAR>(5, wave);
+    c = cn;
+    if (c >= c_end) break;
+  }
+  a1p_stamp<VAR>(6, wave);
 }
 
 // ---------------------------------------------------------------------------
@@ -1066,6 +1345,15 @@ __global__ void assemble_dqkv_kernel(const float* __restrict__ dq, const float* 
 
 // ============================ C entry points ===============================
 extern "C" void tm_debug_set_nys_variant(int value) { g_nys_variant = value; }
+// copy the VAR 9 a1_fwd stamps ([block][wave][8] u64) to a host buffer (diagnostics only)
+extern "C" int tm_debug_a1_stamps(unsigned long long* host, int count) {
+  TM_REQUIRE(count > 0 && count <= 512 * 8 * 8, "a1_stamps: bad count");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_a1_stamps), count * sizeof(unsigned long long)) != hipSuccess) {
+    tm_set_error("a1_stamps: copy");
+    return 2;
+  }
+  return 0;
+}
 
 #define TM_DTYPE_DISPATCH(dt, CALL)                               \
   if ((dt) == TM_BF16) { using T = bf16; CALL; }                  \
@@ -1122,6 +1410,21 @@ extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void
                              const float* wconv, int nbh, int nh, int n, void* merged, float* lse1, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0 && nbh % nh == 0, "a1_fwd: bad shape");
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == TM_BF16 && g_nys_variant != 14) {
+    const int cph = n / 32;
+    int wpg = std::max(1, std::min(256 / std::max(nbh, 1), cph));
+    wpg = std::max(wpg, (cph + A1P_MAXCH - 1) / A1P_MAXCH);  // <= A1P_MAXCH chunks per workgroup
+    // ablation variants 11-19 (microbench only): 10 + VAR
+    auto kern = g_nys_variant == 11 ? a1_fwd_bf16_kernel<1> : g_nys_variant == 12 ? a1_fwd_bf16_kernel<2>
+              : g_nys_variant == 13 ? a1_fwd_bf16_kernel<3> : g_nys_variant == 19 ? a1_fwd_bf16_kernel<9>
+              : a1_fwd_bf16_kernel<0>;
+    tm_allow_smem(kern, A1P_BYTES);
+    kern<<<dim3(wpg, nbh), 256, A1P_BYTES, st>>>((const bf16*)q, (const bf16*)v, (const bf16*)kl_t,
+                                                               (const bf16*)y_t, wconv, n, nh, wpg, (bf16*)merged,
+                                                               lse1);
+    TM_CHECK_LAUNCH();
+    return 0;
+  }
   TM_DTYPE_DISPATCH(dtype, ({
     const size_t sm1 = ((size_t)NL * Lay<T>::KROW + Lay<T>::VELEMS) * sizeof(T);
     const size_t sm = sm1 > A1_EPI_BYTES ? sm1 : A1_EPI_BYTES;
