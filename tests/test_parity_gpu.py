@@ -82,6 +82,32 @@ def test_golden_d512_logits(name, N):
     assert (lo.argmax(1) == fx["logits"].argmax(1)).all()
 
 
+@pytest.mark.parametrize("dtype,atol", [(torch.float32, 1e-4), (torch.bfloat16, 5e-2)])
+def test_golden_long_sequence_c3(dtype, atol):
+    """Config C3 (SURVEY.md section 8 d): 3-class, N = 32768 (n' = 33280, l = 130) against
+    the oracle-generated fixture (tests/golden/make_golden_long.py); fp32 within 1e-4, bf16
+    within 5e-2, argmax equal.  Then one bf16 train-mode backward at that size: every
+    gradient finite and nonzero."""
+    fx = load("d512c3_n32768")
+    _, ours = _pair(3, dtype=dtype)
+    N = 32768
+    x = torch.from_numpy(bag_input(N, 512, 2021 + 1000 + N)).to(DEV)
+    with torch.no_grad():
+        lo = ours(x).cpu().numpy()
+    np.testing.assert_allclose(lo, fx["logits.f64"], rtol=0, atol=atol)
+    assert (lo.argmax(1) == fx["logits"].argmax(1)).all()
+    if dtype == torch.bfloat16:
+        ours.train()
+        logits = ours(x)
+        loss = torch.nn.CrossEntropyLoss()(logits, torch.nn.functional.one_hot(
+            torch.tensor([2], device=DEV), 3).float())
+        loss.backward()
+        torch.cuda.synchronize()
+        for name, p in ours.named_parameters():
+            assert torch.isfinite(p.grad).all(), name
+            assert p.grad.abs().max() > 0, name
+
+
 @pytest.mark.parametrize("N", [1024, 8192])
 def test_bf16_mode_close_to_oracle(N):
     ref, ours = _pair(2, dtype=torch.bfloat16)
