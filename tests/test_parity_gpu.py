@@ -135,9 +135,11 @@ def test_bf16_mode_grads_close_to_oracle(N):
     assert not bad, bad
 
 
-def test_bf16_staged_attention_backward_is_bitwise_the_per_chunk_one():
-    """The once-staged bf16 attention backward (default) and the per-chunk-staged one
-    (variant 3) compute the same sums in the same order: gradients bitwise equal."""
+def test_bf16_staged_attention_backward_matches_the_per_chunk_one():
+    """The once-staged bf16 attention backward (default: the A1 queries split evenly over one
+    workgroup per CU) and the per-chunk-staged one (variant 3: 256-query blocks) compute the
+    same products; only the partition of the landmark-gradient partial sums differs (32 vs 12
+    slabs at N = 3000, n' = 3072), so the gradients agree to fp32 summation-order rounding."""
     from transmil_deepgraft_amd import _lib
     ref, ours = _pair(2, dtype=torch.bfloat16)
     x = torch.from_numpy(bag_input(3000, 512, 7))
@@ -151,7 +153,8 @@ def test_bf16_staged_attention_backward_is_bitwise_the_per_chunk_one():
             _lib.lib().tm_debug_set_variant(1, 0)
         grads.append(g)
     for name in grads[0]:
-        assert torch.equal(grads[0][name], grads[1][name]), name
+        a, b = grads[0][name].double(), grads[1][name].double()
+        assert ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item() < 1e-4, name
 
 
 def test_return_attn_contract():

@@ -902,6 +902,7 @@ struct BwdArgs {
   float* dv; long long dv_bh;
   long long slab_stride;                                // per block partial slab stride (MODE dependent)
   int nh, n_queries_per_wg, n_key_rows;
+  int q_total;  // bf16 A1 kernel: > 0 = split the q_total / 32 query chunks evenly over gridDim.x
 };
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
@@ -1113,14 +1114,15 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
 // dependent HBM round trips per 32-query chunk).  dV/dK operands come from the same
 // row-major images through transposing reads (acc_as_operand k order).
 struct BwdLay16 {
+  static constexpr int MAXQ = 288;  // query rows per workgroup (A1 even split: <= 9 chunks of 32)
   static constexpr int KT_ROW = NL + 8, DS_ROW = NL + 8, QROW = DH + 8;
   static constexpr size_t KT_OFF = 0;
   static constexpr size_t DS_OFF = KT_OFF + DH * KT_ROW * 2;
   static constexpr size_t QS_OFF = DS_OFF + 32 * DS_ROW * 2;
-  static constexpr size_t OS_OFF = QS_OFF + NL * QROW * 2;
-  static constexpr size_t XC_OFF = OS_OFF + NL * QROW * 2;  // fp32 [3][2][1024]
-  static constexpr size_t LS_OFF = XC_OFF + 6 * 1024 * 4;   // fp32 lse[256], D[256]
-  static constexpr size_t MAIN = LS_OFF + 2 * NL * 4;
+  static constexpr size_t OS_OFF = QS_OFF + MAXQ * QROW * 2;
+  static constexpr size_t XC_OFF = OS_OFF + MAXQ * QROW * 2;  // fp32 [3][2][1024]
+  static constexpr size_t LS_OFF = XC_OFF + 6 * 1024 * 4;     // fp32 lse[MAXQ], D[MAXQ]
+  static constexpr size_t MAIN = LS_OFF + 2 * MAXQ * 4;       // 160512 B
   static constexpr size_t EPI = (size_t)NL * 68 * 4;
   static constexpr size_t BYTES = MAIN > EPI ? MAIN : EPI;
 };
@@ -1149,14 +1151,23 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
   bf16* os = (bf16*)(smem + LY::OS_OFF);
   float* xch = (float*)(smem + LY::XC_OFF);
   float* lse_s = (float*)(smem + LY::LS_OFF);
-  float* dd_s = lse_s + NL;
+  float* dd_s = lse_s + LY::MAXQ;
   float* stage = (float*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, bh = blockIdx.y, nh = a.nh;
   const int key0 = (MODE == MODE_A3) ? blk * NL : 0;
-  const int q_begin = (MODE == MODE_A1) ? blk * a.n_queries_per_wg : 0;
-  const int q_count = a.n_queries_per_wg;  // <= 256, a multiple of 32 (host-checked)
+  int q_begin = (MODE == MODE_A1) ? blk * a.n_queries_per_wg : 0;
+  int q_count = a.n_queries_per_wg;  // <= 256, a multiple of 32 (host-checked)
+  if (MODE == MODE_A1 && a.q_total > 0) {
+    // even split of the q_total / 32 query chunks over the gridDim.x workgroups of a head: at
+    // N = 8192 that is 8-9 chunks for each of 32 workgroups (256 = one per CU) instead of 33
+    // blocks of 8 chunks (264 > 256 CUs: a second round for 8 of them)
+    const int cph = a.q_total / 32;
+    const int c0 = (int)((long long)blk * cph / gridDim.x), c1 = (int)((long long)(blk + 1) * cph / gridDim.x);
+    q_begin = 32 * c0;
+    q_count = 32 * (c1 - c0);  // <= MAXQ (host-checked)
+  }
 
   const bf16* Q = (const bf16*)a.q + hoff(bh, nh, a.q_bag, a.q_head) + (size_t)q_begin * a.q_row;
   const bf16* dO = (const bf16*)a.dO + hoff(bh, nh, a.o_bag, a.o_head) + (size_t)q_begin * a.o_row;
@@ -1166,14 +1177,18 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
   const float* dd = a.dd + bh * a.dd_bh + q_begin;
 
   // ---- one burst of loads: K rows (for K^T), Q / dO rows, K / V fragments, lse / D ----
+  constexpr int QP = (LY::MAXQ * 8 + 511) / 512;  // 16-B query-row pieces per thread (5)
   const int mykey = wave * 32;
-  bf16x8 kr[4], qr[4], orow[4], kf[4], vf[4];
-  float lsev = 0.f;
+  bf16x8 kr[4], qr[QP], orow[QP], kf[4], vf[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = tid + 512 * j;  // 16-B piece: row c >> 3, d0 = (c & 7) * 8
     kr[j] = load8(K + (size_t)(c >> 3) * DH + (c & 7) * 8);
-    const int qq = min(c >> 3, q_count - 1);
+  }
+#pragma unroll
+  for (int j = 0; j < QP; ++j) {
+    const int c = tid + 512 * j;
+    const int qq = min(c >> 3, q_count - 1);  // rows past q_count: clamped, never read back
     qr[j] = load8(Q + (size_t)qq * a.q_row + (c & 7) * 8);
     orow[j] = load8(dO + (size_t)qq * a.o_row + (c & 7) * 8);
   }
@@ -1182,9 +1197,11 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
     kf[st] = load8(K + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
     vf[st] = load8(V + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
   }
-  {
-    const int qq = min(tid & (NL - 1), q_count - 1);
-    lsev = tid < NL ? lse[qq] : dd[qq];
+  float lsev = 0.f, ddv = 0.f;
+  if (tid < LY::MAXQ) {
+    const int qq = min(tid, q_count - 1);
+    lsev = lse[qq];
+    ddv = dd[qq];
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1192,10 +1209,19 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
     const int c = tid + 512 * j, row = c >> 3, d0 = (c & 7) * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) kt_s[(d0 + e) * KT_ROW + row] = kr[j][e];
-    *(bf16x8*)(qs + row * QROW + d0) = qr[j];
-    *(bf16x8*)(os + row * QROW + d0) = orow[j];
   }
-  (tid < NL ? lse_s : dd_s)[tid & (NL - 1)] = lsev;
+#pragma unroll
+  for (int j = 0; j < QP; ++j) {
+    const int c = tid + 512 * j, row = c >> 3, d0 = (c & 7) * 8;
+    if (row < LY::MAXQ) {
+      *(bf16x8*)(qs + row * QROW + d0) = qr[j];
+      *(bf16x8*)(os + row * QROW + d0) = orow[j];
+    }
+  }
+  if (tid < LY::MAXQ) {
+    lse_s[tid] = lsev;
+    dd_s[tid] = ddv;
+  }
   __syncthreads();
 
   f32x16 dvt[2], dkt[2];  // [d tile], cols = this wave's 32 keys
@@ -1472,15 +1498,26 @@ extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merge
 
 // A1 backward: keys = landmarks kl_t [bh][256][64], values = y_t, queries = q rows, dO = dmerged.
 // dq (fp32 [bh][n][64]) written; dkl/dy partial slabs [n/qpw][bh][256][64] in work.
+namespace {
+// workgroups per head of the bf16 A1 backward (even split of the n / 32 query chunks)
+int a1_bwd_split(int nbh, int n) {
+  const int cph = n / 32;
+  const int w = std::min(cph, std::max(1, 256 / std::max(nbh, 1)));
+  return std::max(w, (cph + BwdLay16::MAXQ / 32 - 1) / (BwdLay16::MAXQ / 32));
+}
+}  // namespace
+
 extern "C" long long tm_nys_a1_bwd_workspace(int nbh, int n, int queries_per_wg) {
-  return 2LL * (n / queries_per_wg) * nbh * NL * DH * (long long)sizeof(float);
+  const long long slabs = std::max((long long)(n / queries_per_wg), (long long)a1_bwd_split(nbh, n));
+  return 2LL * slabs * nbh * NL * DH * (long long)sizeof(float);
 }
 
 extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t,
                              const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
                              float* dq, float* work, float* dkl, float* dy, int accumulate, void* stream) {
   TM_REQUIRE(queries_per_wg % 32 == 0 && n % queries_per_wg == 0, "a1_bwd: queries_per_wg must divide n, x32");
-  const int nqc = n / queries_per_wg;
+  const bool split = dtype == TM_BF16 && queries_per_wg <= NL && g_nys_variant != 3;
+  const int nqc = split ? a1_bwd_split(nbh, n) : n / queries_per_wg;
   BwdArgs a{};
   a.q = q; a.q_bag = (long long)nh * n * DH; a.q_head = (long long)n * DH; a.q_row = DH;
   a.dO = dmerged; a.o_bag = (long long)n * nh * DH; a.o_head = DH; a.o_row = nh * DH;
@@ -1495,7 +1532,8 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
   a.slab_stride = (long long)nbh * NL * DH;
   a.nh = nh; a.n_queries_per_wg = queries_per_wg; a.n_key_rows = NL;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TM_BF16 && queries_per_wg <= NL && g_nys_variant != 3) {
+  if (split) {
+    a.q_total = n;
     tm_allow_smem(attn_bwd_bf16_kernel<MODE_A1>, BwdLay16::BYTES);
     attn_bwd_bf16_kernel<MODE_A1><<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
   } else {
