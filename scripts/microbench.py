@@ -130,8 +130,17 @@ def main():
     case("bmm Y=ZW 256x64x256 x8", lambda: E.bmm([E.bmm_job(Z, 0, W, 0, Y, 256, 64, 256)], nbh), f // 4)
     case("torch bmm fp32 256^3 x8", lambda: torch.bmm(X, Z, out=P), f)
     saved = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=dev)
-    case("pinv_fwd (26 launches)", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 0, E._p(saved), st()), 24 * f)
-    case("pinv_fwd [bf16x3]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 1, E._p(saved), st()), 24 * f)
+    pwork = torch.empty(_lib.query("tm_pinv_bwd_workspace_floats", nbh), device=dev)
+    pdz = torch.randn(nbh, 256, 256, device=dev) * 1e-3
+    pdX = torch.empty(nbh, 256, 256, device=dev)
+    for team, nm in ((1, "persistent"), (2, "persistent, no sync"), (0, "per-launch")):
+        _lib.lib().tm_debug_set_variant(3, team)
+        case(f"pinv_fwd fp32 [{nm}]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 0, E._p(saved), st()), 24 * f)
+        case(f"pinv_fwd bf16x3 [{nm}]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 1, E._p(saved), st()),
+             24 * f)
+        case(f"pinv_bwd bf16x3 [{nm}]", lambda: _lib.call("tm_pinv_bwd", E._p(X), nbh, 6, 1, E._p(saved), E._p(pdz),
+                                                           E._p(pwork), E._p(pdX), st()), 28 * f)
+    _lib.lib().tm_debug_set_variant(3, 0)
     for gv in ((0, 1, 2) if args.gemm_ab else (0,)):
         _lib.lib().tm_debug_set_variant(2, gv)
         tag[0] = ("", "[2 LDS buf] ", "[glds ring] ")[gv]

@@ -139,7 +139,8 @@ def test_bf16_staged_attention_backward_matches_the_per_chunk_one():
     """The once-staged bf16 attention backward (default: the A1 queries split evenly over one
     workgroup per CU) and the per-chunk-staged one (variant 3: 256-query blocks) compute the
     same products; only the partition of the landmark-gradient partial sums differs (32 vs 12
-    slabs at N = 3000, n' = 3072), so the gradients agree to fp32 summation-order rounding."""
+    slabs at N = 3000, n' = 3072); the fp32 partial sums differ in rounding, which can flip a
+    bf16 rounding downstream, so the gradients agree within 2e-3 (the bf16 gate is 6e-2)."""
     from transmil_deepgraft_amd import _lib
     ref, ours = _pair(2, dtype=torch.bfloat16)
     x = torch.from_numpy(bag_input(3000, 512, 7))
@@ -154,7 +155,7 @@ def test_bf16_staged_attention_backward_matches_the_per_chunk_one():
         grads.append(g)
     for name in grads[0]:
         a, b = grads[0][name].double(), grads[1][name].double()
-        assert ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item() < 1e-4, name
+        assert ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item() < 2e-3, name
 
 
 def test_return_attn_contract():
