@@ -180,12 +180,8 @@ def main():
                 opt.zero_grad(set_to_none=True)
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        engine.probe.target = args.probe
-        engine.probe.events.clear()
         with torch.cuda.graph(graph):
             body()
-        engine.probe.target = None
-        captured_events = list(engine.probe.events)
 
         def step(i):
             load(i)
@@ -199,6 +195,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     kernel_ms_samples = []
+    overhead_samples = []
+    span_samples = []
     for i in range(args.steps):
         step(i)
         if (i + 1) % 50 == 0 and rank == 0:
@@ -213,20 +211,41 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     if graph is not None:
-        # HIP events recorded inside the captured graph hold the LAST replay's timestamps
+        # after the timed region: the same step captured once more with external HIP events
+        # around the probed launches (graph event-record nodes on the kernel's stream), replayed
+        # three times; the events hold each replay's timestamps.  The timed graph has no probes.
         try:
-            kernel_ms_samples = [s.elapsed_time(e) for s, e in captured_events]
-        except Exception:  # noqa: BLE001 - event timing inside graphs unsupported: probe eagerly
+            pgraph = torch.cuda.CUDAGraph()
+            engine.probe.target, engine.probe.external = args.probe, True
+            engine.probe.events.clear()
+            with torch.cuda.graph(pgraph):
+                body()
+            engine.probe.target, engine.probe.external = None, False
+            for i in range(3):
+                load(i)
+                pgraph.replay()
+                torch.cuda.synchronize()
+                kernel_ms_samples += [s.elapsed_time(e) for s, e in engine.probe.events]
+        except Exception as exc:  # noqa: BLE001 - event timing inside graphs unsupported: probe eagerly
+            print(f"# graph event probe unavailable ({exc}); eager probe", file=sys.stderr)
+            engine.probe.target, engine.probe.external = None, False
             kernel_ms_samples = []
         if not kernel_ms_samples:
+            # after the timed region: three eager steps with the probed launch queued behind
+            # a GPU spin (engine._Probe.spin_cycles), so its events bracket the kernel itself
             engine.probe.target = args.probe
+            engine.probe.spin_cycles = 2_000_000
             engine.probe.events.clear()
             for i in range(3):
                 load(i)
                 body()
             torch.cuda.synchronize()
             engine.probe.target = None
-            kernel_ms_samples = [s.elapsed_time(e) for s, e in engine.probe.events]
+            engine.probe.spin_cycles = 0
+            # launch span minus the span of an empty event pair recorded just before it
+            kernel_ms_samples = [s.elapsed_time(e) - zs.elapsed_time(ze) for s, e, zs, ze in engine.probe.events]
+            overhead_samples = [zs.elapsed_time(ze) for _, _, zs, ze in engine.probe.events]
+            span_samples = [s.elapsed_time(e) for s, e, _, _ in engine.probe.events]
     if graph is None:
         kernel_ms_samples = [s.elapsed_time(e) for s, e in engine.probe.events]
     kernel_ms = sum(kernel_ms_samples) / max(len(kernel_ms_samples), 1)
@@ -245,6 +264,9 @@ def main():
                 if hbm_bound else
                 dict(bound="mfma", achieved=round(ach_fl, 2), peak=peak_fl, unit="TFLOP/s",
                      frac=round(ach_fl / peak_fl, 4), traffic=measured_traffic(args.probe, args.n, args.dtype)))
+        if overhead_samples:
+            roof.update(event_span_ms=round(sum(span_samples) / len(span_samples), 5),
+                        event_pair_overhead_ms=round(sum(overhead_samples) / len(overhead_samples), 5))
         roof.update(kernel=args.probe, kernel_ms=round(kernel_ms, 5), launches=len(kernel_ms_samples),
                     algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])
         out = {

@@ -41,6 +41,12 @@ class _Probe:
     def __init__(self):
         self.target = None
         self.events = []
+        # > 0: a GPU spin of this many cycles is queued ahead of the start event, so the host
+        # has already submitted the kernel when the event fires and the pair times the kernel,
+        # not the host's launch latency (used only outside any timed region or graph capture)
+        self.spin_cycles = 0
+        # True while capturing a probe graph: external events become graph event-record nodes
+        self.external = False
 
     def __call__(self, name):
         return _ProbeCtx(self, name)
@@ -52,15 +58,22 @@ class _ProbeCtx:
 
     def __enter__(self):
         if self.p.target == self.name:
-            self.s = torch.cuda.Event(enable_timing=True)
-            self.e = torch.cuda.Event(enable_timing=True)
+            self.z = None
+            if self.p.spin_cycles > 0:
+                torch.cuda._sleep(self.p.spin_cycles)
+                # an empty event pair first: its span is the pair's own overhead
+                self.z = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                self.z[0].record()
+                self.z[1].record()
+            self.s = torch.cuda.Event(enable_timing=True, external=self.p.external)
+            self.e = torch.cuda.Event(enable_timing=True, external=self.p.external)
             self.s.record()
         return self
 
     def __exit__(self, *exc):
         if self.p.target == self.name:
             self.e.record()
-            self.p.events.append((self.s, self.e))
+            self.p.events.append((self.s, self.e) if self.z is None else (self.s, self.e, *self.z))
         return False
 
 
