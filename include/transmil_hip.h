@@ -119,6 +119,12 @@ long long tm_nys_a3_bwd_workspace(int nbh, int n);
 int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
                   const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
                   float* work, float* dql, int accumulate, void* stream);
+/* Row `row` of the return_attn product attn1 Z attn3 (App. A eq. 11; read by
+ * code/visualize_mil.py:580-581 as cls_attention[0,:,padding+1,...]) for every bag and
+ * head, without the [n, n] matrix: out [B*h, n] fp32 from the forward's q, k (T, q
+ * pre-scaled), ql / kl [B*h,256,64], Z [B*h,256,256] and lse3 [B*h,256] (fp32). */
+int tm_nys_attn_row(int dtype, const void* q, const void* k, const float* ql, const float* kl, const float* z,
+                    const float* lse3, int nbh, int n, int row, float* out, void* stream);
 int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const float* dk, const float* dkl,
                          const float* dv, int nbags, int nh, int n, float scale, void* dqkv, void* stream);
 

@@ -270,6 +270,11 @@ def main():
     case("a3_bwd (+reduce)", lambda: _lib.call("tm_nys_a3_bwd", BF16, E._p(ql_t), E._p(dw_t), E._p(k), E._p(v),
                                                E._p(lse3), E._p(d3), nbh, 8, n, E._p(dk), E._p(dv), E._p(a3bw),
                                                E._p(dql), 1, st()), 10 * nbh * n * 256 * 64)
+    zz = torch.randn(nbh, 256, 256, device=dev) * 1e-2
+    arow = torch.empty(nbh, n, device=dev)
+    case("attn_row (return_attn row)", lambda: _lib.call("tm_nys_attn_row", BF16, E._p(q), E._p(k), E._p(ql), E._p(kl),
+                                                         E._p(zz), E._p(lse3), nbh, n, 167, E._p(arow), st()),
+         2 * nbh * n * 256 * 64)
     # ---------------- PPEG ----------------
     x = torch.randn(1, S, 512, device=dev)
     wf = torch.randn(512 * 49, device=dev) * 0.1

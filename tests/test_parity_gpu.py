@@ -172,6 +172,46 @@ def test_return_attn_contract():
     assert ((row_o - row_r).abs().max() / row_r.abs().max()).item() < 1e-3
 
 
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("N,B", [(200, 1), (1000, 2)])
+def test_attention_map_rows_match_the_full_product(dtype, tol, N, B):
+    """SURVEY.md section 8 f rank 1: return_attn rows through tm_nys_attn_row (no n x n
+    matrix) against the materialised attn1 Z attn3 of the same factors, for the consumers'
+    row (padding + 1), the class-token row, the last row (negative index) and bag 1."""
+    from transmil_deepgraft_amd.nystrom_attention import AttentionMap
+    _, ours = _pair(2, dtype=dtype)
+    x = torch.from_numpy(bag_input(N, 512, 31 + N, B)).to(DEV)
+    with torch.no_grad():
+        _, (attn, pad) = ours(x, return_attn=True)
+    assert isinstance(attn, AttentionMap)
+    n = attn.shape[-1]
+    assert attn.shape == (B, 8, n, n) and (n - pad) % 1 == 0
+    rows = [(0, pad + 1), (0, pad), (B - 1, -1), (B - 1, n // 2)]
+    got = [attn[b, :, r, pad + 1:pad + 1 + N].clone() for b, r in rows]
+    full = attn.full()
+    for (b, r), g in zip(rows, got):
+        ref = full[b, :, r, pad + 1:pad + 1 + N]
+        assert g.shape == ref.shape
+        assert ((g - ref).abs().max() / ref.abs().max()).item() < tol, (b, r)
+    # after materialisation every index goes through the full tensor
+    assert torch.equal(attn[0, :, pad + 1], full[0, :, pad + 1])
+
+
+def test_nystrom_module_return_attn_is_an_attention_map():
+    from transmil_deepgraft_amd.nystrom_attention import NystromAttention, AttentionMap
+    torch.manual_seed(3)
+    m = NystromAttention(dim=512, dim_head=64, heads=8, num_landmarks=256, pinv_iterations=6,
+                         residual=True, dropout=0.7).to(DEV).eval()
+    x = torch.randn(1, 300, 512, device=DEV)
+    with torch.no_grad():
+        out, attn = m(x, return_attn=True)
+    assert isinstance(attn, AttentionMap) and attn.shape == (1, 8, 512, 512)
+    r = attn[0, :, 300, :]
+    full = attn.full()[0, :, 300, :]
+    assert ((r - full).abs().max() / full.abs().max()).item() < 1e-5
+    assert attn.sum().item() == attn.full().sum().item()  # tensor methods forward to the full product
+
+
 def test_train_mode_dropout_is_applied_and_reproducible():
     """The mask stream is a device-side counter (hipGraph-safe): restoring the
     counter reproduces the mask; every forward advances it; eval mode has none."""

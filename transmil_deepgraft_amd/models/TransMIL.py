@@ -26,7 +26,7 @@ import torch
 import torch.nn as nn
 
 from ..engine import TransMILEngine, NystromEngine
-from ..nystrom_attention import NystromAttention, attention_matrix
+from ..nystrom_attention import NystromAttention, AttentionMap
 from .. import ops
 
 
@@ -135,7 +135,7 @@ class TransMIL(nn.Module):
             c = holder["ctx"]
             S = c["geo"].S
             padding = 256 - S % 256 if S % 256 else 0      # :190-193
-            attn2 = attention_matrix(c["s2"]["qkv"], c["s2"]["core"], c["geo"].heads)
+            attn2 = AttentionMap(c["s2"]["qkv"], c["s2"]["core"], c["geo"].heads)
             return logits, (attn2, padding)
         return logits
 

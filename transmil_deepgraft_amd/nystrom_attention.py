@@ -13,17 +13,22 @@ Supported geometry on the HIP path: ``dim_head == 64``, ``num_landmarks ==
 call site).  Anything else raises ``NotImplementedError`` -- there is no CPU
 or eager-PyTorch fallback.
 
-``return_attn=True`` materialises ``attn1 @ attn2_inv @ attn3`` ([B, h, n, n],
-SURVEY.md App. A eq. 11) on the device from the saved factors; it is off the
-training hot path (the reference computes it on every call, 301 GF per layer at
-N = 8192, and never uses it for the loss).
+``return_attn=True`` returns an :class:`AttentionMap` -- ``attn1 @ attn2_inv @ attn3``
+([B, h, n, n], SURVEY.md App. A eq. 11) held as the forward's factors.  Indexing one
+row of it, ``attn[b, heads, r, cols]`` (the only access the reference's consumers
+make, code/visualize_mil.py:580-581), runs the ``tm_nys_attn_row`` kernel:
+O(h (m^2 + m n)) work and no n x n matrix.  Any other use materialises the full
+product once (on the device).  The reference computes that product on every call
+(301 GF per layer at N = 8192) and never uses it for the loss.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 
-from .engine import NystromEngine, NL, DH
+from . import _lib
+from ._lib import BF16, F32
+from .engine import NystromEngine, NL, DH, _p, _stream
 
 
 def _check_dtype(dtype):
@@ -97,7 +102,7 @@ class NystromAttention(nn.Module):
         engine = NystromEngine(torch.float32)
         _, c = engine.forward(x.float(), self.to_qkv.weight, self.to_out[0].weight, self.to_out[0].bias,
                               self.res_conv.weight, self.heads, 0.0, 0)
-        return attention_matrix(c["qkv"], c["core"], self.heads)
+        return AttentionMap(c["qkv"], c["core"], self.heads)
 
 
 @torch.no_grad()
@@ -109,3 +114,64 @@ def attention_matrix(qkv, core, heads):
     attn = (a1 @ core["z"]) @ a3
     n = attn.shape[-1]
     return attn.view(-1, heads, n, n)
+
+
+@torch.no_grad()
+def attention_row(qkv, core, heads, row):
+    """Row `row` of attn1 @ Z @ attn3 for every bag and head: [B, h, n] fp32 (HIP kernel)."""
+    q, k = qkv[0], qkv[1]
+    nbh, n = q.shape[0], q.shape[1]
+    if not -n <= row < n:
+        raise IndexError(f"attention row {row} out of range for n = {n}")
+    row %= n
+    out = torch.empty(nbh, n, device=q.device, dtype=torch.float32)
+    _lib.call("tm_nys_attn_row", BF16 if q.dtype == torch.bfloat16 else F32, _p(q), _p(k), _p(core["ql"]),
+              _p(core["kl"]), _p(core["z"]), _p(core["lse3"]), nbh, n, row, _p(out), _stream())
+    return out.view(-1, heads, n)
+
+
+class AttentionMap:
+    """The [B, h, n, n] ``return_attn`` product of one NystromAttention forward, kept as its
+    factors (q, k, landmarks, Z = pinv(attn2), attn3's log-sum-exp rows).
+
+    ``attn[b, heads, r, cols]`` with an integer row ``r`` computes that row only
+    (``tm_nys_attn_row``); every other index, attribute or tensor use materialises the full
+    product once (``attention_matrix``) and forwards to it."""
+
+    def __init__(self, qkv, core, heads):
+        self._qkv, self._core, self._heads = qkv, core, heads
+        nbh, n = qkv.shape[1], qkv.shape[2]
+        self.shape = torch.Size((nbh // heads, heads, n, n))
+        self.dtype = torch.float32
+        self.device = qkv.device
+        self.ndim = 4
+        self._full = None
+
+    def __len__(self):
+        return self.shape[0]
+
+    def size(self, dim=None):
+        return self.shape if dim is None else self.shape[dim]
+
+    def row(self, r):
+        """[B, h, n] row r of every bag and head."""
+        return attention_row(self._qkv, self._core, self._heads, int(r))
+
+    def full(self):
+        if self._full is None:
+            self._full = attention_matrix(self._qkv, self._core, self._heads)
+        return self._full
+
+    def __getitem__(self, key):
+        if isinstance(key, tuple) and len(key) == 4 and isinstance(key[2], int) and self._full is None:
+            return self.row(key[2])[key[0], key[1], key[3]]
+        return self.full()[key]
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return getattr(self.full(), name)
+
+    def __array__(self, dtype=None):
+        a = self.full().cpu().numpy()
+        return a if dtype is None else a.astype(dtype)
