@@ -212,6 +212,51 @@ def test_nystrom_module_return_attn_is_an_attention_map():
     assert attn.sum().item() == attn.full().sum().item()  # tensor methods forward to the full product
 
 
+def _hook_norms(model, acts, grads):
+    def fwd_hook(name):
+        def h(_m, _inp, out):
+            acts[name] = out.detach().cpu().double()
+            out.register_hook(lambda g: grads.__setitem__(name, g.detach().cpu().double()))
+        return h
+    return [model.norm.register_forward_hook(fwd_hook("norm")),
+            model.layer1.norm.register_forward_hook(fwd_hook("layer1.norm")),
+            model.layer2.norm.register_forward_hook(fwd_hook("layer2.norm"))]
+
+
+def test_norm_hooks_fire_and_match_the_oracle():
+    """GradCAM hooks model.norm / layer{1,2}.norm (code/visualize_mil.py:225-234): with a
+    hook registered the model runs module by module on the HIP ops; the hooked activations
+    and the gradients flowing into them match the oracle's (fp32 parity mode), and logits
+    and parameter gradients match the fused path."""
+    ref, ours = _pair(2)
+    x = torch.from_numpy(bag_input(300, 512, 41))
+    lf, gf = _ours_forward_backward(ours, x, 1, 2)          # fused path, no hooks
+    ours.zero_grad(set_to_none=True)
+    acts, grads, racts, rgrads = {}, {}, {}, {}
+    handles = _hook_norms(ours, acts, grads)
+    try:
+        assert ours._hooked()
+        lh, gh = _ours_forward_backward(ours, x, 1, 2)
+    finally:
+        for hd in handles:
+            hd.remove()
+    assert not ours._hooked()
+    rh = _hook_norms(ref, racts, rgrads)
+    try:
+        _ref_forward_backward(ref, x, 1, 2)
+    finally:
+        for hd in rh:
+            hd.remove()
+    np.testing.assert_allclose(lh.numpy(), lf.numpy(), rtol=0, atol=1e-5)
+    for name in gf:
+        assert ((gh[name].double() - gf[name].double()).abs().max()
+                / gf[name].double().abs().max().clamp_min(1e-12)).item() < 2e-3, name
+    for name in ("norm", "layer1.norm", "layer2.norm"):
+        assert acts[name].shape == racts[name].shape == (1, 18 * 18 + 1, 512), name
+        assert (acts[name] - racts[name]).abs().max().item() < 1e-4, name
+        assert ((grads[name] - rgrads[name]).abs().max() / rgrads[name].abs().max()).item() < 2e-3, name
+
+
 def test_train_mode_dropout_is_applied_and_reproducible():
     """The mask stream is a device-side counter (hipGraph-safe): restoring the
     counter reproduces the mask; every forward advances it; eval mode has none."""

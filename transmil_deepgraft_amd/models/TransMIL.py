@@ -35,13 +35,13 @@ class TransLayer(nn.Module):
 
     def __init__(self, norm_layer=nn.LayerNorm, dim=512):
         super().__init__()
-        self.norm = norm_layer(dim)
+        self.norm = (ops.LayerNorm if norm_layer is nn.LayerNorm else norm_layer)(dim)
         heads = 8
         self.attn = NystromAttention(dim=dim, dim_head=dim // heads, heads=heads, num_landmarks=dim // 2,
                                      pinv_iterations=6, residual=True, dropout=0.7)
 
     def forward(self, x):
-        out, attn = self.attn(ops.layer_norm(self.norm, x), return_attn=True)
+        out, attn = self.attn(self.norm(x), return_attn=True)   # module calls: hooks fire
         return x + out, attn
 
 
@@ -80,7 +80,7 @@ class _TransMILFn(torch.autograd.Function):
 class TransMIL(nn.Module):
     def __init__(self, n_classes, in_features, out_features=512):
         super().__init__()
-        norm_layer = nn.LayerNorm
+        norm_layer = ops.LayerNorm     # nn.LayerNorm parameters, HIP forward (hookable)
         self.pos_layer = PPEG(dim=out_features)
         if in_features in (2048, 1024, 768):
             self._fc1 = _reference_fc1(in_features, out_features, norm_layer)
@@ -98,6 +98,39 @@ class TransMIL(nn.Module):
         # (hipGraph-safe); seeded from torch's generator so torch.manual_seed pins it
         self.register_buffer("_dropout_counter", torch.randint(0, 2 ** 62, (1,), dtype=torch.int64),
                              persistent=False)
+
+    # False: always run module by module (what a hook on a submodule switches to by itself)
+    fused = True
+
+    def _hooked(self):
+        """A forward / backward hook on any submodule (GradCAM on model.norm or
+        model.layer{1,2}.norm, code/visualize_mil.py:225-234) needs the module-by-module path."""
+        g = torch.nn.modules.module
+        if any(getattr(g, n, None) for n in ("_global_forward_hooks", "_global_forward_pre_hooks",
+                                              "_global_backward_hooks", "_global_backward_pre_hooks")):
+            return True
+        for m in self.modules():
+            if m is not self and (m._forward_hooks or m._forward_pre_hooks or m._backward_hooks
+                                  or getattr(m, "_backward_pre_hooks", None)):
+                return True
+        return False
+
+    def _forward_modules(self, x, return_attn):
+        """code/models/TransMIL.py:175-211 as module calls on the HIP ops, so hooks on
+        ``norm``, ``layer{1,2}.norm``, ``layer{1,2}``, ``pos_layer`` ... fire: _fc1 + pad +
+        class token, layer1, PPEG, layer2, norm (all S tokens), _fc on the class token."""
+        B, N, _ = x.shape
+        G = int(math.ceil(math.sqrt(N)))
+        h = ops.embed(self._fc1, self.cls_token, x)    # :175-186
+        h, _ = self.layer1(h)                           # :196
+        h = self.pos_layer(h, G, G)                     # :198
+        h, attn = self.layer2(h)                        # :199
+        h = self.norm(h)[:, 0]                          # :202-203
+        logits = ops.linear(self._fc, h)                # :204
+        if return_attn:
+            S = G * G + 1
+            return logits, (attn, 256 - S % 256 if S % 256 else 0)
+        return logits
 
     def set_compute_dtype(self, dtype):
         """torch.bfloat16 (bench) or torch.float32 (parity); propagates to submodules."""
@@ -121,6 +154,8 @@ class TransMIL(nn.Module):
                 f"in_features={self.in_features}: only the Linear+GELU _fc1 branch "
                 "(code/models/TransMIL.py:128-133) runs on the HIP path")
         x = x.float().contiguous()             # :174
+        if not self.fused or self._hooked():
+            return self._forward_modules(x, return_attn)
         names = tuple(n for n, _ in self.named_parameters())
         params = tuple(p for _, p in self.named_parameters())
         drop_p = self.layer1.attn.to_out[1].p if self.training else 0.0

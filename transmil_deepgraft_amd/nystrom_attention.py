@@ -39,15 +39,17 @@ def _check_dtype(dtype):
 
 class _NystromFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine, heads, drop_p, seed_dev, x, wqkv, wo, bo, wconv):
+    def forward(ctx, engine, heads, drop_p, seed_dev, holder, x, wqkv, wo, bo, wconv):
         out, c = engine.forward(x, wqkv, wo, bo, wconv, heads, drop_p, 0x51ED27, seed_dev)
         ctx.engine, ctx.c = engine, c
+        if holder is not None:
+            holder["c"] = c
         return out
 
     @staticmethod
     def backward(ctx, dout):
         dx, dwqkv, dwo, dbo, dwconv = ctx.engine.backward(dout, ctx.c)
-        return None, None, None, None, dx, dwqkv, dwo, dbo, dwconv
+        return None, None, None, None, None, dx, dwqkv, dwo, dbo, dwconv
 
 
 class NystromAttention(nn.Module):
@@ -91,18 +93,12 @@ class NystromAttention(nn.Module):
         if drop_p > 0:
             self._dropout_counter.add_(1)
             seed_dev = self._dropout_counter.clone()
-        out = _NystromFn.apply(engine, self.heads, drop_p, seed_dev, x.float(), self.to_qkv.weight,
+        holder = {} if return_attn else None
+        out = _NystromFn.apply(engine, self.heads, drop_p, seed_dev, holder, x.float(), self.to_qkv.weight,
                                self.to_out[0].weight, self.to_out[0].bias, self.res_conv.weight)
-        if return_attn:
-            return out, self._attn_matrix(x)
+        if return_attn:   # the factors of THIS forward (the reference returns attn of the same call)
+            return out, AttentionMap(holder["c"]["qkv"], holder["c"]["core"], self.heads)
         return out
-
-    @torch.no_grad()
-    def _attn_matrix(self, x):
-        engine = NystromEngine(torch.float32)
-        _, c = engine.forward(x.float(), self.to_qkv.weight, self.to_out[0].weight, self.to_out[0].bias,
-                              self.res_conv.weight, self.heads, 0.0, 0)
-        return AttentionMap(c["qkv"], c["core"], self.heads)
 
 
 @torch.no_grad()

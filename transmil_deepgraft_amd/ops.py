@@ -1,9 +1,11 @@
 """Standalone (unfused) HIP ops behind the drop-in submodules.
 
-``TransMIL.forward`` never uses these -- it runs the fused engine.  They back
-``TransLayer.forward`` / ``PPEG.forward`` when a caller drives a submodule on
-its own (e.g. the reference's GradCAM / attention visualisation scripts hook
-``model.layer1.norm``, code/visualize_mil.py:225-234).
+``TransMIL.forward`` uses the fused engine unless a hook is registered on one of its
+submodules.  These ops back the module-by-module path it then takes (and
+``TransLayer.forward`` / ``PPEG.forward`` / the norms when a caller drives a submodule
+on its own): the reference's GradCAM / attention visualisation hooks ``model.norm`` and
+``model.layer{1,2}.norm`` (code/visualize_mil.py:225-234, test_visualize.py:122,127).
+fp32 operands throughout (a visualisation / analysis path, not the benchmark step).
 """
 from __future__ import annotations
 
@@ -11,9 +13,11 @@ import ctypes as C
 
 import torch
 
+import torch.nn as nn
+
 from . import _lib
 from ._lib import F32
-from .engine import _p, _stream, LN_EPS
+from .engine import Geometry, Pool, _p, _stream, LN_EPS, colsum, gemm, weight_grad
 
 
 class _LayerNormFn(torch.autograd.Function):
@@ -89,3 +93,101 @@ def ppeg(module, x, G):
         raise ValueError(f"PPEG expects 1 + G*G tokens, got {x.shape[1]} for G={G}")
     return _PPEGFn.apply(x.float(), G, module.proj.weight, module.proj.bias, module.proj1.weight,
                          module.proj1.bias, module.proj2.weight, module.proj2.bias)
+
+
+class LayerNorm(nn.LayerNorm):
+    """``nn.LayerNorm`` (same parameters and state_dict keys) whose forward is the HIP
+    kernel, so forward / backward hooks registered on it fire."""
+
+    def forward(self, x):
+        return layer_norm(self, x)
+
+
+class _EmbedFn(torch.autograd.Function):
+    """_fc1 (Linear + GELU), grid pad (repeat the first G*G - N tokens) and the class token
+    (code/models/TransMIL.py:175-186): x [B, N, F] -> H [B, S, D] fp32 on the GEMM epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cls):
+        B, N, F = x.shape
+        D = w.shape[0]
+        geo = Geometry(B, N, F, D, 8)
+        x2 = x.reshape(B * N, F).contiguous()
+        H = torch.empty(B * geo.S, D, device=x.device)
+        pre = torch.empty(B * N, D, device=x.device)
+        gemm(x2, w.contiguous(), H, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=F32, c_dtype=F32, bias=b, gelu=True,
+             pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
+        _lib.call("tm_put_cls", _p(cls.contiguous()), B, geo.S, D, _p(H), _stream())
+        ctx.save_for_backward(x2, w, pre)
+        ctx.geo = geo
+        return H.view(B, geo.S, D)
+
+    @staticmethod
+    def backward(ctx, dH):
+        x2, w, pre = ctx.saved_tensors
+        geo = ctx.geo
+        B, N, F, D, S = geo.B, geo.N, geo.F, w.shape[0], geo.S
+        pool = Pool(dH.device)
+        dpre = torch.empty(B * N, D, device=dH.device)
+        dcls = torch.empty(1, 1, D, device=dH.device)
+        _lib.call("tm_fc1_gelu_bwd", F32, _p(dH.float().contiguous()), _p(pre), B, N, S, geo.add, D, _p(dpre),
+                  _p(dcls), _stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(B * N, F, device=dH.device)
+            gemm(dpre, w.contiguous(), dx, B * N, F, D, lda=D, ldb=F, ldc=F, b_kn=1, dtype=F32, c_dtype=F32)
+            dx = dx.view(B, N, F)
+        dw = torch.empty(D, F, device=dH.device)
+        weight_grad(dpre, x2, dw, D, F, B * N, ldy=D, ldx=F, dtype=F32, work_pool=pool)
+        db = torch.empty(D, device=dH.device)
+        colsum(dpre, B * N, D, D, F32, db, pool)
+        return dx, dw, db, dcls
+
+
+def embed(fc1, cls_token, x):
+    """``_fc1`` = Sequential(Linear, GELU) + grid pad + class token on the HIP GEMM."""
+    if not x.is_cuda:
+        raise RuntimeError("HIP _fc1 needs a GPU tensor")
+    lin = fc1[0]
+    return _EmbedFn.apply(x.float(), lin.weight, lin.bias, cls_token)
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b (fp32) on the HIP GEMM; backward dX = dY W, dW = dY^T X, db = colsum dY."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        M, K = x.shape
+        Nout = w.shape[0]
+        xc = x.contiguous()
+        y = torch.empty(M, Nout, device=x.device)
+        gemm(xc, w.contiguous(), y, M, Nout, K, lda=K, ldb=K, ldc=Nout, dtype=F32, c_dtype=F32, bias=b)
+        ctx.save_for_backward(xc, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        M, K = x.shape
+        Nout = w.shape[0]
+        pool = Pool(dy.device)
+        # the GEMM wants 16-B leading dimensions: pad the output features (n_classes) to 4
+        Np = (Nout + 3) // 4 * 4
+        dyp = torch.zeros(M, Np, device=dy.device)
+        dyp[:, :Nout] = dy
+        wp = torch.zeros(Np, K, device=dy.device)
+        wp[:Nout] = w
+        dx = torch.empty(M, K, device=dy.device)
+        gemm(dyp, wp, dx, M, K, Np, lda=Np, ldb=K, ldc=K, b_kn=1, dtype=F32, c_dtype=F32)
+        dw = torch.empty(Np, K, device=dy.device)
+        weight_grad(dyp, x, dw, Np, K, M, ldy=Np, ldx=K, dtype=F32, work_pool=pool)
+        db = torch.empty(Np, device=dy.device)
+        colsum(dyp, M, Np, Np, F32, db, pool)
+        return dx, dw[:Nout], db[:Nout]
+
+
+def linear(module, x):
+    """``nn.Linear`` forward on the HIP GEMM (x [M, K] fp32)."""
+    if not x.is_cuda:
+        raise RuntimeError("HIP Linear needs a GPU tensor")
+    return _LinearFn.apply(x.float(), module.weight, module.bias)
