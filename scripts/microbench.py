@@ -275,6 +275,36 @@ def main():
     case("attn_row (return_attn row)", lambda: _lib.call("tm_nys_attn_row", BF16, E._p(q), E._p(k), E._p(ql), E._p(kl),
                                                          E._p(zz), E._p(lse3), nbh, n, 167, E._p(arow), st()),
          2 * nbh * n * 256 * 64)
+    if args.only == "overlap":
+        # pinv backward chain beside the A3 backward on a second stream (fork / join in one graph)
+        saved8 = torch.empty(_lib.query("tm_pinv_saved_floats", nbh, 6), device=dev)
+        X8 = torch.softmax(torch.randn(nbh, 256, 256, device=dev), -1)
+        _lib.call("tm_pinv_fwd", E._p(X8), nbh, 6, 1, E._p(saved8), st())
+        pw = torch.empty(_lib.query("tm_pinv_bwd_workspace_floats", nbh), device=dev)
+        dz8 = torch.randn(nbh, 256, 256, device=dev) * 1e-3
+        dX8 = torch.empty(nbh, 256, 256, device=dev)
+        side = torch.cuda.Stream()
+
+        def chain():
+            _lib.call("tm_pinv_bwd", E._p(X8), nbh, 6, 1, E._p(saved8), E._p(dz8), E._p(pw), E._p(dX8), st())
+
+        def a3():
+            _lib.call("tm_nys_a3_bwd", BF16, E._p(ql_t), E._p(dw_t), E._p(k), E._p(v), E._p(lse3), E._p(d3), nbh, 8,
+                      n, E._p(dk), E._p(dv), E._p(a3bw), E._p(dql), 1, st())
+
+        def both():
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                a3()
+            chain()
+            torch.cuda.current_stream().wait_stream(side)
+
+        args.only = ""
+        case("overlap: pinv_bwd alone", chain)
+        case("overlap: a3_bwd alone", a3)
+        case("overlap: serial", lambda: (chain(), a3()))
+        case("overlap: a3_bwd on a side stream", both)
+        return
     # ---------------- PPEG ----------------
     x = torch.randn(1, S, 512, device=dev)
     wf = torch.randn(512 * 49, device=dev) * 0.1
