@@ -139,6 +139,9 @@ typedef struct tm_bmm_job {
   float alpha, diag;
   float* C; int ldc; long long sc;
   int M, N, K;
+  /* optional second output of the same product (C's layout): C2 = c2_alpha*(products)
+   * + c2_diag*I + c2_e1*E1 (null: none) */
+  float* C2; float c2_alpha, c2_diag, c2_e1;
 } tm_bmm_job;
 /* prec 0: exact fp32 MFMA; prec 1: bf16x3 (hi/lo split, ~16-bit operands, fp32 accumulate) */
 int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream);

@@ -284,7 +284,9 @@ def test_pinv_persistent_chain_matches_per_launch_chain(nbh, prec):
         outs.append((saved[:7 * nbh * 65536].clone(), dX.clone()))
     (sa, da), (sb, db) = outs
     assert torch.isfinite(sa).all() and torch.isfinite(da).all()
-    tol = 1e-5 if prec == 0 else 5e-5  # bf16x3: the split roundings differ with the summation order
+    # the two chains associate the products differently (the per-launch forward carries P by
+    # its recurrence); bf16x3's hi/lo split roundings follow the summation order
+    tol = 2e-5 if prec == 0 else 2e-4
     assert _rel(sa.cpu(), sb.cpu()) < tol
     assert _rel(da.cpu(), db.cpu()) < 10 * tol
 

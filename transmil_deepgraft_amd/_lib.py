@@ -37,7 +37,8 @@ class BmmJob(C.Structure):
     _fields_ = [("A", P), ("B", P), ("ta", I), ("tb", I), ("lda", I), ("ldb", I), ("sa", L), ("sb", L),
                 ("A2", P), ("B2", P), ("ta2", I), ("tb2", I), ("lda2", I), ("ldb2", I), ("sa2", L), ("sb2", L),
                 ("E1", P), ("e1", Fl), ("E2", P), ("e2", Fl), ("alpha", Fl), ("diag", Fl),
-                ("C", P), ("ldc", I), ("sc", L), ("M", I), ("N", I), ("K", I)]
+                ("C", P), ("ldc", I), ("sc", L), ("M", I), ("N", I), ("K", I),
+                ("C2", P), ("c2_alpha", Fl), ("c2_diag", Fl), ("c2_e1", Fl)]
 
 
 OPTIM_MAX_TENSORS = 40
