@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=8192, help="patches per bag")
     ap.add_argument("--classes", type=int, default=2)
+    ap.add_argument("--features", type=int, default=512, choices=[512, 2048],
+                    help="in_features: 512 (Linear+GELU _fc1, the metric's config) or 2048 (the RCC "
+                         "_fc1 branch on RetCCL-width features, config C5 without its encoder)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--probe", default="a1_fwd", help="call site timed for the roofline object")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -91,7 +94,7 @@ def measured_traffic(site, n_patches, dtype):
     return rec.get("traffic_bytes")
 
 
-def cpu_baseline(n_patches, ncls, steps):
+def cpu_baseline(n_patches, ncls, steps, feat=512):
     """fp32 CPU oracle, logits path (no unused n'xn' attention product), timed on this host."""
     from oracle.transmil_ref import TransMIL as RefTransMIL, TransLayer
     threads = min(16, os.cpu_count() or 1)
@@ -139,14 +142,14 @@ def main():
     from transmil_deepgraft_amd import engine
 
     torch.manual_seed(1234)  # same random-init weights on every rank
-    model = TransMIL(args.classes, 512, 512).to(dev).train()
+    model = TransMIL(args.classes, args.features, 512).to(dev).train()
     model.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     task = TransMILTask(model)
     opt = task.configure_optimizers()[0][0]
     allreduce = GradAllReduce(model.parameters())
 
     g = torch.Generator(device=dev).manual_seed(2021 + rank)
-    bags = [torch.rand(1, args.n, 512, device=dev, generator=g) for _ in range(4)]
+    bags = [torch.rand(1, args.n, args.features, device=dev, generator=g) for _ in range(4)]
     labels = [torch.randint(0, args.classes, (1,), device=dev, generator=g) for _ in range(4)]
     static_x = torch.empty_like(bags[0])
     static_y = torch.empty_like(labels[0])
@@ -270,7 +273,8 @@ def main():
         roof.update(kernel=args.probe, kernel_ms=round(kernel_ms, 5), launches=len(kernel_ms_samples),
                     algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])
         out = {
-            "metric": "slides/sec (fwd+bwd) at N=8192 patches, d=512",
+            "metric": "slides/sec (fwd+bwd) at N=8192 patches, d=512" if args.features == 512 else
+                      f"slides/sec (fwd+bwd) at N={args.n} patches, in_features={args.features}",
             "value": round(slides / elapsed, 3),
             "unit": "slides/sec",
             "n_gpus": world,
@@ -282,7 +286,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (torch.rand bags resident in HBM, random-init weights)",
-            "config": {"workload": f"TransMIL_feat {args.classes}-class, 1 bag N={args.n}x512 per GPU, "
+            "config": {"workload": f"TransMIL_feat {args.classes}-class, 1 bag N={args.n}x{args.features} per GPU, "
                                    "train step fwd+CE+bwd+allreduce+Lookahead(RAdam)",
                        "execution": "eager" if args.eager else "hipGraph replay of the whole step",
                        "global_batch": world, "seq_len": args.n, "parallelism": f"dp{world}"},

@@ -173,6 +173,9 @@ int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int 
 int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, int pad, int D, void* y, void* stream);
 int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
                     void* dpre, float* dcls, void* stream);
+/* dpre = dy * GELU'(pre) elementwise (fp32 dy / pre, dpre in dtype): the backward of the inner
+ * Linear + GELU of the in_features = 2048 _fc1 branch (code/models/TransMIL.py:100-111) */
+int tm_gelu_bwd(int dtype, const float* dy, const float* pre, long long count, void* dpre, void* stream);
 
 /* fp32 -> dtype copies of up to 8 tensors (per-step bf16 GEMM weight operands) in one launch;
  * offset[] = prefix sums of the element counts, offset[0] = 0 */

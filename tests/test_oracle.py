@@ -108,3 +108,43 @@ def test_pinv_global_max_couples_bags():
     joint = moore_penrose_iter_pinv(torch.cat([a, b]), 6)
     alone = moore_penrose_iter_pinv(a, 6)
     assert (joint[0] - alone[0]).abs().max() > 1e-6
+
+
+def _branch_oracle(name, dtype):
+    from oracle.transmil_ref import TransMIL, deterministic_params_
+    from oracle.mdmil_ref import MDMIL
+    meta = index()[name]
+    torch.manual_seed(0)
+    m = MDMIL(2) if meta["model"] == "MDMIL" else TransMIL(2, meta["feat"], 512)
+    deterministic_params_(m, 2021)
+    x = torch.from_numpy(bag_input(meta["n"], meta["feat"], 2021 + 1000 + meta["n"]))
+    return m.to(dtype).eval(), x.to(dtype), meta
+
+
+@pytest.mark.parametrize("name", ["fc2048_n300", "mdmil_n300"])
+def test_oracle_branches_match_reference_fixture(name):
+    """The in_features=2048 TransMIL branch (code/models/TransMIL.py:100-111) and MDMIL
+    (code/models/MDMIL.py:60-114) in the oracle against the reference's own outputs
+    (tests/golden/make_golden_branches.py): fp32 logits 1e-6, fp64 logits / loss / small
+    gradients 1e-10."""
+    fx = load(name)
+    for dt, tag, tol in ((torch.float32, "", 1e-6), (torch.float64, ".f64", 1e-10)):
+        m, x, meta = _branch_oracle(name, dt)
+        orig = torch.Tensor.float
+        if dt == torch.float64:
+            torch.Tensor.float = lambda self, *a, **k: self
+        try:
+            out = m(x)
+        finally:
+            torch.Tensor.float = orig
+        logits = out[0] if isinstance(out, tuple) else out
+        loss = torch.nn.CrossEntropyLoss()(logits, torch.nn.functional.one_hot(
+            torch.tensor([meta["label"]]), 2).to(dt))
+        loss.backward()
+        np.testing.assert_allclose(logits.detach().numpy(), fx["logits" + tag], rtol=0, atol=tol)
+        np.testing.assert_allclose(loss.detach().numpy().reshape(1), fx["loss" + tag], rtol=0, atol=tol)
+        grads = dict(m.named_parameters())
+        for k in fx:
+            if k.startswith("grad.") and k.endswith(tag) and (tag or not k.endswith(".f64")):
+                pname = k[5:len(k) - len(tag)] if tag else k[5:]
+                np.testing.assert_allclose(grads[pname].grad.numpy(), fx[k], rtol=0, atol=tol * 10)

@@ -337,3 +337,85 @@ def test_train_mode_dropout_matches_oracle_with_same_mask():
         if err > 2e-3:
             bad.append((name, err))
     assert not bad, bad
+
+
+def _branch_pair(name, dtype):
+    """(oracle fp64, ours) for the in_features=2048 TransMIL branch or MDMIL with the
+    deterministic weights of tests/golden/make_golden_branches.py."""
+    from golden_util import index
+    from oracle.transmil_ref import TransMIL as Ref, deterministic_params_
+    from oracle.mdmil_ref import MDMIL as RefMD
+    from transmil_deepgraft_amd.models import TransMIL, MDMIL
+    meta = index()[name]
+    torch.manual_seed(0)
+    if meta["model"] == "MDMIL":
+        ref, ours = RefMD(2), MDMIL(2)
+    else:
+        ref, ours = Ref(2, meta["feat"], 512), TransMIL(2, meta["feat"], 512)
+    deterministic_params_(ref, 2021)
+    ref = ref.double().eval()
+    ours = ours.to(DEV).eval()
+    ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    ours.set_compute_dtype(dtype)
+    x = torch.from_numpy(bag_input(meta["n"], meta["feat"], 2021 + 1000 + meta["n"]))
+    return ref, ours, x, meta
+
+
+def _logits_of(out):
+    return out[0] if isinstance(out, tuple) else out
+
+
+@pytest.mark.parametrize("hooked", [False, True])
+@pytest.mark.parametrize("name", ["fc2048_n300", "mdmil_n300"])
+def test_branch_models_fp32_logits_and_grads(name, hooked):
+    """TransMIL(in_features=2048) (RCC _fc1: Linear+GELU+LayerNorm(1024)+Linear+GELU,
+    code/models/TransMIL.py:100-111) and MDMIL (code/models/MDMIL.py:60-114) on the fused
+    engine (and, ``hooked``, on the module-by-module path a hook on ``model.norm`` selects):
+    fp32 logits within 1e-4 of the reference's fp64 fixture, the small gradients against the
+    fixture and every gradient within 2e-3 (relative max) of the fp64 oracle."""
+    fx = load(name)
+    ref, ours, x, meta = _branch_pair(name, torch.float32)
+    handle = ours.norm.register_forward_hook(lambda m, i, o: None) if hooked else None
+    out = ours(x.float().to(DEV))
+    if name.startswith("mdmil"):
+        assert isinstance(out, tuple) and len(out) == 2      # (logits, attn2), MDMIL.py:114
+    lo = _logits_of(out)
+    loss = torch.nn.CrossEntropyLoss()(lo, torch.nn.functional.one_hot(
+        torch.tensor([meta["label"]], device=DEV), 2).float())
+    loss.backward()
+    torch.cuda.synchronize()
+    if handle is not None:
+        handle.remove()
+    np.testing.assert_allclose(lo.detach().cpu().numpy(), fx["logits.f64"], rtol=0, atol=1e-4)
+    assert (lo.detach().cpu().numpy().argmax(1) == fx["logits"].argmax(1)).all()
+    go = {n: p.grad.detach().cpu().double() for n, p in ours.named_parameters()}
+    for k in fx:
+        if k.startswith("grad.") and k.endswith(".f64"):
+            g = torch.from_numpy(fx[k])
+            err = ((go[k[5:-4]] - g).abs().max() / g.abs().max().clamp_min(1e-12)).item()
+            assert err < 2e-3, (k, err)
+    lr = _logits_of(_ref64(ref, x))
+    torch.nn.CrossEntropyLoss()(lr, torch.nn.functional.one_hot(torch.tensor([meta["label"]]), 2).double()).backward()
+    bad = []
+    for n, p in ref.named_parameters():
+        err = ((go[n] - p.grad).abs().max() / p.grad.abs().max().clamp_min(1e-12)).item()
+        if err > 2e-3:
+            bad.append((n, err))
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("name", ["fc2048_n300", "mdmil_n300"])
+def test_branch_models_bf16_close_to_reference(name):
+    """bf16 (bench) mode of the same two models: logits within 5e-2 of the reference fixture,
+    one train-mode backward with every gradient finite and nonzero."""
+    fx = load(name)
+    _, ours, x, meta = _branch_pair(name, torch.bfloat16)
+    with torch.no_grad():
+        lo = _logits_of(ours(x.to(DEV))).cpu().numpy()
+    np.testing.assert_allclose(lo, fx["logits.f64"], rtol=0, atol=5e-2)
+    ours.train()
+    loss = torch.nn.CrossEntropyLoss()(_logits_of(ours(x.to(DEV))), torch.nn.functional.one_hot(
+        torch.tensor([1], device=DEV), 2).float())
+    loss.backward()
+    for n, p in ours.named_parameters():
+        assert torch.isfinite(p.grad).all() and p.grad.abs().max() > 0, n

@@ -62,6 +62,24 @@ __global__ void fc1_gelu_bwd_kernel(const float* __restrict__ dH, const float* _
   }
 }
 
+// dpre[i] = dy[i] * gelu'(pre[i]) over a flat [rows, D] block (the Linear+GELU stages of the
+// _fc1 branches other than the last, code/models/TransMIL.py:100-111); 4 elements per lane
+template <typename T>
+__global__ void gelu_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ pre, size_t count,
+                                T* __restrict__ dpre) {
+  const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= count) {
+    const float4 g = *(const float4*)(dy + i);
+    const float4 x = *(const float4*)(pre + i);
+    dpre[i] = from_f<T>(g.x * gelu_erf_grad(x.x));
+    dpre[i + 1] = from_f<T>(g.y * gelu_erf_grad(x.y));
+    dpre[i + 2] = from_f<T>(g.z * gelu_erf_grad(x.z));
+    dpre[i + 3] = from_f<T>(g.w * gelu_erf_grad(x.w));
+  } else {
+    for (size_t j = i; j < count; ++j) dpre[j] = from_f<T>(dy[j] * gelu_erf_grad(pre[j]));
+  }
+}
+
 // y[b][pad + i][c] = x[b*S + i][c] (cast to T), y[b][0..pad)[c] = 0; grid (n_pad, B)
 template <typename T>
 __global__ void pad_rows_kernel(const float* __restrict__ x, int S, int n_pad, int pad, int D, T* __restrict__ y) {
@@ -119,6 +137,18 @@ extern "C" int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int
                                                                                (T*)dpre)));
   TM_CHECK_LAUNCH();
   cls_grad_kernel<<<1, 256, 0, st>>>(dH, B, S, D, dcls);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_gelu_bwd(int dtype, const float* dy, const float* pre, long long count, void* dpre,
+                           void* stream) {
+  TM_REQUIRE(dy && pre && dpre && count >= 0, "gelu_bwd: bad args");
+  TM_REQUIRE(((uintptr_t)dy % 16) == 0 && ((uintptr_t)pre % 16) == 0, "gelu_bwd: dy / pre must be 16-B aligned");
+  if (count == 0) return 0;
+  const unsigned blocks = (unsigned)(((count + 3) / 4 + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  TM_DTYPE_DISPATCH(dtype, (gelu_bwd_kernel<T><<<blocks, 256, 0, st>>>(dy, pre, (size_t)count, (T*)dpre)));
   TM_CHECK_LAUNCH();
   return 0;
 }

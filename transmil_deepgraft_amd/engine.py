@@ -352,15 +352,27 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
 
 
 # ----------------------------------------------------------------------------- whole model
-class TransMILEngine:
-    """Fused TransMIL forward / backward for the ``in_features -> Linear+GELU`` branch
-    (code/models/TransMIL.py:128-133), heads = 8, dim_head = 64, 256 landmarks."""
+# _fc1 layouts the fused engine runs: the parameter prefix of the Linear whose GELU output is
+# grid-padded (``main``) and the optional Linear + GELU + LayerNorm stage before it (``inner``)
+FC1_PLAIN = {"main": "_fc1.0", "inner": None}                                  # TransMIL.py:128-133
+FC1_RCC2048 = {"main": "_fc1.3", "inner": ("_fc1.0", "_fc1.2")}               # TransMIL.py:100-111
 
-    def __init__(self, dtype: torch.dtype = torch.bfloat16):
+
+class TransMILEngine:
+    """Fused TransMIL forward / backward, heads = 8, dim_head = 64, 256 landmarks.
+
+    ``fc1``: FC1_PLAIN (``in_features -> Linear+GELU``, code/models/TransMIL.py:128-133) or
+    FC1_RCC2048 (``Linear(2048,1024)+GELU+LayerNorm(1024)+Linear(1024,512)+GELU``, :100-111).
+    ``head``: parameter prefix of the class-token Linear (``_fc`` in TransMIL :155, ``_fc2`` in
+    code/models/MDMIL.py:73)."""
+
+    def __init__(self, dtype: torch.dtype = torch.bfloat16, fc1=None, head="_fc"):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("compute dtype must be torch.bfloat16 or torch.float32")
         self.tdtype = dtype
         self.dt_code = BF16 if dtype == torch.bfloat16 else F32
+        self.fc1 = FC1_PLAIN if fc1 is None else fc1
+        self.head = head
         _lib.lib()
 
     def _cast(self, w, pool):
@@ -392,11 +404,18 @@ class TransMILEngine:
         """fp32 master parameters -> the per-call operand set (T copies of GEMM weights)."""
         D = params["norm.weight"].shape[0]
         p = {"D": D}
-        w1, wqkv1, wo1, wqkv2, wo2 = self._cast_many(
-            [params["_fc1.0.weight"], params["layer1.attn.to_qkv.weight"], params["layer1.attn.to_out.0.weight"],
-             params["layer2.attn.to_qkv.weight"], params["layer2.attn.to_out.0.weight"]], pool)
+        main, inner = self.fc1["main"], self.fc1["inner"]
+        ws = [params[main + ".weight"], params["layer1.attn.to_qkv.weight"], params["layer1.attn.to_out.0.weight"],
+              params["layer2.attn.to_qkv.weight"], params["layer2.attn.to_out.0.weight"]]
+        if inner is not None:
+            ws.append(params[inner[0] + ".weight"])
+        ws = self._cast_many(ws, pool)
+        w1, wqkv1, wo1, wqkv2, wo2 = ws[:5]
         p["w1"] = w1
-        p["b1"] = params["_fc1.0.bias"]
+        p["b1"] = params[main + ".bias"]
+        if inner is not None:
+            p["w0"], p["b0"] = ws[5], params[inner[0] + ".bias"]
+            p["ln0_w"], p["ln0_b"] = params[inner[1] + ".weight"], params[inner[1] + ".bias"]
         p["cls"] = params["cls_token"]
         for li, (wqkv, wo) in ((1, (wqkv1, wo1)), (2, (wqkv2, wo2))):
             pre = f"layer{li}."
@@ -415,7 +434,7 @@ class TransMILEngine:
                   _p(bfold), _stream())
         p["wfold"], p["bfold"] = wfold, bfold
         p["norm_w"], p["norm_b"] = params["norm.weight"], params["norm.bias"]
-        p["fc_w"], p["fc_b"] = params["_fc.weight"], params["_fc.bias"]
+        p["fc_w"], p["fc_b"] = params[self.head + ".weight"], params[self.head + ".bias"]
         return p
 
     def forward(self, x, params, drop_p=0.0, seeds=(0x1F123BB5, 0x2A9F4C61), seed_dev=None):
@@ -435,6 +454,21 @@ class TransMILEngine:
         prm = self.prepare(params, pool)
         st = _stream()
         xt = self._cast(x.reshape(B * N, F), pool) if self.dt_code == BF16 else x.reshape(B * N, F).contiguous()
+        inner = None
+        if self.fc1["inner"] is not None:
+            # inner stage: y0 = GELU(x W0^T + b0) (fp32, pre-activation kept), then LayerNorm -> T,
+            # the operand of the main Linear (code/models/TransMIL.py:101-110)
+            Fm = prm["w0"].shape[0]
+            y0 = pool(B * N * Fm).view(B * N, Fm)
+            pre0 = pool(B * N * Fm).view(B * N, Fm)
+            gemm(xt, prm["w0"], y0, B * N, Fm, F, lda=F, ldb=F, ldc=Fm, dtype=self.dt_code, c_dtype=F32,
+                 bias=prm["b0"], gelu=True, pre=pre0, ld_pre=Fm)
+            xln = pool(B * N * Fm, self.tdtype).view(B * N, Fm)
+            mean0, rstd0 = pool(B * N), pool(B * N)
+            _lib.call("tm_layernorm_fwd", _p(y0), _p(prm["ln0_w"]), _p(prm["ln0_b"]), C.c_float(LN_EPS), B * N, Fm,
+                      N, N, 0, self.dt_code, _p(xln), _p(mean0), _p(rstd0), st)
+            inner = dict(xt=xt, y0=y0, pre0=pre0, mean0=mean0, rstd0=rstd0, F=F)
+            xt, F = xln, Fm
         # _fc1: Linear + GELU, grid pad (duplicate the first `add` rows) and class token
         H0 = pool(B * geo.S * D).view(B * geo.S, D)
         pre = pool(B * N * D).view(B * N, D)   # fp32 pre-activation for the GELU backward
@@ -451,7 +485,8 @@ class TransMILEngine:
         hrstd = pool(B)
         _lib.call("tm_head_fwd", _p(H3), B, geo.S, D, _p(prm["norm_w"]), _p(prm["norm_b"]), C.c_float(LN_EPS),
                   _p(prm["fc_w"]), _p(prm["fc_b"]), Ccls, _p(logits), _p(xhat), _p(hrstd), st)
-        ctx = dict(geo=geo, prm=prm, xt=xt, pre=pre, H0=H0, H1=H1, H2=H2, s1=s1, s2=s2, xhat=xhat, hrstd=hrstd)
+        ctx = dict(geo=geo, prm=prm, xt=xt, pre=pre, H0=H0, H1=H1, H2=H2, s1=s1, s2=s2, xhat=xhat, hrstd=hrstd,
+                   inner=inner)
         return logits, ctx
 
     def backward(self, dlogits, ctx, params):
@@ -465,7 +500,8 @@ class TransMILEngine:
         Ccls = prm["fc_w"].shape[0]
         dH = torch.zeros(B * S, D, dtype=torch.float32, device=dev)
         _lib.call("tm_head_bwd", _p(dlogits.contiguous()), B, Ccls, S, D, _p(ctx["xhat"]), _p(ctx["hrstd"]),
-                  _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g["_fc.weight"]), _p(g["_fc.bias"]),
+                  _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g[self.head + ".weight"]),
+                  _p(g[self.head + ".bias"]),
                   _p(g["norm.weight"]), _p(g["norm.bias"]), _p(dH), st)
         for li, Hin, saved in ((2, ctx["H2"], ctx["s2"]), (1, ctx["H0"], ctx["s1"])):
             pre = f"layer{li}."
@@ -486,9 +522,28 @@ class TransMILEngine:
         dpre = pool(B * N * D, self.tdtype).view(B * N, D)
         _lib.call("tm_fc1_gelu_bwd", self.dt_code, _p(dH), _p(ctx["pre"]), B, N, S, geo.add, D, _p(dpre),
                   _p(g["cls_token"]), st)
-        weight_grad(dpre, ctx["xt"], g["_fc1.0.weight"], D, F, B * N, ldy=D, ldx=F, dtype=self.dt_code,
+        main, inner = self.fc1["main"], ctx["inner"]
+        Fx = F if inner is None else prm["w0"].shape[0]
+        weight_grad(dpre, ctx["xt"], g[main + ".weight"], D, Fx, B * N, ldy=D, ldx=Fx, dtype=self.dt_code,
                     work_pool=pool)
-        colsum(dpre, B * N, D, D, self.dt_code, g["_fc1.0.bias"], pool)
+        colsum(dpre, B * N, D, D, self.dt_code, g[main + ".bias"], pool)
+        if inner is not None:
+            # d LN-out = dpre W1 ; LayerNorm backward ; GELU backward ; W0 / b0 gradients
+            w0n, lnn = self.fc1["inner"]
+            Fm, Fin = Fx, inner["F"]
+            dxln = pool(B * N * Fm).view(B * N, Fm)
+            gemm(dpre, prm["w1"], dxln, B * N, Fm, D, lda=D, ldb=Fm, ldc=Fm, b_kn=1, dtype=self.dt_code, c_dtype=F32)
+            dy0 = torch.zeros(B * N, Fm, dtype=torch.float32, device=dev)
+            rpb = 64
+            work = pool(_lib.query("tm_layernorm_bwd_workspace", B * N, Fm, rpb) // 4)
+            _lib.call("tm_layernorm_bwd", _p(dxln), F32, _p(inner["y0"]), _p(prm["ln0_w"]), _p(inner["mean0"]),
+                      _p(inner["rstd0"]), B * N, Fm, N, N, 0, rpb, _p(dy0), _p(work), _p(g[lnn + ".weight"]),
+                      _p(g[lnn + ".bias"]), st)
+            dpre0 = pool(B * N * Fm, self.tdtype).view(B * N, Fm)
+            _lib.call("tm_gelu_bwd", self.dt_code, _p(dy0), _p(inner["pre0"]), B * N * Fm, _p(dpre0), st)
+            weight_grad(dpre0, inner["xt"], g[w0n + ".weight"], Fm, Fin, B * N, ldy=Fm, ldx=Fin, dtype=self.dt_code,
+                        work_pool=pool)
+            colsum(dpre0, B * N, Fm, Fm, self.dt_code, g[w0n + ".bias"], pool)
         return g
 
 

@@ -14,9 +14,12 @@ hand-written HIP kernels of ``libtransmil_hip.so`` (``engine.TransMILEngine``).
 fp32 (the parity mode: f32 MFMA, results within fp32 rounding of the CPU
 oracle).  There is no CPU / eager fallback: a CPU tensor raises.
 
-Supported _fc1 branch: ``in_features`` not in {2048, 1024, 768}, i.e.
-``Linear(in, out) + GELU`` (:128-133) -- the branch every d=512 config uses.
-``dim_head`` is fixed at 64 by TransLayer (dim // 8 with dim = 512).
+Supported _fc1 branches: ``Linear(in, out) + GELU`` for ``in_features`` not in
+{2048, 1024, 768} (:128-133, every d=512 config), and the RCC ``in_features = 2048``
+branch ``Linear(2048,1024) + GELU + LayerNorm(1024) + Linear(1024,512) + GELU``
+(:100-111, the RetCCL-feature config).  The 1024 branch raises, as the reference's does
+(its LayerNorm(out_features) meets a 1024-wide input, :117-121); the 768 branch raises
+(not on the HIP path).  ``dim_head`` is fixed at 64 by TransLayer (dim // 8, dim = 512).
 """
 from __future__ import annotations
 
@@ -25,7 +28,7 @@ import math
 import torch
 import torch.nn as nn
 
-from ..engine import TransMILEngine, NystromEngine
+from ..engine import TransMILEngine, NystromEngine, FC1_PLAIN, FC1_RCC2048
 from ..nystrom_attention import NystromAttention, AttentionMap
 from .. import ops
 
@@ -101,6 +104,20 @@ class TransMIL(nn.Module):
 
     # False: always run module by module (what a hook on a submodule switches to by itself)
     fused = True
+    _head = "_fc"     # class-token Linear (code/models/TransMIL.py:155)
+
+    def _fc1_layout(self):
+        if len(self._fc1) == 2:
+            return FC1_PLAIN
+        if self.in_features == 2048 and len(self._fc1) == 5:
+            return FC1_RCC2048
+        if self.in_features == 1024:
+            raise NotImplementedError(
+                "in_features=1024: the reference's branch (code/models/TransMIL.py:117-121) applies "
+                "LayerNorm(out_features=512) to a 1024-wide activation and fails; it has no HIP path")
+        raise NotImplementedError(
+            f"in_features={self.in_features}: only the Linear+GELU (code/models/TransMIL.py:128-133) and "
+            "in_features=2048 (:100-111) _fc1 branches run on the HIP path")
 
     def _hooked(self):
         """A forward / backward hook on any submodule (GradCAM on model.norm or
@@ -121,12 +138,17 @@ class TransMIL(nn.Module):
         class token, layer1, PPEG, layer2, norm (all S tokens), _fc on the class token."""
         B, N, _ = x.shape
         G = int(math.ceil(math.sqrt(N)))
-        h = ops.embed(self._fc1, self.cls_token, x)    # :175-186
+        if self._fc1_layout() is FC1_RCC2048:           # :101-110 inner Linear + GELU + LayerNorm
+            x = ops.linear_gelu(self._fc1[0], x)
+            x = self._fc1[2](x)
+            h = ops.embed(self._fc1[3], self.cls_token, x)
+        else:
+            h = ops.embed(self._fc1[0], self.cls_token, x)   # :175-186
         h, _ = self.layer1(h)                           # :196
         h = self.pos_layer(h, G, G)                     # :198
         h, attn = self.layer2(h)                        # :199
         h = self.norm(h)[:, 0]                          # :202-203
-        logits = ops.linear(self._fc, h)                # :204
+        logits = ops.linear(getattr(self, self._head), h)   # :204
         if return_attn:
             S = G * G + 1
             return logits, (attn, 256 - S % 256 if S % 256 else 0)
@@ -149,10 +171,7 @@ class TransMIL(nn.Module):
             x = x.unsqueeze(0)
         if not x.is_cuda:
             raise RuntimeError("TransMIL (HIP) needs a GPU tensor: there is no CPU path")
-        if len(self._fc1) != 2:
-            raise NotImplementedError(
-                f"in_features={self.in_features}: only the Linear+GELU _fc1 branch "
-                "(code/models/TransMIL.py:128-133) runs on the HIP path")
+        layout = self._fc1_layout()
         x = x.float().contiguous()             # :174
         if not self.fused or self._hooked():
             return self._forward_modules(x, return_attn)
@@ -164,7 +183,7 @@ class TransMIL(nn.Module):
             self._dropout_counter.add_(1)
             seed_dev = self._dropout_counter.clone()   # snapshot for this forward's backward
         holder = {} if return_attn else None
-        engine = TransMILEngine(self.compute_dtype)
+        engine = TransMILEngine(self.compute_dtype, fc1=layout, head=self._head)
         logits = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, x, *params)
         if return_attn:
             c = holder["ctx"]
@@ -188,3 +207,4 @@ def _reference_fc1(in_features, out_features, norm_layer):
     return nn.Sequential(nn.Linear(in_features, in_features), nn.GELU(), nn.Dropout(p=0.6),
                          norm_layer(in_features), nn.Linear(in_features, out_features), nn.GELU(),
                          nn.Dropout(p=0.6), norm_layer(out_features))
+

@@ -144,12 +144,57 @@ class _EmbedFn(torch.autograd.Function):
         return dx, dw, db, dcls
 
 
-def embed(fc1, cls_token, x):
-    """``_fc1`` = Sequential(Linear, GELU) + grid pad + class token on the HIP GEMM."""
+def embed(lin, cls_token, x):
+    """The last ``Linear + GELU`` of ``_fc1`` + grid pad + class token on the HIP GEMM."""
     if not x.is_cuda:
         raise RuntimeError("HIP _fc1 needs a GPU tensor")
-    lin = fc1[0]
     return _EmbedFn.apply(x.float(), lin.weight, lin.bias, cls_token)
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    """y = GELU(x W^T + b) (fp32) on the HIP GEMM epilogue (pre-activation kept); backward
+    dpre = dy GELU'(pre) (tm_gelu_bwd), dX = dpre W, dW = dpre^T X, db = colsum dpre."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        shp = x.shape
+        K = shp[-1]
+        x2 = x.reshape(-1, K).contiguous()
+        M, Nout = x2.shape[0], w.shape[0]
+        y = torch.empty(M, Nout, device=x.device)
+        pre = torch.empty(M, Nout, device=x.device)
+        gemm(x2, w.contiguous(), y, M, Nout, K, lda=K, ldb=K, ldc=Nout, dtype=F32, c_dtype=F32, bias=b, gelu=True,
+             pre=pre, ld_pre=Nout)
+        ctx.save_for_backward(x2, w, pre)
+        ctx.shp = shp
+        return y.view(*shp[:-1], Nout)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, pre = ctx.saved_tensors
+        M, K = x2.shape
+        Nout = w.shape[0]
+        pool = Pool(dy.device)
+        dpre = torch.empty(M, Nout, device=dy.device)
+        _lib.call("tm_gelu_bwd", F32, _p(dy.float().reshape(M, Nout).contiguous()), _p(pre), M * Nout, _p(dpre),
+                  _stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, device=dy.device)
+            gemm(dpre, w.contiguous(), dx, M, K, Nout, lda=Nout, ldb=K, ldc=K, b_kn=1, dtype=F32, c_dtype=F32)
+            dx = dx.view(ctx.shp)
+        dw = torch.empty(Nout, K, device=dy.device)
+        weight_grad(dpre, x2, dw, Nout, K, M, ldy=Nout, ldx=K, dtype=F32, work_pool=pool)
+        db = torch.empty(Nout, device=dy.device)
+        colsum(dpre, M, Nout, Nout, F32, db, pool)
+        return dx, dw, db
+
+
+def linear_gelu(lin, x):
+    """``Sequential(Linear, GELU)`` forward on the HIP GEMM (the inner stage of the 2048 _fc1 branch)."""
+    if not x.is_cuda:
+        raise RuntimeError("HIP Linear+GELU needs a GPU tensor")
+    return _LinearGeluFn.apply(x.float(), lin.weight, lin.bias)
 
 
 class _LinearFn(torch.autograd.Function):
