@@ -101,9 +101,9 @@ def cpu_baseline(n_patches, ncls, steps, feat=512):
     torch.set_num_threads(threads)
     TransLayer.compute_attn = False
     torch.manual_seed(0)
-    model = RefTransMIL(ncls, 512, 512).train()
+    model = RefTransMIL(ncls, feat, 512).train()
     opt = torch.optim.RAdam(model.parameters(), lr=2e-4)
-    x = torch.rand(1, n_patches, 512)
+    x = torch.rand(1, n_patches, feat)
     y = torch.tensor([1])
     lossf = torch.nn.CrossEntropyLoss()
 
@@ -121,7 +121,7 @@ def cpu_baseline(n_patches, ncls, steps, feat=512):
     dt = time.perf_counter() - t0
     TransLayer.compute_attn = True
     return dict(value=steps / dt, unit="slides/sec", cores=threads, kind="port",
-                sample=f"{steps} fwd+bwd+RAdam steps (after 1 warm-up), 1 bag N={n_patches}x512, fp32, "
+                sample=f"{steps} fwd+bwd+RAdam steps (after 1 warm-up), 1 bag N={n_patches}x{feat}, fp32, "
                        f"train mode, torch.set_num_threads({threads})")
 
 
@@ -293,7 +293,7 @@ def main():
             "roofline": roof,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args.n, args.classes, args.cpu_steps)
+            out["cpu_baseline"] = cpu_baseline(args.n, args.classes, args.cpu_steps, args.features)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
