@@ -157,3 +157,23 @@ def test_fused_radam_lookahead_matches_torch(k):
         sa, sb = opt_a.state[pa], base.state[pb]
         torch.testing.assert_close(sa["exp_avg"], sb["exp_avg"], rtol=2e-5, atol=1e-8)
         torch.testing.assert_close(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=2e-5, atol=1e-10)
+
+
+def test_fc1_branches_and_mdmil_state_dict_keys():
+    """Host logic of the model entry points (no GPU): the 2048 branch selects the RCC engine
+    layout, the reference-broken 1024 branch raises, and MDMIL / TransMIL(2048) expose exactly
+    the oracle's (= the reference's) state_dict keys and shapes."""
+    import pytest
+    from oracle.mdmil_ref import MDMIL as RefMD
+    from oracle.transmil_ref import TransMIL as Ref
+    from transmil_deepgraft_amd.engine import FC1_PLAIN, FC1_RCC2048
+    from transmil_deepgraft_amd.models import MDMIL, TransMIL
+    assert TransMIL(2, 512)._fc1_layout() is FC1_PLAIN
+    assert TransMIL(2, 2048)._fc1_layout() is FC1_RCC2048
+    with pytest.raises(NotImplementedError):
+        TransMIL(2, 1024)._fc1_layout()
+    for ours, ref in ((MDMIL(3), RefMD(3)), (TransMIL(2, 2048), Ref(2, 2048))):
+        a = {k: tuple(v.shape) for k, v in ours.state_dict().items()}
+        b = {k: tuple(v.shape) for k, v in ref.state_dict().items()}
+        assert a == b
+    assert MDMIL(3)._head == "_fc2" and MDMIL(3).n_classes == 3
