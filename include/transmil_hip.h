@@ -155,6 +155,24 @@ long long tm_pinv_bwd_workspace_floats(int nbh);
 int tm_pinv_bwd(const float* X, int nbh, int iters, int prec, const float* saved, float* dZ, float* work,
                 float* dX, void* stream);
 
+/* ---- pseudo-inverse on split operands, bf16 (bench) mode (pinv_split.hip) --
+ * Same function as tm_pinv_fwd / tm_pinv_bwd with prec 1, restructured for MI355X: every chain
+ * matrix is kept as bf16 hi / lo planes (hi = bf16(M), lo = bf16(M - hi); the lo plane follows the
+ * hi plane at + nbh*256*256 elements), products are hi*hi + hi*lo + lo*hi on the bf16 MFMA with
+ * fp32 accumulation, 64x64 output tiles fed by LDS-DMA; 14 launches forward.
+ * A2 = softmax(ql kl^T) with its split planes (replaces tm_nys_sim2_softmax on this path): */
+int tm_nys_sim2_softmax_split(const float* ql, const float* kl, int nbh, float* a2, void* a2s, void* stream);
+/* saved: Z_iters fp32 at saved[0 .. nbh*65536), then the split chain matrices, sums and maxima */
+long long tm_pinv_split_saved_floats(int nbh, int iters);
+int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* saved, void* stream);
+/* work: the gradient w.r.t. Z_iters as split planes at work[0 .. nbh*65536) on entry (tm_split_f32);
+ * out = dL/dX (softmax == 0) or the backward of A2 = softmax(.) through X (softmax != 0), fp32 */
+long long tm_pinv_bwd_split_workspace_floats(int nbh);
+int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int iters, const float* saved, float* work,
+                      int softmax, float* out, void* stream);
+/* fp32 -> split planes: y[i] = bf16(x[i]), y[count + i] = bf16(x[i] - y[i]); count % 8 == 0 */
+int tm_split_f32(const float* x, void* y, long long count, void* stream);
+
 /* ---- PPEG (ppeg.hip) -- code/models/TransMIL.py:60-75 -------------------- */
 int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, const float* b5, const float* w3,
                  const float* b3, int D, float* wfold, float* bfold, void* stream);

@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--stamps", action="store_true", help="a1_fwd in-kernel s_memtime stamps")
     ap.add_argument("--gemm-ab", action="store_true", help="also time the GEMMs on the register-staged loop")
+    ap.add_argument("--split-stamps", action="store_true", help="per-wave s_memtime stamps of the split pinv chain")
     args = ap.parse_args()
     dev = "cuda"
     N = args.n
@@ -141,6 +142,52 @@ def main():
         case(f"pinv_bwd bf16x3 [{nm}]", lambda: _lib.call("tm_pinv_bwd", E._p(X), nbh, 6, 1, E._p(saved), E._p(pdz),
                                                            E._p(pwork), E._p(pdX), st()), 28 * f)
     _lib.lib().tm_debug_set_variant(3, 0)
+    # split-operand chain (pinv_split.hip): 14 launches forward, 4 per iteration + 2 backward
+    Xs = torch.empty(2 * nbh * 65536, dtype=torch.bfloat16, device=dev)
+    _lib.call("tm_split_f32", E._p(X), E._p(Xs), nbh * 65536, st())
+    ssaved = torch.empty(_lib.query("tm_pinv_split_saved_floats", nbh, 6), device=dev)
+    swork = torch.empty(_lib.query("tm_pinv_bwd_split_workspace_floats", nbh), device=dev)
+    sout = torch.empty(nbh, 256, 256, device=dev)
+    for v, nm in ((1, "no DMA"), (2, "no MFMA"), (3, "no epilogue"), (4, "epilogue only"), (5, "empty"), (0, "full")):
+        _lib.lib().tm_debug_set_split_variant(v)
+        case(f"pinv_fwd split [{nm}]", lambda: _lib.call("tm_pinv_fwd_split", E._p(X), E._p(Xs), nbh, 6,
+                                                           E._p(ssaved), st()), 24 * f)
+    _lib.lib().tm_debug_set_split_variant(0)
+    if args.split_stamps:
+        import numpy as np
+        # workgroups per launch: L1 (S + abs sums), A_0, B_0, (A_k, B_k) k=1..4, A_5, B_5, F
+        t16 = 16 * nbh
+        wgs = [2 * t16, t16, 2 * t16] + [2 * t16] * 8 + [2 * t16, t16, t16]
+        nl = len(wgs)
+        buf = torch.zeros(sum(wgs) * 4 * 8, dtype=torch.int64, device=dev)
+        for rep in range(3):  # the third run is measured (warm caches)
+            buf.zero_()
+            _lib.lib().tm_debug_set_split_stamps(C.c_void_p(buf.data_ptr()))
+            _lib.call("tm_pinv_fwd_split", E._p(X), E._p(Xs), nbh, 6, E._p(ssaved), st())
+            _lib.lib().tm_debug_set_split_stamps(None)
+            torch.cuda.synchronize()
+        a = buf.cpu().numpy()
+        off = 0
+        prev_end = None
+        names = ["setup", "wait c0", "chunk0", "chunks1+", "epilogue"]
+        print("split pinv_fwd stamps: per launch, medians over waves (shader cycles); realtime in us")
+        for li in range(nl):
+            nwg = wgs[li]
+            seg = a[off:off + nwg * 32].reshape(nwg, 4, 8)
+            off += nwg * 32
+            seg = seg[seg[:, 0, 7] > 0]  # product workgroups (abs-sum ones do not stamp)
+            rt0, rt1 = seg[:, :, 0].min(), seg[:, :, 7].max()
+            d = np.diff(seg[:, :, 1:7].astype(np.int64), axis=2)
+            med = [int(np.median(d[:, :, i])) for i in range(5)]
+            mx = [int(np.max(d[:, :, i])) for i in range(5)]
+            gap = (rt0 - prev_end) / 100.0 if prev_end is not None else float("nan")
+            startspread = (seg[:, :, 0].max() - rt0) / 100.0
+            print(f"  launch {li:2d} ({nwg} wg): span {(rt1 - rt0) / 100.0:6.2f} us  gap {gap:6.2f} us  start spread "
+                  f"{startspread:5.2f} us  " + "  ".join(f"{n} {m}/{x}" for n, m, x in zip(names, med, mx)))
+            prev_end = rt1
+    _lib.call("tm_split_f32", E._p(pdz), E._p(swork), nbh * 65536, st())
+    case("pinv_bwd split (+softmax bwd)", lambda: _lib.call("tm_pinv_bwd_split", E._p(X), E._p(Xs), nbh, 6,
+                                                            E._p(ssaved), E._p(swork), 1, E._p(sout), st()), 32 * f)
     for gv in ((0, 1, 2) if args.gemm_ab else (0,)):
         _lib.lib().tm_debug_set_variant(2, gv)
         tag[0] = ("", "[2 LDS buf] ", "[glds ring] ")[gv]

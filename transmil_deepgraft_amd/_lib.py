@@ -97,6 +97,12 @@ _SIGS = {
     "tm_pinv_fwd": (I, [P, I, I, I, P, P]),
     "tm_pinv_bwd_workspace_floats": (L, [I]),
     "tm_pinv_bwd": (I, [P, I, I, I, P, P, P, P, P]),
+    "tm_nys_sim2_softmax_split": (I, [P, P, I, P, P, P]),
+    "tm_pinv_split_saved_floats": (L, [I, I]),
+    "tm_pinv_fwd_split": (I, [P, P, I, I, P, P]),
+    "tm_pinv_bwd_split_workspace_floats": (L, [I]),
+    "tm_pinv_bwd_split": (I, [P, P, I, I, P, P, I, P, P]),
+    "tm_split_f32": (I, [P, P, L, P]),
     "tm_ppeg_fold": (I, [P, P, P, P, P, P, I, P, P, P]),
     "tm_ppeg_fwd": (I, [P, I, I, I, P, P, P, P]),
     "tm_ppeg_bwd_workspace": (L, [I, I, I]),

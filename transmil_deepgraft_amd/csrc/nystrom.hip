@@ -71,8 +71,10 @@ __global__ void landmarks_kernel(const T* __restrict__ q, const T* __restrict__ 
 
 // ---------------------------------------------------------------------------
 // A2 = softmax_j(ql_i . kl_j), fp32 FMA.  grid (nbh, 16), block 256: 16 rows per block, thread = column j.
+// a2s (optional): the same values as bf16 hi / lo planes (hi = bf16(a), lo = bf16(a - hi); lo plane at
+// a2s + nbh * 256 * 256), the operand format of the split pseudo-inverse chain (pinv_split.hip).
 __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restrict__ ql, const float* __restrict__ kl,
-                                                           float* __restrict__ a2) {
+                                                           float* __restrict__ a2, bf16* __restrict__ a2s) {
   const int bh = blockIdx.x, i0 = blockIdx.y * 16, j = threadIdx.x, lane = j & 63, wave = j >> 6;
   __shared__ float kt[DH][NL + 1];
   __shared__ float qs[16][DH];
@@ -110,7 +112,14 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const float tot = (red[0][r] + red[1][r]) + (red[2][r] + red[3][r]);
-    a2[((size_t)bh * NL + i0 + r) * NL + j] = s[r] / tot;
+    const size_t o = ((size_t)bh * NL + i0 + r) * NL + j;
+    const float v = s[r] / tot;
+    a2[o] = v;
+    if (a2s) {
+      const bf16 hi = (bf16)v;
+      a2s[o] = hi;
+      a2s[o + (size_t)gridDim.x * NL * NL] = (bf16)(v - (float)hi);
+    }
   }
 }
 
@@ -1397,7 +1406,15 @@ extern "C" int tm_nys_landmarks(int dtype, const void* q, const void* k, int nbh
 }
 
 extern "C" int tm_nys_sim2_softmax(const float* ql, const float* kl, int nbh, float* a2, void* stream) {
-  sim2_softmax_kernel<<<dim3(nbh, NL / 16), 256, 0, (hipStream_t)stream>>>(ql, kl, a2);
+  sim2_softmax_kernel<<<dim3(nbh, NL / 16), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, nullptr);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_nys_sim2_softmax_split(const float* ql, const float* kl, int nbh, float* a2, void* a2s,
+                                         void* stream) {
+  TM_REQUIRE(a2s, "sim2_softmax_split: a2s is required");
+  sim2_softmax_kernel<<<dim3(nbh, NL / 16), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, (bf16*)a2s);
   TM_CHECK_LAUNCH();
   return 0;
 }

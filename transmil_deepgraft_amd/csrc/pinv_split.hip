@@ -1,0 +1,763 @@
+// Moore-Penrose iterative pseudo-inverse (SURVEY.md App. A eq. 7) for the bf16 (bench) mode:
+// the chain of moore_penrose_iter_pinv (third-party nystrom_attention, called from
+// NystromAttention.forward, code/models/TransMIL.py:47) and its backward, on "split" operands.
+//
+// Split storage.  Every 256x256 chain matrix M of B*h heads is kept as two bf16 planes,
+// hi = bf16(M) and lo = bf16(M - hi) (lo plane at hi + nbh*65536 elements; the pair takes the
+// bytes of one fp32 matrix and holds M to ~2^-17 relative).  A product C = op(A) op(B) is
+// hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_bf16 with fp32 accumulation ("bf16x3"), so the
+// operands feed the MFMA straight from LDS: no per-fragment fp32 -> bf16 split in the consumer.
+//
+// Stage kernel.  One launch = up to three independent jobs (products of 1-2 terms, or the
+// abs-sum reduction), each over all heads.  Workgroup = one 64x64 output tile of one head,
+// 8 waves: 2x2 subtiles of 32x32, each subtile's k-steps split over the two waves of one SIMD
+// (partial tiles summed in the epilogue), the whole K of every term.  Operand chunks (64 rows x 64 k, hi and lo)
+// come by LDS-DMA (global_load_lds, 16 B per lane, no VGPR round trip) into a 3-slot ring of
+// 32 KB, two chunks ahead of the MFMAs (counted s_waitcnt vmcnt + raw s_barrier).  LDS images:
+//   "kc" (k-contiguous: the stored row is the output index, op(A) = A or op(B) = B^T):
+//       [64 rows][64 k], 16-B slot c of row r at c ^ ((r >> 1) & 7)  -> ds_read_b128 fragments
+//   "kr" (k-rows: the stored row is k, op(A) = A^T or op(B) = B):
+//       [64 k][64 cols], slot c of k-row k at c ^ (((k >> 1) & 1) << 2) -> 2 x ds_read_b64_tr_b16
+// (both bank-conflict free; the swizzle is applied to the DMA source address).  The epilogue
+// stages the fp32 tile through LDS and writes whole 16-B row pieces: scale, diagonal, up to two
+// addend matrices, and up to four outputs (split, fp32, and two split side outputs).
+//
+// Forward schedule (P_k = X Z_k, carried by its own recurrence, as in pinv.hip), per layer:
+//   L1:  S = X X^T                       + |X| row / column sums, per-head maxima
+//   A_0: R = S S / c^2,  T3 = R - 7 S/c + 15I,  P_0 = S/c          (c = max rowsum * max colsum)
+//   B_k: T5 = 13I - P T3,  P_{k+1} = 3.25 P - 0.25 R T3
+//   A_k: R = P P, T3 = R - 7P + 15I,  Z_k = 0.25 Z_{k-1} T5_{k-1}  (Z_0 = X^T / c is never formed)
+//   F:   Z_6 = 0.25 Z_5 T5_5  (split + fp32)
+// 14 dependent launches.  The backward runs the reference graph's adjoint (4 launches per
+// iteration), then one launch for the partial sums of the c gradient and one that applies the
+// Z_0 = X^T / c terms and (optionally) the softmax backward of A2 = X.
+#include "common.h"
+#include "../../include/transmil_hip.h"
+
+namespace {
+
+constexpr int NL = 256;
+constexpr int MAT = NL * NL;            // elements per head matrix
+constexpr int PC = 64 * 128;            // one 64 x 64 bf16 plane chunk image: 8 KB
+constexpr int SLOT = 4 * PC;            // A hi, A lo, B hi, B lo
+constexpr int NSLOT = 3;
+constexpr int STAGE_LDS = NSLOT * SLOT; // 96 KB ring
+constexpr int EROW = 68;                // epilogue tile row (floats)
+constexpr int EPI_LDS = 64 * EROW * 4;  // the fp32 output tile (17 KB); one workgroup per CU
+constexpr int MAXJ = 3;
+constexpr int NPROD = 8;                // producer (LDS-DMA) waves; 4 consumer waves
+constexpr int NTHREADS = 64 * (4 + NPROD);
+
+typedef __attribute__((address_space(3))) void lds_t;
+typedef __attribute__((address_space(1))) void glb_t;
+typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+
+struct SOp {
+  const bf16* p;  // hi plane of head 0 (lo plane at p + plane)
+  int kr;         // 1: stored row index is k ("kr" image), 0: stored row is the output index ("kc")
+  int pad;
+};
+
+enum { KIND_PRODUCT = 0, KIND_ABSSUMS = 1 };
+
+struct SJob {
+  SOp a[2], b[2];
+  int nterms, kind;
+  float alpha, diag;       // s = alpha * invc^alpha_cpow * sum;  v = s + diag*I + e1s*E1' + e2s*E2
+  int alpha_cpow, e1_cpow; // E1' = E1 * invc^e1_cpow
+  const void* e1; float e1s; int e1_f32;
+  const void* e2; float e2s; int e2_f32;
+  void* c; int c_f32; int pad0;
+  float* cf;                                // optional fp32 copy of v
+  bf16* c2; float c2_alpha, c2_diag, c2_e1; // optional split: c2_alpha*s + c2_diag*I + c2_e1*E1'
+  bf16* c3; float c3_e1; int pad1;          // optional split: c3_e1 * E1'
+};
+
+struct SLaunch {
+  SJob j[MAXJ];
+  int njobs, nbh;
+  long long plane;          // elements between the hi and lo planes of a split matrix
+  const float* maxima;      // [2][nbh] per-head maxima of the |X| row / column sums (for invc), or null
+  const float* X;           // fp32 X (abs-sum jobs)
+  float* sums;              // [2][nbh][256] row / column sums (abs-sum jobs)
+  float* maxima_out;        // [2][nbh] (abs-sum jobs)
+  int dbg;                  // ablation (microbench only): 1 no DMA, 2 no LDS reads / MFMA, 3 no epilogue,
+                            // 4 epilogue only, 5 empty
+  unsigned long long* stamps;  // diagnostic build only: per-wave s_memtime stamps, or null
+};
+
+int g_split_dbg = 0;
+unsigned long long* g_split_stamps = nullptr;
+
+// one s_memtime stamp (shader clock), its own lgkmcnt wait inside the statement
+TM_DEV unsigned long long stamp() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+TM_DEV unsigned long long rstamp() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+TM_DEV float powc(float c, int p) { return p == 0 ? 1.f : (p == 1 ? c : c * c); }
+
+// 1 / (max_all rowsum * max_all colsum) from the per-head maxima
+// (scalar loads through the constant address space: no VMEM counter traffic, so the DMA ring's
+// counted waits are not disturbed)
+TM_DEV float inv_c(const float* maxima, int nbh) {
+  typedef const __attribute__((address_space(4))) float cfloat;
+  cfloat* m = (cfloat*)(uintptr_t)maxima;
+  float mc = -INFINITY, mr = -INFINITY;
+  for (int h = 0; h < nbh; ++h) { mc = fmaxf(mc, m[h]); mr = fmaxf(mr, m[nbh + h]); }
+  return 1.f / (mc * mr);
+}
+
+// LDS reads as inline asm: hipcc (ROCm 7.2) puts an `s_waitcnt vmcnt(0)` in front of every
+// ds_read_b64_tr_b16 builtin while an LDS-DMA is in flight (it cannot tell the DMA's target from
+// the read's), which would drain the prefetch ring every k-step.  The asm reads are ordered by
+// explicit lgkmcnt waits + sched_barrier (hipcc does not count them).
+TM_DEV unsigned lds_off(const void* p) { return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p; }
+template <int OFF> TM_DEV void ds_b128(bf16x8& d, unsigned a) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+template <int OFF> TM_DEV void ds_tr(bf16x4& d, unsigned a) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+template <int N> TM_DEV void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// "kc" image: lane address of k-step s (rows ob + (lane&31), 16-B chunk 2s + (lane>>5))
+TM_DEV unsigned kc_addr(int ob, int s, int lane) {
+  const int r = ob + (lane & 31), c = 2 * s + (lane >> 5);
+  return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+}
+// "kr" image: lane address of k-step 0, first 4 k-rows (16-lane group g: lane 4q+p -> k-row 8(g>>1)+q,
+// outputs ob + 16(g&1) + 4p..+3); k-step s adds 16 rows (2048 B), the second 4 rows 512 B.
+TM_DEV unsigned kr_addr(int ob, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int o = ob + (g & 1) * 16 + 4 * p;
+  const int k = 8 * (g >> 1) + q;
+  const int c = o >> 3, half = (o >> 2) & 1;
+  return k * 128 + ((c ^ (((k >> 1) & 1) << 2)) << 4) + half * 8;
+}
+
+struct Frag { bf16x8 h, l; };
+TM_DEV bf16x8 join(const bf16x4& a, const bf16x4& b) { return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
+
+// issue the LDS reads of one operand's (hi, lo) fragments of k-step S; PL = plane pair (0 A, 2 B)
+template <int KR, int S, int PL>
+TM_DEV void read_op(Frag& f, unsigned krbase, const unsigned (&kc)[4]) {
+  if constexpr (KR) {
+    bf16x4 a, b, c, d;
+    ds_tr<PL * PC + S * 2048>(a, krbase);
+    ds_tr<PL * PC + S * 2048 + 512>(b, krbase);
+    ds_tr<(PL + 1) * PC + S * 2048>(c, krbase);
+    ds_tr<(PL + 1) * PC + S * 2048 + 512>(d, krbase);
+    f.h = join(a, b);
+    f.l = join(c, d);
+  } else {
+    ds_b128<PL * PC>(f.h, kc[S]);
+    ds_b128<(PL + 1) * PC>(f.l, kc[S]);
+  }
+}
+
+// One 64-deep chunk of one term from ring slot `sb` (byte offset), by one consumer wave (its
+// 32x32 subtile): 4 k-steps of 3 MFMAs, the LDS reads of step s+1 in flight during step s.
+template <int AKR, int BKR>
+TM_DEV void chunk_mma(f32x16& acc, unsigned sb, unsigned akr, unsigned bkr, const unsigned (&akc0)[4],
+                      const unsigned (&bkc0)[4]) {
+  constexpr int RS = (AKR ? 4 : 2) + (BKR ? 4 : 2);  // LDS reads per k-step
+  unsigned akc[4], bkc[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) { akc[s] = akc0[s] + sb; bkc[s] = bkc0[s] + sb; }
+  const unsigned ab = akr + sb, bb = bkr + sb;
+  Frag a[2], b[2];
+  read_op<AKR, 0, 0>(a[0], ab, akc); read_op<BKR, 0, 2>(b[0], bb, bkc);
+  read_op<AKR, 1, 0>(a[1], ab, akc); read_op<BKR, 1, 2>(b[1], bb, bkc);
+  wait_lgkm<RS>();
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0].l, b[0].h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0].h, b[0].l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0].h, b[0].h, acc, 0, 0, 0);
+  read_op<AKR, 2, 0>(a[0], ab, akc); read_op<BKR, 2, 2>(b[0], bb, bkc);
+  wait_lgkm<RS>();
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1].l, b[1].h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1].h, b[1].l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1].h, b[1].h, acc, 0, 0, 0);
+  read_op<AKR, 3, 0>(a[1], ab, akc); read_op<BKR, 3, 2>(b[1], bb, bkc);
+  wait_lgkm<RS>();
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0].l, b[0].h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0].h, b[0].l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0].h, b[0].h, acc, 0, 0, 0);
+  wait_lgkm<0>();
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1].l, b[1].h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1].h, b[1].l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1].h, b[1].h, acc, 0, 0, 0);
+}
+
+template <int N>
+TM_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// 8 consecutive elements of a split matrix as fp32
+TM_DEV void load_split8(const bf16* hi, long long plane, size_t off, float* v) {
+  const bf16x8 h = *(const bf16x8*)(hi + off), l = *(const bf16x8*)(hi + plane + off);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)l[e];
+}
+TM_DEV void store_split8(bf16* hi, long long plane, size_t off, const float* v) {
+  bf16x8 h, l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h[e] = (bf16)v[e];
+    l[e] = (bf16)(v[e] - (float)h[e]);
+  }
+  *(bf16x8*)(hi + off) = h;
+  *(bf16x8*)(hi + plane + off) = l;
+}
+TM_DEV void load_f8(const float* p, size_t off, float* v) {
+  const f32x4 a = *(const f32x4*)(p + off), b = *(const f32x4*)(p + off + 4);
+  v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
+}
+TM_DEV void store_f8(float* p, size_t off, const float* v) {
+  *(f32x4*)(p + off) = (f32x4){v[0], v[1], v[2], v[3]};
+  *(f32x4*)(p + off + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+}
+
+// |X| row sums (which = 0) or column sums (which = 1) of one head, and their maximum
+// (threads 0..255 work, the other waves only meet the barriers)
+TM_DEV void abssums(const SLaunch& L, int head, int which, float* red) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bool on = t < NL;
+  const float* x = L.X + (size_t)head * MAT;
+  float s = 0.f;
+  if (which == 0) {
+    // wave w < 4: rows 64w..64w+63; lane l sums columns 4l..4l+3 of each row, the row total via LDS
+    float* part = red + 16 + (wave & 3) * 64 * 65;
+    if (on)
+      for (int r = 0; r < 64; ++r) {
+        const f32x4 v = *(const f32x4*)(x + (size_t)(wave * 64 + r) * NL + lane * 4);
+        part[r * 65 + lane] = fabsf(v[0]) + fabsf(v[1]) + fabsf(v[2]) + fabsf(v[3]);
+      }
+    __syncthreads();
+    if (on)
+      for (int l = 0; l < 64; ++l) s += part[lane * 65 + l];
+    // thread t now holds the sum of row 64*wave + lane = t
+  } else if (on) {
+    for (int i = 0; i < NL; ++i) s += fabsf(x[(size_t)i * NL + t]);
+  }
+  if (on) L.sums[((size_t)which * L.nbh + head) * NL + t] = s;
+  const float m = wave_max(s);
+  if (lane == 0 && on) red[wave] = m;
+  __syncthreads();
+  if (t == 0) L.maxima_out[which * L.nbh + head] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// Roles: waves 0-3 are consumers (one 32x32 subtile each, the whole K: LDS reads + MFMAs +
+// epilogue), waves 4-7 producers (wave 4+p issues plane p of every chunk by LDS-DMA: 0 A hi,
+// 1 A lo, 2 B hi, 3 B lo).  One s_barrier per chunk: a chunk is read after the barrier that
+// follows its producers' counted vmcnt wait, and its slot is refilled after the barrier that
+// follows the consumers' last read of it.  Grid: (16 * nbh, njobs); blockIdx.y is the job.
+__global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SJob& J = L.j[blockIdx.y];
+  const int u = blockIdx.x;
+  const int nbh = L.nbh;
+  const int head = u % nbh, tile = u / nbh;
+  if (J.kind == KIND_ABSSUMS) {
+    if (u < 2 * nbh) abssums(L, head, tile, (float*)smem);
+    return;
+  }
+  if (L.dbg == 5) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = (tile >> 2) * 64, n0 = (tile & 3) * 64;
+  const size_t hoff = (size_t)head * MAT;
+  const long long plane = L.plane;
+  const int nch = J.nterms * 4;
+  const int nchl = L.dbg == 4 ? 0 : nch;
+  const bool st_on = L.stamps != nullptr;
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (st_on) { ts[0] = rstamp(); ts[1] = stamp(); }
+
+  // epilogue operands first (plain loads, issued before any DMA: every later counted wait covers
+  // them): this thread's 8-element row piece (row tid/8, cols 8 (tid&7)) of E1 / E2, raw 16-B words
+  const int lr = tid >> 3, lc = (tid & 7) * 8;
+  const size_t eoff = hoff + (size_t)(m0 + lr) * NL + n0 + lc;
+  const void* e1p = J.e1;
+  const void* e2p = J.e2;
+  const int e1f = J.e1_f32, e2f = J.e2_f32;
+  f32x4 e1raw[2], e2raw[2];
+  auto eload = [&](const void* e, int f32, f32x4 (&r)[2]) {
+    if (f32) {
+      const float* q = (const float*)e;
+      r[0] = *(const f32x4*)(q + eoff); r[1] = *(const f32x4*)(q + eoff + 4);
+    } else {
+      const bf16* q = (const bf16*)e;
+      r[0] = *(const f32x4*)(q + eoff); r[1] = *(const f32x4*)(q + plane + eoff);
+    }
+  };
+  const bool epi = tid < 512;  // the 512 threads that each own one 8-element piece of the 64x64 tile
+  if (e1p && epi) eload(e1p, e1f, e1raw);
+  if (e2p && epi) eload(e2p, e2f, e2raw);
+  // per-head maxima for 1/c: one raw vector load per lane now, reduced in the epilogue
+  const bool need_c = J.alpha_cpow || J.e1_cpow;
+  float mcv = -INFINITY, mrv = -INFINITY;
+  if (need_c && nbh <= 64 && lane < nbh) { mcv = L.maxima[lane]; mrv = L.maxima[nbh + lane]; }
+  float* ep = (float*)(smem + STAGE_LDS);  // [64][EROW] fp32 tile for the epilogue
+
+  if (wv >= 4) {  // ------------------------------------------------------------ producer
+    // producer p = wv - 4 (0..NPROD-1) stages image rows of plane p / (NPROD/4) (0 A hi, 1 A lo,
+    // 2 B hi, 3 B lo): PPW pieces of 8 rows each, starting at row 8 * PPW * (p % (NPROD/4))
+    constexpr int PPW = 32 / NPROD;
+    const int p = wv - 4, pl = p / (NPROD / 4), rb = (p % (NPROD / 4)) * PPW * 8;
+    const SOp op0 = pl < 2 ? J.a[0] : J.b[0];
+    const SOp op1 = pl < 2 ? J.a[1] : J.b[1];
+    const int o0w = pl < 2 ? m0 : n0;
+    const bf16* const pb0 = op0.p + hoff + ((pl & 1) ? plane : 0);
+    const bf16* const pb1 = op1.p + hoff + ((pl & 1) ? plane : 0);
+    unsigned loff[2][PPW];  // [kr][piece]: row * 256 + 8 * (slot ^ swizzle(row))
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int row = rb + i * 8 + (lane >> 3), pos = lane & 7;
+      loff[0][i] = row * NL + 8 * (pos ^ ((row >> 1) & 7));
+      loff[1][i] = row * NL + 8 * (pos ^ (((row >> 1) & 1) << 2));
+    }
+    auto issue = [&](int c) {
+      char* img = smem + (c % NSLOT) * SLOT + pl * PC + rb * 128;
+      const int t = c >> 2, k0 = (c & 3) * 64;
+      const int kr = t ? op1.kr : op0.kr;
+      const bf16* base = (t ? pb1 : pb0) + (kr ? k0 * NL + o0w : o0w * NL + k0);
+#pragma unroll
+      for (int i = 0; i < PPW; ++i)
+        __builtin_amdgcn_global_load_lds((glb_t*)(base + (kr ? loff[1][i] : loff[0][i])), (lds_t*)(img + i * 1024),
+                                         16, 0, 0);
+    };
+    if (L.dbg != 1) {
+      issue(0);
+      issue(1);  // nch >= 4
+    }
+    for (int c = 0; c < nchl; ++c) {
+      if (c + 1 < nch) wait_vm<PPW>(); else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();  // chunk c landed (every producer); slot (c+2)%3 read by every consumer
+      asm volatile("" ::: "memory");
+      if (c + 2 < nch && L.dbg != 1) issue(c + 2);
+    }
+  } else {  // ---------------------------------------------------------------- consumer
+    const int wm = wv >> 1, wn = wv & 1;
+    const int code0 = J.a[0].kr | (J.b[0].kr << 1), code1 = J.a[1].kr | (J.b[1].kr << 1);
+    const unsigned lbase = lds_off(smem);
+    unsigned akc[4], bkc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      akc[s] = lbase + kc_addr(wm * 32, s, lane);
+      bkc[s] = lbase + kc_addr(wn * 32, s, lane);
+    }
+    const unsigned akr = lbase + kr_addr(wm * 32, lane), bkr = lbase + kr_addr(wn * 32, lane);
+    f32x16 acc = (f32x16){};
+    if (st_on) ts[2] = stamp();
+    for (int c = 0; c < nchl; ++c) {
+      __builtin_amdgcn_s_barrier();  // chunk c landed; every consumer is done with chunk c-1
+      asm volatile("" ::: "memory");
+      if (st_on && c == 0) ts[3] = stamp();
+      if (L.dbg == 2) continue;
+      const unsigned sb = (c % NSLOT) * SLOT;
+      switch ((c >> 2) ? code1 : code0) {
+        case 0: chunk_mma<0, 0>(acc, sb, akr, bkr, akc, bkc); break;
+        case 1: chunk_mma<1, 0>(acc, sb, akr, bkr, akc, bkc); break;
+        case 2: chunk_mma<0, 1>(acc, sb, akr, bkr, akc, bkc); break;
+        default: chunk_mma<1, 1>(acc, sb, akr, bkr, akc, bkc); break;
+      }
+      if (st_on && c == 0) ts[4] = stamp();
+    }
+    if (st_on) ts[5] = stamp();
+    const int h = lane >> 5, cc = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) ep[(wm * 32 + acc_row(r, h)) * EROW + wn * 32 + cc] = acc[r];
+  }
+  __syncthreads();  // the tile is in `ep`; every wave (producers too) takes one 8-element row piece
+  if (L.dbg == 3 || !epi) return;
+  const float diag = J.diag, e1s = J.e1s, e2s = J.e2s;
+  float ic = 1.f;
+  if (need_c) ic = nbh <= 64 ? 1.f / (wave_max(mcv) * wave_max(mrv)) : inv_c(L.maxima, nbh);
+  const float alpha = J.alpha * powc(ic, J.alpha_cpow);
+  const float e1m = powc(ic, J.e1_cpow);
+  auto edecode = [&](const f32x4 (&r)[2], int f32, float* v) {
+    if (f32) {
+      const f32x4 x = r[0], y = r[1];
+      v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
+    } else {
+      const bf16x8 hh = __builtin_bit_cast(bf16x8, r[0]), ll = __builtin_bit_cast(bf16x8, r[1]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (float)hh[e] + (float)ll[e];
+    }
+  };
+  {
+    const int row = m0 + lr, col = n0 + lc;
+    const bool dg = row >= col && row < col + 8;  // the piece holds the diagonal element (row, row)
+    float s[8], e1v[8], e2v[8], v[8];
+    {
+      const f32x4 x0 = *(const f32x4*)(ep + lr * EROW + lc), x1 = *(const f32x4*)(ep + lr * EROW + lc + 4);
+      s[0] = x0[0]; s[1] = x0[1]; s[2] = x0[2]; s[3] = x0[3]; s[4] = x1[0]; s[5] = x1[1]; s[6] = x1[2]; s[7] = x1[3];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s[e] *= alpha; e1v[e] = 0.f; e2v[e] = 0.f; }
+    if (e1p) {
+      edecode(e1raw, e1f, e1v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) e1v[e] *= e1m;
+    }
+    if (e2p) edecode(e2raw, e2f, e2v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = s[e] + e1s * e1v[e] + e2s * e2v[e];
+    if (dg) v[row - col] += diag;
+    if (J.c_f32) store_f8((float*)J.c, eoff, v); else store_split8((bf16*)J.c, plane, eoff, v);
+    if (J.cf) store_f8(J.cf, eoff, v);
+    if (J.c2) {
+      float w[8];
+      const float c2a = J.c2_alpha, c2e = J.c2_e1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = c2a * s[e] + c2e * e1v[e];
+      if (dg) w[row - col] += J.c2_diag;
+      store_split8(J.c2, plane, eoff, w);
+    }
+    if (J.c3) {
+      float w[8];
+      const float c3e = J.c3_e1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) w[e] = c3e * e1v[e];
+      store_split8(J.c3, plane, eoff, w);
+    }
+  }
+  if (st_on && wv < 4) {
+    ts[6] = stamp();
+    ts[7] = rstamp();
+    if (lane == 0) {
+      unsigned long long* o = L.stamps + (((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wv) * 8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = ts[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward of Z_0 = X^T / c (c = max_i rowsum|X|_i * max_j colsum|X|_j) and of A2 = softmax.
+// part[bh*16 + y] = sum over rows i of slice y of G0[i][j] * X[j][i]   (grid (nbh, 16))
+__global__ __launch_bounds__(256) void pinv_c_dot_kernel(const bf16* __restrict__ G0, long long plane,
+                                                         const float* __restrict__ X, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int bh = blockIdx.x, i0 = blockIdx.y * 16, j = threadIdx.x;
+  const size_t hb = (size_t)bh * MAT;
+  float xs[16];
+  {
+    const float* xr = X + hb + (size_t)j * NL + i0;  // X[j][i0..i0+15]
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = *(const f32x4*)(xr + 4 * q);
+      xs[4 * q] = v[0]; xs[4 * q + 1] = v[1]; xs[4 * q + 2] = v[2]; xs[4 * q + 3] = v[3];
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int ii = 0; ii < 16; ++ii) {
+    const size_t o = hb + (size_t)(i0 + ii) * NL + j;
+    s += ((float)G0[o] + (float)G0[o + plane]) * xs[ii];
+  }
+  s = wave_sum(s);
+  if ((j & 63) == 0) red[j >> 6] = s;
+  __syncthreads();
+  if (j == 0) part[bh * 16 + blockIdx.y] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// dX[i][j] = dXc[i][j] + G0[j][i]/c + sign(X_ij) (tie_c(i) dMc/nc + tie_r(j) dMr/nr),
+// dc = -sum(G0 o Z0)/c = -T/c^2,  dMc = dc * maxr, dMr = dc * maxc  (max ties share the gradient);
+// softmax != 0: out = X o (dX - rowsum(X o dX)) (the backward of A2 = softmax, X = A2), else out = dX.
+// grid (nbh, 16), block 256: 16 rows of one head, thread = column j.
+__global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __restrict__ X, const float* __restrict__ sums,
+                                                             const float* __restrict__ maxima, const bf16* __restrict__ G0,
+                                                             long long plane, const float* __restrict__ part, int nbh,
+                                                             const float* __restrict__ dXc, int softmax,
+                                                             float* __restrict__ out) {
+  __shared__ float tile[NL][17];
+  __shared__ float red[4][16];
+  __shared__ float bc[4];
+  const int bh = blockIdx.x, i0 = blockIdx.y * 16, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const size_t hb = (size_t)bh * MAT;
+  // G0[j][i0 + ii] -> tile[j][ii]
+  for (int e = t; e < NL * 16; e += 256) {
+    const int j = e >> 4, ii = e & 15;
+    const size_t o = hb + (size_t)j * NL + i0 + ii;
+    tile[j][ii] = (float)G0[o] + (float)G0[o + plane];
+  }
+  // maxima, tie counts and the fixed-order sum of the partial dots
+  float mc = -INFINITY, mr = -INFINITY;
+  for (int h = 0; h < nbh; ++h) { mc = fmaxf(mc, maxima[h]); mr = fmaxf(mr, maxima[nbh + h]); }
+  float nc = 0.f, nr = 0.f, ps = 0.f;
+  for (int e = t; e < nbh * NL; e += 256) { nc += sums[e] == mc; nr += sums[nbh * NL + e] == mr; }
+  for (int e = t; e < nbh * 16; e += 256) ps += part[e];
+  nc = wave_sum(nc); nr = wave_sum(nr); ps = wave_sum(ps);
+  if (lane == 0) { red[wave][0] = nc; red[wave][1] = nr; red[wave][2] = ps; }
+  __syncthreads();
+  if (t == 0) {
+    bc[0] = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    bc[1] = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+    bc[2] = (red[0][2] + red[1][2]) + (red[2][2] + red[3][2]);
+  }
+  __syncthreads();
+  const float c = mc * mr, ic = 1.f / c;
+  const float dc = -bc[2] * ic * ic;
+  const float dMc = dc * mr / bc[0], dMr = dc * mc / bc[1];
+  const float* rs = sums + (size_t)bh * NL;
+  const float* cs = sums + (size_t)(nbh + bh) * NL;
+  const float tie_r = cs[t] == mr ? dMr : 0.f;
+  float dx[16], xv[16];
+#pragma unroll
+  for (int ii = 0; ii < 16; ++ii) {
+    const int i = i0 + ii;
+    const size_t off = hb + (size_t)i * NL + t;
+    xv[ii] = X[off];
+    const float sg = xv[ii] > 0.f ? 1.f : (xv[ii] < 0.f ? -1.f : 0.f);
+    const float tie_c = rs[i] == mc ? dMc : 0.f;
+    dx[ii] = dXc[off] + tile[t][ii] * ic + sg * (tie_c + tie_r);
+  }
+  if (!softmax) {
+#pragma unroll
+    for (int ii = 0; ii < 16; ++ii) out[hb + (size_t)(i0 + ii) * NL + t] = dx[ii];
+    return;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int ii = 0; ii < 16; ++ii) {
+    const float d = wave_sum(xv[ii] * dx[ii]);
+    if (lane == 0) red[wave][ii] = d;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int ii = 0; ii < 16; ++ii) {
+    const float rd = (red[0][ii] + red[1][ii]) + (red[2][ii] + red[3][ii]);
+    out[hb + (size_t)(i0 + ii) * NL + t] = xv[ii] * (dx[ii] - rd);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+struct Split {  // one split matrix slot: nbh * MAT fp32-equivalents = hi plane + lo plane
+  bf16* p;
+};
+
+SOp op(const void* p, int kr) { return SOp{(const bf16*)p, kr, 0}; }
+
+SJob product(SOp a, SOp b, void* c, float alpha, float diag = 0.f) {
+  SJob j{};
+  j.kind = KIND_PRODUCT;
+  j.nterms = 1;
+  j.a[0] = a; j.b[0] = b;
+  j.c = c;
+  j.alpha = alpha; j.diag = diag;
+  return j;
+}
+
+struct Launcher {
+  SLaunch L{};
+  explicit Launcher(int nbh, long long plane, const float* maxima) {
+    L.nbh = nbh; L.plane = plane; L.maxima = maxima;
+    L.dbg = g_split_dbg;
+    L.stamps = g_split_stamps;
+  }
+  void add(const SJob& j) { L.j[L.njobs++] = j; }
+  int go(hipStream_t st) {
+    tm_allow_smem(pinv_stage_kernel, STAGE_LDS + EPI_LDS);
+    const dim3 grid(16 * L.nbh, L.njobs);
+    pinv_stage_kernel<<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
+    TM_CHECK_LAUNCH();
+    if (g_split_stamps) g_split_stamps += (size_t)grid.x * grid.y * 4 * 8;  // the next launch's stamps follow
+    return 0;
+  }
+};
+
+// saved-buffer layout (floats); every slot is nbh*MAT floats
+struct FwdLayout {
+  long long mat;
+  int iters;
+  float* base;
+  float* zf() const { return base; }                                      // Z_iters fp32
+  bf16* z(int k) const { return (bf16*)(base + (long long)k * mat); }     // Z_k split, k = 1..iters
+  bf16* p(int k) const { return (bf16*)(base + (long long)(iters + 1 + k) * mat); }       // P_k, k = 0..iters-1
+  bf16* t3(int k) const { return (bf16*)(base + (long long)(2 * iters + 1 + k) * mat); }
+  bf16* t5(int k) const { return (bf16*)(base + (long long)(3 * iters + 1 + k) * mat); }
+  bf16* scratch(int i) const { return (bf16*)(base + (long long)(4 * iters + 1 + i) * mat); }
+  float* sums() const { return base + (long long)(4 * iters + 3) * mat; }
+  float* maxima(int nbh) const { return sums() + 2LL * nbh * NL; }
+};
+
+FwdLayout fwd_layout(float* saved, int nbh, int iters) {
+  FwdLayout f;
+  f.mat = (long long)nbh * MAT;
+  f.iters = iters;
+  f.base = saved;
+  return f;
+}
+
+}  // namespace
+
+extern "C" long long tm_pinv_split_saved_floats(int nbh, int iters) {
+  return (4LL * iters + 3) * nbh * MAT + 2LL * nbh * NL + 2LL * nbh + 64;
+}
+
+// X: fp32 [nbh][256][256]; Xs: its split planes (tm_nys_sim2_softmax_split).  saved: see FwdLayout;
+// Z_iters (fp32) sits at the start of `saved`.
+extern "C" int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* saved, void* stream) {
+  TM_REQUIRE(X && Xs && saved && nbh > 0 && iters >= 1, "pinv_fwd_split: bad args (iters >= 1)");
+  TM_REQUIRE(((uintptr_t)Xs % 16) == 0 && ((uintptr_t)saved % 16) == 0, "pinv_fwd_split: 16-B aligned buffers");
+  hipStream_t st = (hipStream_t)stream;
+  const FwdLayout F = fwd_layout(saved, nbh, iters);
+  const long long plane = F.mat;
+  float* maxima = F.maxima(nbh);
+  {  // L1: S = X X^T, |X| sums
+    Launcher l(nbh, plane, nullptr);
+    l.add(product(op(Xs, 0), op(Xs, 0), F.scratch(0), 1.f));
+    SJob s{};
+    s.kind = KIND_ABSSUMS;
+    l.add(s);
+    l.L.X = X; l.L.sums = F.sums(); l.L.maxima_out = maxima;
+    if (int rc = l.go(st)) return rc;
+  }
+  for (int k = 0; k < iters; ++k) {
+    bf16* R = F.scratch((k + 1) & 1);
+    {  // A_k: R = P P (T3 = R - 7P + 15I); Z_k = 0.25 Z_{k-1} T5_{k-1}
+      Launcher l(nbh, plane, maxima);
+      SJob r;
+      if (k == 0) {  // P_0 = S / c: R = S S / c^2, T3 = R - 7 S/c + 15I, P_0 written as a side output
+        r = product(op(F.scratch(0), 0), op(F.scratch(0), 1), R, 1.f);
+        r.alpha_cpow = 2;
+        r.e1 = F.scratch(0); r.e1_cpow = 1;
+        r.c3 = F.p(0); r.c3_e1 = 1.f;
+      } else {
+        r = product(op(F.p(k), 0), op(F.p(k), 1), R, 1.f);
+        r.e1 = F.p(k);
+      }
+      r.c2 = F.t3(k); r.c2_alpha = 1.f; r.c2_diag = 15.f; r.c2_e1 = -7.f;
+      l.add(r);
+      if (k >= 1) {
+        SJob z = k == 1 ? product(op(Xs, 1), op(F.t5(0), 1), F.z(1), 0.25f)           // Z_0 = X^T / c
+                        : product(op(F.z(k - 1), 0), op(F.t5(k - 1), 1), F.z(k), 0.25f);
+        if (k == 1) z.alpha_cpow = 1;
+        l.add(z);
+      }
+      if (int rc = l.go(st)) return rc;
+    }
+    {  // B_k: T5 = 13I - P T3; P_{k+1} = 3.25 P - 0.25 R T3
+      Launcher l(nbh, plane, maxima);
+      l.add(product(op(F.p(k), 0), op(F.t3(k), 1), F.t5(k), -1.f, 13.f));
+      if (k + 1 < iters) {
+        SJob p = product(op(R, 0), op(F.t3(k), 1), F.p(k + 1), -0.25f);
+        p.e1 = F.p(k); p.e1s = 3.25f;
+        l.add(p);
+      }
+      if (int rc = l.go(st)) return rc;
+    }
+  }
+  {  // F: Z_iters = 0.25 Z_{iters-1} T5_{iters-1}  (split + fp32)
+    Launcher l(nbh, plane, maxima);
+    SJob z = iters == 1 ? product(op(Xs, 1), op(F.t5(0), 1), F.z(1), 0.25f)
+                        : product(op(F.z(iters - 1), 0), op(F.t5(iters - 1), 1), F.z(iters), 0.25f);
+    if (iters == 1) z.alpha_cpow = 1;
+    z.cf = F.zf();
+    l.add(z);
+    if (int rc = l.go(st)) return rc;
+  }
+  return 0;
+}
+
+// workspace: G, dT5, dZa, dP, dT3 (split) + dX (fp32) + partial dots
+extern "C" long long tm_pinv_bwd_split_workspace_floats(int nbh) {
+  return 6LL * nbh * MAT + nbh * 16LL + 64;
+}
+
+// dZ: the gradient w.r.t. Z_iters as split planes, placed by the caller at the start of `work`
+// (tm_bmm with c_split).  out: dL/dX (softmax == 0) or dL/d(sim2 logits) = softmax backward of
+// A2 = X (softmax != 0), fp32.
+extern "C" int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int iters, const float* saved, float* work,
+                                 int softmax, float* out, void* stream) {
+  TM_REQUIRE(X && Xs && saved && work && out && nbh > 0 && iters >= 1, "pinv_bwd_split: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  const FwdLayout F = fwd_layout((float*)saved, nbh, iters);
+  const long long mat = F.mat, plane = mat;
+  const float* maxima = F.maxima(nbh);
+  bf16* G = (bf16*)work;
+  bf16* dT5 = (bf16*)(work + mat);
+  bf16* dZa = (bf16*)(work + 2 * mat);
+  bf16* dP = (bf16*)(work + 3 * mat);
+  bf16* dT3 = (bf16*)(work + 4 * mat);
+  float* dXc = work + 5 * mat;
+  float* part = work + 6 * mat;
+  for (int k = iters - 1; k >= 0; --k) {
+    {  // dT5 = 0.25 Z_k^T G ; dZa = 0.25 G T5_k^T
+      Launcher l(nbh, plane, maxima);
+      SJob a = k == 0 ? product(op(Xs, 0), op(G, 1), dT5, 0.25f)          // Z_0^T = X / c
+                      : product(op(F.z(k), 1), op(G, 1), dT5, 0.25f);
+      if (k == 0) a.alpha_cpow = 1;
+      l.add(a);
+      l.add(product(op(G, 0), op(F.t5(k), 0), dZa, 0.25f));
+      if (int rc = l.go(st)) return rc;
+    }
+    {  // dP = -dT5 T3^T ; dT3 = -P^T dT5
+      Launcher l(nbh, plane, maxima);
+      l.add(product(op(dT5, 0), op(F.t3(k), 0), dP, -1.f));
+      l.add(product(op(F.p(k), 1), op(dT5, 1), dT3, -1.f));
+      if (int rc = l.go(st)) return rc;
+    }
+    {  // dP += dT3 P^T + P^T dT3 - 7 dT3   (T3 = P P - 7P + 15I)
+      Launcher l(nbh, plane, maxima);
+      SJob j = product(op(dT3, 0), op(F.p(k), 0), dP, 1.f);
+      j.nterms = 2;
+      j.a[1] = op(F.p(k), 1); j.b[1] = op(dT3, 1);
+      j.e1 = dP; j.e1s = 1.f;
+      j.e2 = dT3; j.e2s = -7.f;
+      l.add(j);
+      if (int rc = l.go(st)) return rc;
+    }
+    {  // dX (+)= dP Z_k^T ; G = dZa + X^T dP
+      Launcher l(nbh, plane, maxima);
+      SJob a = k == 0 ? product(op(dP, 0), op(Xs, 1), dXc, 1.f)            // Z_0^T = X / c
+                      : product(op(dP, 0), op(F.z(k), 0), dXc, 1.f);
+      if (k == 0) a.alpha_cpow = 1;
+      a.c_f32 = 1;
+      if (k != iters - 1) { a.e1 = dXc; a.e1_f32 = 1; a.e1s = 1.f; }
+      l.add(a);
+      SJob g = product(op(Xs, 1), op(dP, 1), G, 1.f);
+      g.e1 = dZa; g.e1s = 1.f;
+      l.add(g);
+      if (int rc = l.go(st)) return rc;
+    }
+  }
+  // Z_0 = X^T / c: the c gradient's partial sums, then the transpose term, the max-tie terms and the softmax
+  pinv_c_dot_kernel<<<dim3(nbh, 16), 256, 0, st>>>(G, plane, X, part);
+  TM_CHECK_LAUNCH();
+  pinv_apply_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, F.sums(), maxima, G, plane, part, nbh, dXc, softmax, out);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" void tm_debug_set_split_variant(int v) { g_split_dbg = v; }
+// diagnostic: per-wave stamps (8 x u64 per wave, 8 waves per workgroup) of every later stage launch; null: off
+extern "C" void tm_debug_set_split_stamps(unsigned long long* buf) { g_split_stamps = buf; }
+
+// fp32 -> split planes (hi at dst, lo at dst + count), count a multiple of 8
+__global__ void split_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long count) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= count) return;
+  float v[8];
+  load_f8(x, i, v);
+  store_split8(y, count, i, v);
+}
+
+extern "C" int tm_split_f32(const float* x, void* y, long long count, void* stream) {
+  TM_REQUIRE(count % 8 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 16) == 0, "split_f32: count % 8, alignment");
+  if (count == 0) return 0;
+  split_kernel<<<(unsigned)((count / 8 + 255) / 256), 256, 0, (hipStream_t)stream>>>(x, (bf16*)y, count);
+  TM_CHECK_LAUNCH();
+  return 0;
+}

@@ -218,7 +218,6 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
     kl_t = pool(nbh * NL * DH, tdtype).view(nbh, NL, DH)
     _lib.call("tm_nys_landmarks", dt_code, _p(q), _p(k), nbh, n, _p(ql), _p(kl), _p(ql_t), _p(kl_t), st)
     a2 = pool(nbh * NL * NL).view(nbh, NL, NL)
-    saved = pool(_lib.query("tm_pinv_saved_floats", nbh, PINV_ITERS))
     w = pool(nbh * NL * DH).view(nbh, NL, DH)
     lse3 = pool(nbh * NL)
     work = pool(_lib.query("tm_nys_a3_workspace", nbh, n) // 4)
@@ -226,10 +225,20 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
     #  the step -- the chain's launches then wait for CUs -- so the path stays serial)
     with probe("a3_fwd"):
         _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
-    _lib.call("tm_nys_sim2_softmax", _p(ql), _p(kl), nbh, _p(a2), st)
     prec = 1 if dt_code == BF16 else 0
-    _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, prec, _p(saved), st)
-    z = saved[PINV_ITERS * nbh * NL * NL:(PINV_ITERS + 1) * nbh * NL * NL].view(nbh, NL, NL)
+    a2s = None
+    if prec:
+        # bench mode: the pseudo-inverse chain on split bf16 hi/lo operands (pinv_split.hip)
+        a2s = pool(nbh * NL * NL)   # hi + lo bf16 planes = one fp32 matrix's bytes
+        saved = pool(_lib.query("tm_pinv_split_saved_floats", nbh, PINV_ITERS))
+        _lib.call("tm_nys_sim2_softmax_split", _p(ql), _p(kl), nbh, _p(a2), _p(a2s), st)
+        _lib.call("tm_pinv_fwd_split", _p(a2), _p(a2s), nbh, PINV_ITERS, _p(saved), st)
+        z = saved[:nbh * NL * NL].view(nbh, NL, NL)
+    else:
+        saved = pool(_lib.query("tm_pinv_saved_floats", nbh, PINV_ITERS))
+        _lib.call("tm_nys_sim2_softmax", _p(ql), _p(kl), nbh, _p(a2), st)
+        _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, prec, _p(saved), st)
+        z = saved[PINV_ITERS * nbh * NL * NL:(PINV_ITERS + 1) * nbh * NL * NL].view(nbh, NL, NL)
     y = pool(nbh * NL * DH).view(nbh, NL, DH)
     bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh, prec)
     y_t = pool(nbh * NL * DH, tdtype)
@@ -239,8 +248,8 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
     with probe("a1_fwd"):
         _lib.call("tm_nys_a1_fwd", dt_code, _p(q), _p(v), _p(kl_t), _p(y_t), _p(wconv), nbh, nh, n, _p(merged),
                   _p(lse1), st)
-    state = dict(ql=ql, kl=kl, ql_t=ql_t, kl_t=kl_t, a2=a2, pinv=saved, z=z, w=w, lse3=lse3, y=y, y_t=y_t,
-                 lse1=lse1)
+    state = dict(ql=ql, kl=kl, ql_t=ql_t, kl_t=kl_t, a2=a2, a2s=a2s, pinv=saved, z=z, w=w, lse3=lse3, y=y,
+                 y_t=y_t, lse1=lse1)
     return merged, state
 
 
@@ -285,12 +294,19 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         _lib.call("tm_nys_a3_bwd", dt_code, _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]),
                   _p(d3), nbh, nh, n, _p(dk), _p(dv), _p(work3), _p(dql3), 0, st)
     # pseudo-inverse backward -> dA2, then softmax backward
-    da2 = pool(mat).view(nbh, NL, NL)
-    pwork = pool(_lib.query("tm_pinv_bwd_workspace_floats", nbh))
-    _lib.call("tm_pinv_bwd", _p(state["a2"]), nbh, PINV_ITERS, prec, _p(state["pinv"]), _p(dz), _p(pwork),
-              _p(da2), st)
     ds2 = pool(mat).view(nbh, NL, NL)
-    _lib.call("tm_softmax_bwd_rows256", _p(state["a2"]), _p(da2), _p(ds2), nbh * NL, st)
+    if state["a2s"] is not None:
+        # split operands; the softmax backward is fused into the chain's last launch
+        pwork = pool(_lib.query("tm_pinv_bwd_split_workspace_floats", nbh))
+        _lib.call("tm_split_f32", _p(dz), _p(pwork), mat, st)
+        _lib.call("tm_pinv_bwd_split", _p(state["a2"]), _p(state["a2s"]), nbh, PINV_ITERS, _p(state["pinv"]),
+                  _p(pwork), 1, _p(ds2), st)
+    else:
+        da2 = pool(mat).view(nbh, NL, NL)
+        pwork = pool(_lib.query("tm_pinv_bwd_workspace_floats", nbh))
+        _lib.call("tm_pinv_bwd", _p(state["a2"]), nbh, PINV_ITERS, prec, _p(state["pinv"]), _p(dz), _p(pwork),
+                  _p(da2), st)
+        _lib.call("tm_softmax_bwd_rows256", _p(state["a2"]), _p(da2), _p(ds2), nbh * NL, st)
     dql = pool(nbh * NL * DH).view(nbh, NL, DH)
     bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL, E1=dql3, e1=1.0),
          bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
