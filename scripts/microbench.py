@@ -113,18 +113,11 @@ def main():
     case("bmm 2-job 256^3 x8", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
                                               E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh), 2 * f)
     case("bmm NN 256^3 x8 [bf16x3]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh, 1), f)
-    for var, nm in ((1, "no loads/MFMA"), (2, "loads only"), (4, "store only"), (5, "A loads only"),
-                    (6, "B loads only"), (7, "tiny footprint"), (8, "B as NT")):
-        _lib.lib().tm_debug_set_variant(0, var)
-        case(f"bmm NN+E1 bf16x3 [{nm}]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256, E1=Y2, e1=1.0)],
-                                                         nbh, 1), f)
-    _lib.lib().tm_debug_set_variant(0, 0)
     case("bmm NT bf16x3", lambda: E.bmm([E.bmm_job(X, 0, Z, 1, P, 256, 256, 256)], nbh, 1), f)
     case("bmm TN bf16x3", lambda: E.bmm([E.bmm_job(X, 1, Z, 0, P, 256, 256, 256)], nbh, 1), f)
     case("bmm Y=ZW bf16x3", lambda: E.bmm([E.bmm_job(Z, 0, W, 0, Y, 256, 64, 256)], nbh, 1), f // 4)
     case("bmm dependent pair bf16x3 (per bmm)", lambda: (E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256)], nbh, 1),
                                                         E.bmm([E.bmm_job(X, 0, P, 0, Z2, 256, 256, 256)], nbh, 1)), 2 * f)
-    _lib.lib().tm_debug_set_variant(0, 0)
     case("bmm NN+E1 bf16x3", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256, E1=Y2, e1=1.0)], nbh, 1), f)
     case("bmm 2-job 256^3 x8 [bf16x3]", lambda: E.bmm([E.bmm_job(X, 0, Z, 0, P, 256, 256, 256),
                                               E.bmm_job(Z, 1, X, 0, Y.new_empty(nbh, 256, 256), 256, 256, 256)], nbh, 1), 2 * f)
@@ -134,14 +127,11 @@ def main():
     pwork = torch.empty(_lib.query("tm_pinv_bwd_workspace_floats", nbh), device=dev)
     pdz = torch.randn(nbh, 256, 256, device=dev) * 1e-3
     pdX = torch.empty(nbh, 256, 256, device=dev)
-    for team, nm in ((1, "persistent"), (2, "persistent, no sync"), (0, "per-launch")):
-        _lib.lib().tm_debug_set_variant(3, team)
-        case(f"pinv_fwd fp32 [{nm}]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 0, E._p(saved), st()), 24 * f)
-        case(f"pinv_fwd bf16x3 [{nm}]", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 1, E._p(saved), st()),
-             24 * f)
-        case(f"pinv_bwd bf16x3 [{nm}]", lambda: _lib.call("tm_pinv_bwd", E._p(X), nbh, 6, 1, E._p(saved), E._p(pdz),
-                                                           E._p(pwork), E._p(pdX), st()), 28 * f)
-    _lib.lib().tm_debug_set_variant(3, 0)
+    case("pinv_fwd fp32", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 0, E._p(saved), st()), 24 * f)
+    case("pinv_fwd bf16x3 (fp32 storage)", lambda: _lib.call("tm_pinv_fwd", E._p(X), nbh, 6, 1, E._p(saved), st()),
+         24 * f)
+    case("pinv_bwd bf16x3 (fp32 storage)", lambda: _lib.call("tm_pinv_bwd", E._p(X), nbh, 6, 1, E._p(saved),
+                                                              E._p(pdz), E._p(pwork), E._p(pdX), st()), 28 * f)
     # split-operand chain (pinv_split.hip): 14 launches forward, 4 per iteration + 2 backward
     Xs = torch.empty(2 * nbh * 65536, dtype=torch.bfloat16, device=dev)
     _lib.call("tm_split_f32", E._p(X), E._p(Xs), nbh * 65536, st())

@@ -73,6 +73,41 @@ def test_device_lookahead_matches_reference_semantics():
         torch.testing.assert_close(pa, pb, rtol=0, atol=1e-7)
 
 
+@pytest.mark.parametrize("base", ["radam", "sgd"])
+def test_lookahead_state_dict_roundtrip(base):
+    """state_dict -> fresh optimizer -> load_state_dict resumes bit-identically: base moments,
+    slow weights, the device step counter and the lookahead_* group fields all survive
+    (the reference wrapper saves base state + slow state, code/MyOptimizer/lookahead.py:56-88)."""
+    from transmil_deepgraft_amd.interface import Lookahead, add_weight_decay
+
+    def make(m):
+        groups = add_weight_decay(m, 0.01)
+        inner = torch.optim.RAdam(groups, lr=2e-3) if base == "radam" else torch.optim.SGD(groups, lr=1e-2,
+                                                                                          momentum=0.9)
+        return Lookahead(inner, k=3)
+
+    a = _toy(3)
+    opt_a = make(a)
+    for step in range(7):           # two syncs done, one step into the third window
+        _grads(a, step)
+        opt_a.step()
+    import copy
+    sd = copy.deepcopy(opt_a.state_dict())   # as a checkpoint file would hold it (no shared tensors)
+    assert set(sd) == {"state", "slow_state", "param_groups"} and sd["slow_state"]
+    b = _toy(9)
+    b.load_state_dict(a.state_dict())
+    opt_b = make(b)
+    opt_b.load_state_dict(sd)
+    assert opt_b.param_groups[0]["lookahead_step"] == 7
+    for step in range(7, 13):
+        _grads(a, step)
+        _grads(b, step)
+        opt_a.step()
+        opt_b.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=0, atol=0)
+
+
 def test_task_surface_cpu():
     """training_step(batch) -> loss [1]; configure_optimizers() -> ([opt], [sched dict])."""
     from transmil_deepgraft_amd.interface import TransMILTask, Lookahead

@@ -159,6 +159,9 @@ extern "C" int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* str
   for (int i = 0; i < table->count; ++i) {
     TM_REQUIRE(table->src[i] && table->dst[i], "cast_many: null tensor");
     TM_REQUIRE(table->offset[i] == off && table->offset[i + 1] >= off, "cast_many: offsets must be a prefix sum");
+    // a thread converts 4 consecutive elements of the concatenated index space: a tensor that
+    // ended mid-quad would leave the next one's first elements unconverted
+    TM_REQUIRE(table->offset[i + 1] % 4 == 0, "cast_many: every tensor's element count must be a multiple of 4");
     off = table->offset[i + 1];
   }
   if (off == 0) return 0;

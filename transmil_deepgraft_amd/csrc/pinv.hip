@@ -12,8 +12,10 @@
 // P_{k+1} = 3.25 P - 0.25 R T3}: 2 dependent launches instead of 4 (14 in all instead of 24);
 // the saved P / T3 / T5 / Z are the same tensors the backward uses.
 //
-// Always fp32, on v_mfma_f32_32x32x2_f32 (exact fp32 fmaf chains): the
-// attn2 entries sit in a ~5 % band around 1/256 and do not survive bf16.
+// prec 0 (parity mode): exact fp32 on v_mfma_f32_32x32x2_f32 (fmaf chains); prec 1: the
+// bf16x3 split of fp32 storage (the bench mode runs pinv_split.hip instead, which keeps
+// the split planes in memory).  The attn2 entries sit in a ~5 % band around 1/256 and do
+// not survive plain bf16.
 // Every product is a 256x256(x64) fp32 batch over B*heads; one workgroup
 // computes one 32x32 output tile with its 4 waves splitting K (reduced in LDS
 // in a fixed order), batch index = blockIdx % nbatch so all tiles of one head
@@ -75,11 +77,11 @@ TM_DEV void mma_f32_step(f32x16& acc, const f32x8& a, const f32x8& b) {
 // One workgroup = one 32x32 output tile of one batch entry; its 8 waves take the
 // k-steps round-robin (s = wave, wave + 8, ...; every fragment requested before the
 // first MFMA) and are summed in LDS in a fixed order.  4 waves per SIMD hide the L2
-// latency of the operand loads behind each other's MFMAs.
+// latency of the operand loads behind each other's MFMAs.  (Generic layouts; the
+// layout-specialised bmm_spec_kernel below serves every product the engine issues.)
 constexpr int BMM_WAVES = 8;
-int g_bmm_variant = 0;
 
-template <int PREC, int VAR = 0>  // VAR (ablation): 1 no loads/MFMA, 2 loads only, 3 no E terms, 4 store only
+template <int PREC>
 __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
   __shared__ float red[BMM_WAVES][16][64];
   int b = blockIdx.x;
@@ -93,45 +95,24 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
   const int nterms = J.A2 ? 2 : 1;
   const int nsteps = J.K * nterms / 16;
   f32x16 acc = (f32x16){};
-  if constexpr (VAR == 4) {
-    const int row = tm * 32 + (tid >> 5) % 32, col = tn * 32 + (tid & 31);
-    if (tid < 1024) J.C[(size_t)bh * J.sc + (size_t)row * J.ldc + col] = 0.f;
-    return;
-  }
   f32x8 af[4], bfr[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int st = wave + BMM_WAVES * i;
-    if (VAR != 1 && st < nsteps) {
+    if (st < nsteps) {
       const int kk = st * 16;
       const int term = kk / J.K, kl = kk % J.K;
       const float* A = term ? J.A2 + bh * J.sa2 : J.A + bh * J.sa;
       const float* B = term ? J.B2 + bh * J.sb2 : J.B + bh * J.sb;
       const int ta = term ? J.ta2 : J.ta, tb = term ? J.tb2 : J.tb;
       const int lda = term ? J.lda2 : J.lda, ldb = term ? J.ldb2 : J.ldb;
-      if constexpr (VAR == 7) {  // tiny footprint: every block reads tile (0,0) of batch 0
-        af[i] = frag_a(J.A, ta, lda, r, kl + 8 * h);
-        bfr[i] = frag_b(J.B, tb, ldb, kl + 8 * h, r);
-      } else if constexpr (VAR == 8) {  // B read as if stored transposed (contiguous 32 B per lane)
-        af[i] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
-        bfr[i] = frag_b(B, 1, ldb, kl + 8 * h, tn * 32 + r);
-      } else {
-        if constexpr (VAR != 6) af[i] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
-        else af[i] = (f32x8){(float)lane, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
-        if constexpr (VAR != 5) bfr[i] = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
-        else bfr[i] = (f32x8){(float)lane, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
-      }
+      af[i] = frag_a(A, ta, lda, tm * 32 + r, kl + 8 * h);
+      bfr[i] = frag_b(B, tb, ldb, kl + 8 * h, tn * 32 + r);
     }
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (wave + BMM_WAVES * i < nsteps) {
-      if constexpr (VAR == 0 || VAR == 3 || VAR >= 5) mma_f32_step<PREC>(acc, af[i], bfr[i]);
-      if constexpr (VAR == 2) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += af[i][e] * bfr[i][e];
-      }
-    }
+    if (wave + BMM_WAVES * i < nsteps) mma_f32_step<PREC>(acc, af[i], bfr[i]);
 #pragma unroll
   for (int i = 0; i < 16; ++i) red[wave][i][lane] = acc[i];
   __syncthreads();
@@ -145,9 +126,9 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
     const size_t off = (size_t)bh * J.sc + (size_t)row * J.ldc + col;
     float v = J.alpha * s;
     if (row == col) v += J.diag;
-    const float e1v = (VAR != 3 && J.E1) ? J.E1[off] : 0.f;
+    const float e1v = J.E1 ? J.E1[off] : 0.f;
     v += J.e1 * e1v;
-    if (VAR != 3 && J.E2) v += J.e2 * J.E2[off];
+    if (J.E2) v += J.e2 * J.E2[off];
     J.C[off] = v;
     if (J.C2) J.C2[off] = J.c2_alpha * s + (row == col ? J.c2_diag : 0.f) + J.c2_e1 * e1v;
   }
@@ -393,32 +374,17 @@ int launch_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, hipStrea
     if (i == 0) jp.tiles0 = tiles;
     total += tiles * nbatch;
   }
-  if (g_bmm_variant == 0) {
-    const int c0 = bmm_code(jobs[0]), c1 = njobs > 1 ? bmm_code(jobs[1]) : -1;
-    if (c0 >= 0 && (njobs == 1 || c1 >= 0)) {
-      const bool ok = prec == 1 ? launch_spec<1>(jp, c0, c1, total, nbatch, st)
-                                : launch_spec<0>(jp, c0, c1, total, nbatch, st);
-      if (ok) {
-        TM_CHECK_LAUNCH();
-        return 0;
-      }
+  const int c0 = bmm_code(jobs[0]), c1 = njobs > 1 ? bmm_code(jobs[1]) : -1;
+  if (c0 >= 0 && (njobs == 1 || c1 >= 0)) {
+    const bool ok = prec == 1 ? launch_spec<1>(jp, c0, c1, total, nbatch, st)
+                              : launch_spec<0>(jp, c0, c1, total, nbatch, st);
+    if (ok) {
+      TM_CHECK_LAUNCH();
+      return 0;
     }
   }
-  if (prec == 1) {
-    switch (g_bmm_variant) {
-      case 1: bmm_kernel<1, 1><<<total, 512, 0, st>>>(jp, nbatch); break;
-      case 2: bmm_kernel<1, 2><<<total, 512, 0, st>>>(jp, nbatch); break;
-      case 3: bmm_kernel<1, 3><<<total, 512, 0, st>>>(jp, nbatch); break;
-      case 4: bmm_kernel<1, 4><<<total, 512, 0, st>>>(jp, nbatch); break;
-      case 5: bmm_kernel<1, 5><<<total, 512, 0, st>>>(jp, nbatch); break;
-      case 6: bmm_kernel<1, 6><<<total, 512, 0, st>>>(jp, nbatch); break;
-      case 7: bmm_kernel<1, 7><<<total, 512, 0, st>>>(jp, nbatch); break;
-      case 8: bmm_kernel<1, 8><<<total, 512, 0, st>>>(jp, nbatch); break;
-      default: bmm_kernel<1><<<total, 512, 0, st>>>(jp, nbatch);
-    }
-  } else {
-    bmm_kernel<0><<<total, 512, 0, st>>>(jp, nbatch);
-  }
+  if (prec == 1) bmm_kernel<1><<<total, 512, 0, st>>>(jp, nbatch);
+  else bmm_kernel<0><<<total, 512, 0, st>>>(jp, nbatch);
   TM_CHECK_LAUNCH();
   return 0;
 }
@@ -442,306 +408,6 @@ void add_term(tm_bmm_job& j, const float* A, int ta, const float* B, int tb) {
   j.sa2 = (long long)j.M * j.K; j.sb2 = (long long)j.K * j.N;
 }
 
-// ---------------------------------------------------------------------------
-// Persistent pseudo-inverse chains.  The forward (24 dependent 256^3 products per layer)
-// and the backward (24 more) are latency-bound chains: launched one product per kernel,
-// each product pays a kernel boundary plus a cold operand fetch for ~0.3 us of MFMA work.
-// Here ONE launch of 256 workgroups (one per CU: the LDS request forces it) runs a whole
-// chain.  Team t = the workgroups with blockIdx % 8 == t (one XCD under round-robin
-// dispatch: a speed effect only, never relied on) owns the heads h with h % 8 == t;
-// between dependent products the team meets at a counter barrier.
-// Hand-off (placement-independent, the write-through form of the guide's Guideline 16):
-// every chain store is an sc1 (write-through) buffer store, 16 B per lane from an
-// LDS-staged tile; every storing wave drains its stores (s_waitcnt vmcnt(0)) before the
-// workgroup barrier; one lane then adds to the team's agent-scope counter and polls it
-// (relaxed = sc1 load); every load of chain data is an sc1 (L1-bypassing) buffer load, so
-// no acquire fence is needed.  The counters are zeroed by a memset node before every
-// launch and every spin is bounded (an expired spin sets an error word, never hangs).
-// A pass computes T tiles at once (T = 2 for one-job products, 4 for the backward's job
-// pairs): 8/T waves per tile, each a strided share of the k-steps, summed in LDS in wave
-// order -- deterministic run to run.
-typedef __attribute__((address_space(1))) unsigned gu32;
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-struct TeamState {   // 128 B, zeroed per call
-  unsigned cnt[8];   // per-team barrier counters
-  unsigned err;      // a spin expired
-  unsigned pad[23];
-};
-constexpr int TEAMS = 8;
-constexpr int TEAM_GRID = 256;
-constexpr size_t TEAM_LDS = 96 * 1024;    // > 80 KB: one workgroup per CU
-constexpr size_t TEAM_STATE_FLOATS = 64;  // the 128-B state block + alignment slack
-constexpr int SC1 = 16;                   // buffer-op aux bits: sc1
-constexpr int OST = 36;                   // staged output tile row stride (floats)
-// Measured (scripts/microbench.py, N = 8192, 8 heads, bf16x3): forward 169 us vs 131 us for the
-// launch-per-product chain, backward 336 vs 210 us; without the barrier (results invalid) still
-// 111 / 271 us.  The sc1 stores drop the lines from the producer XCD's L2, so every operand
-// panel comes back at the cross-XCD rate, where the per-launch chain reads L2-resident panels.
-// Kept as a tested ablation (tm_debug_set_variant(3, 1); 2 = barrier skipped, timing only).
-int g_pinv_team = 0;
-
-struct DJob {  // C = diag I + alpha (op(A) op(B) [+ op(A2) op(B2)]) + e1 E1 + e2 E2, 256^3 per head
-  const float* A; const float* B; const float* A2; const float* B2;
-  const float* E1; const float* E2; float* C;
-  int ta, tb, ta2, tb2;
-  float alpha, diag, e1, e2;
-};
-
-TM_DEV DJob djob(const float* A, int ta, const float* B, int tb, float* C, float alpha, float diag = 0.f) {
-  DJob j{};
-  j.A = A; j.ta = ta; j.B = B; j.tb = tb; j.C = C; j.alpha = alpha; j.diag = diag;
-  return j;
-}
-
-TM_DEV __amdgpu_buffer_rsrc_t mat_rsrc(const float* m) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)m, (short)0, NL * NL * (int)sizeof(float), 0x00020000);
-}
-TM_DEV f32x4 ld4_sc1(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, SC1));
-}
-TM_DEV float ld1_sc1(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, SC1));
-}
-TM_DEV void st4_sc1(__amdgpu_buffer_rsrc_t r, int off, f32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, SC1);
-}
-
-// fragment of op(X) at (rc, k..k+7): contiguous -> X[rc][k..k+7], else X[k..k+7][rc]
-TM_DEV f32x8 team_frag(__amdgpu_buffer_rsrc_t r, bool contiguous, int rc, int k) {
-  if (contiguous) {
-    const int off = (rc * NL + k) * 4;
-    const f32x4 a = ld4_sc1(r, off), b = ld4_sc1(r, off + 16);
-    return (f32x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  }
-  f32x8 v;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = ld1_sc1(r, ((k + e) * NL + rc) * 4);
-  return v;
-}
-
-// One pass: tile slots s = 0..T-1 hold units u0 + s*size (valid below `per`); unit u is
-// tile u & 63 of job u < 64 ? J0 : J1 of head bh.
-// smem: red [8 waves][16][64] fp32, then the staged outputs [T][32][OST] fp32.
-template <int PREC, int T, int TWO>
-TM_DEV void team_pass(const DJob& J0, const DJob& J1, int u0, int size, int per, int bh, float* red) {
-  constexpr int WPT = 8 / T;              // waves per tile
-  constexpr int KPT = 16 / WPT;           // k-steps per wave per term
-  constexpr int NS = KPT * (TWO ? 2 : 1);  // fragment slots per wave
-  constexpr int OPT = 2 * T;              // outputs per thread
-  float* outs = red + 8 * 16 * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
-  const size_t hs = (size_t)bh * NL * NL;
-  // epilogue operands first (their latency overlaps the fragment loads)
-  float ev1[OPT], ev2[OPT];
-#pragma unroll
-  for (int o = 0; o < OPT; ++o) {
-    const int e = tid + 512 * o, s = e >> 10, reg = (e >> 6) & 15, ln = e & 63;
-    const int u = u0 + s * size;
-    ev1[o] = 0.f;
-    ev2[o] = 0.f;
-    if (u < per) {
-      const DJob& Jo = u < 64 ? J0 : J1;
-      const int t = u & 63;
-      const int off = (((t >> 3) * 32 + acc_row(reg, ln >> 5)) * NL + (t & 7) * 32 + (ln & 31)) * 4;
-      if (Jo.E1) ev1[o] = ld1_sc1(mat_rsrc(Jo.E1 + hs), off);
-      if (Jo.E2) ev2[o] = ld1_sc1(mat_rsrc(Jo.E2 + hs), off);
-    }
-  }
-  const int sel = wave / WPT, q = wave % WPT;
-  const int u = u0 + sel * size;
-  f32x16 acc = (f32x16){};
-  if (u < per) {
-    const DJob& J = u < 64 ? J0 : J1;
-    const int t = u & 63, m0 = (t >> 3) * 32, n0 = (t & 7) * 32;
-    f32x8 af[NS], bf[NS];
-    {
-      const __amdgpu_buffer_rsrc_t ra = mat_rsrc(J.A + hs), rb = mat_rsrc(J.B + hs);
-#pragma unroll
-      for (int i = 0; i < KPT; ++i) {
-        const int k = (q + WPT * i) * 16 + 8 * h;
-        af[i] = team_frag(ra, J.ta == 0, m0 + r, k);
-        bf[i] = team_frag(rb, J.tb == 1, n0 + r, k);
-      }
-    }
-    if constexpr (TWO) {
-      const __amdgpu_buffer_rsrc_t ra = mat_rsrc(J.A2 + hs), rb = mat_rsrc(J.B2 + hs);
-#pragma unroll
-      for (int i = 0; i < KPT; ++i) {
-        const int k = (q + WPT * i) * 16 + 8 * h;
-        af[KPT + i] = team_frag(ra, J.ta2 == 0, m0 + r, k);
-        bf[KPT + i] = team_frag(rb, J.tb2 == 1, n0 + r, k);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);  // every load issued before the first MFMA waits
-#pragma unroll
-    for (int i = 0; i < NS; ++i) mma_f32_step<PREC>(acc, af[i], bf[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) red[(wave * 16 + i) * 64 + lane] = acc[i];
-  __syncthreads();
-#pragma unroll
-  for (int o = 0; o < OPT; ++o) {
-    const int e = tid + 512 * o, s = e >> 10, reg = (e >> 6) & 15, ln = e & 63;
-    const int uo = u0 + s * size;
-    if (uo >= per) continue;
-    const DJob& Jo = uo < 64 ? J0 : J1;
-    const int t = uo & 63, rl = acc_row(reg, ln >> 5), cl = ln & 31;
-    float sum = red[((s * WPT) * 16 + reg) * 64 + ln];
-#pragma unroll
-    for (int w = 1; w < WPT; ++w) sum += red[((s * WPT + w) * 16 + reg) * 64 + ln];
-    float v = Jo.alpha * sum;
-    if ((t >> 3) == (t & 7) && rl == cl) v += Jo.diag;
-    v += Jo.e1 * ev1[o] + Jo.e2 * ev2[o];
-    outs[(s * 32 + rl) * OST + cl] = v;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int p = 0; p < T / 2; ++p) {  // 16 B per lane, write-through
-    const int pc = tid + 512 * p, s = pc >> 8, idx = pc & 255, rl = idx >> 3, c4 = (idx & 7) * 4;
-    const int uo = u0 + s * size;
-    if (uo < per) {
-      const DJob& Jo = uo < 64 ? J0 : J1;
-      const int t = uo & 63;
-      st4_sc1(mat_rsrc(Jo.C + hs), (((t >> 3) * 32 + rl) * NL + (t & 7) * 32 + c4) * 4,
-              *(const f32x4*)&outs[(s * 32 + rl) * OST + c4]);
-    }
-  }
-  // red / outs are rewritten by the next pass only behind that pass's first barrier
-}
-
-TM_DEV void team_spin(gu32* word, unsigned target, gu32* err) {
-  unsigned spins = 0;
-  while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    __builtin_amdgcn_s_sleep(2);
-    if (++spins > (1u << 22)) {  // ~0.3 s: give up (results invalid, error word set), never hang
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-  }
-}
-
-// every storing wave drains its sc1 stores, the workgroup meets, one lane signals and
-// waits for the whole team, the workgroup meets again
-TM_DEV void team_sync(TeamState* st, int team, int size, unsigned& epoch) {
-  if (size < 0) return;  // ablation (timing only): no hand-off at all
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ++epoch;
-  if (threadIdx.x == 0) {
-    gu32* cnt = (gu32*)&st->cnt[team];
-    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    team_spin(cnt, epoch * (unsigned)size, (gu32*)&st->err);
-  }
-  __syncthreads();
-}
-
-// this team's units of a 1- or 2-job product
-template <int PREC, int T, int TWO>
-TM_DEV void team_stage(const DJob& j0, const DJob& j1, int njobs, int nbh, int team, int rank, int size,
-                       float* red) {
-  const int per = njobs * 64;
-  for (int bh = team; bh < nbh; bh += TEAMS)
-    for (int u0 = rank; u0 < per; u0 += T * size) team_pass<PREC, T, TWO>(j0, j1, u0, size, per, bh, red);
-}
-
-template <int PREC>
-__global__ __launch_bounds__(512) void pinv_fwd_team_kernel(const float* X, int nbh, int iters, float* saved,
-                                                            TeamState* st) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = (float*)smem;
-  const int team = blockIdx.x % TEAMS, rank = blockIdx.x / TEAMS, size = gridDim.x / TEAMS;
-  const int ssize = st->pad[0] ? -1 : size;  // pad[0] != 0: sync ablation
-  const size_t mat = (size_t)nbh * NL * NL;
-  float* Zs = saved;
-  float* Ps = Zs + (iters + 1) * mat;
-  float* T3s = Ps + iters * mat;
-  float* T5s = T3s + iters * mat;
-  unsigned epoch = 0;
-  const DJob none{};
-  for (int it = 0; it < iters; ++it) {
-    float* Z = Zs + it * mat;
-    float* P = Ps + it * mat;
-    float* T3 = T3s + it * mat;
-    float* T5 = T5s + it * mat;
-    DJob j = djob(X, 0, Z, 0, P, 1.f);                        // P = X Z
-    team_stage<PREC, 2, 0>(j, none, 1, nbh, team, rank, size, red);
-    team_sync(st, team, ssize, epoch);
-    j = djob(P, 0, P, 0, T3, 1.f, 15.f);                      // T3 = 15I + P P - 7P
-    j.E1 = P; j.e1 = -7.f;
-    team_stage<PREC, 2, 0>(j, none, 1, nbh, team, rank, size, red);
-    team_sync(st, team, ssize, epoch);
-    j = djob(P, 0, T3, 0, T5, -1.f, 13.f);                    // T5 = 13I - P T3
-    team_stage<PREC, 2, 0>(j, none, 1, nbh, team, rank, size, red);
-    team_sync(st, team, ssize, epoch);
-    j = djob(Z, 0, T5, 0, Zs + (it + 1) * mat, 0.25f);        // Z' = 0.25 Z T5
-    team_stage<PREC, 2, 0>(j, none, 1, nbh, team, rank, size, red);
-    if (it + 1 < iters) team_sync(st, team, ssize, epoch);
-  }
-}
-
-// the iterations of tm_pinv_bwd (its init part stays in its own kernels)
-template <int PREC>
-__global__ __launch_bounds__(512) void pinv_bwd_team_kernel(const float* X, int nbh, int iters, const float* saved,
-                                                            float* dZ, float* work, float* dX, TeamState* st) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = (float*)smem;
-  const int team = blockIdx.x % TEAMS, rank = blockIdx.x / TEAMS, size = gridDim.x / TEAMS;
-  const int ssize = st->pad[0] ? -1 : size;  // pad[0] != 0: sync ablation
-  const size_t mat = (size_t)nbh * NL * NL;
-  const float* Zs = saved;
-  const float* Ps = Zs + (iters + 1) * mat;
-  const float* T3s = Ps + iters * mat;
-  const float* T5s = T3s + iters * mat;
-  float* dT5 = work;
-  float* dZa = dT5 + mat;
-  float* dP = dZa + mat;
-  float* dT3 = dP + mat;
-  float* G = dZ;
-  unsigned epoch = 0;
-  for (int it = iters - 1; it >= 0; --it) {
-    const float* Z = Zs + it * mat;
-    const float* P = Ps + it * mat;
-    const float* T3 = T3s + it * mat;
-    const float* T5 = T5s + it * mat;
-    DJob a = djob(Z, 1, G, 0, dT5, 0.25f);                    // dT5 = 0.25 Z^T G
-    DJob b = djob(G, 0, T5, 1, dZa, 0.25f);                   // dZa = 0.25 G T5^T
-    team_stage<PREC, 4, 0>(a, b, 2, nbh, team, rank, size, red);
-    team_sync(st, team, ssize, epoch);
-    a = djob(dT5, 0, T3, 1, dP, -1.f);                        // dP  = -dT5 T3^T
-    b = djob(P, 1, dT5, 0, dT3, -1.f);                        // dT3 = -P^T dT5
-    team_stage<PREC, 4, 0>(a, b, 2, nbh, team, rank, size, red);
-    team_sync(st, team, ssize, epoch);
-    a = djob(dT3, 0, P, 1, dP, 1.f);                          // dP += dT3 P^T + P^T dT3 - 7 dT3
-    a.A2 = P; a.ta2 = 1; a.B2 = dT3; a.tb2 = 0;
-    a.E1 = dP; a.e1 = 1.f; a.E2 = dT3; a.e2 = -7.f;
-    team_stage<PREC, 2, 1>(a, a, 1, nbh, team, rank, size, red);
-    team_sync(st, team, ssize, epoch);
-    a = djob(dP, 0, Z, 1, dX, 1.f);                           // dX (+)= dP Z^T
-    if (it != iters - 1) { a.E1 = dX; a.e1 = 1.f; }
-    b = djob(X, 1, dP, 0, G, 1.f);                            // G = dZa + X^T dP
-    b.E1 = dZa; b.e1 = 1.f;
-    team_stage<PREC, 4, 0>(a, b, 2, nbh, team, rank, size, red);
-    if (it > 0) team_sync(st, team, ssize, epoch);
-  }
-}
-
-TeamState* team_state_at(float* p) {
-  return (TeamState*)(((uintptr_t)p + 127) & ~(uintptr_t)127);
-}
-
-// one workgroup per CU, a multiple of the team count
-int team_grid() {
-  static int grid = 0;
-  if (!grid) {
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = std::max(TEAMS, std::min(TEAM_GRID, cus / TEAMS * TEAMS));
-  }
-  return grid;
-}
-
 }  // namespace
 
 // Debug/ablation switch for microbenchmarks only (not part of the supported ABI surface).
@@ -760,10 +426,8 @@ extern "C" int tm_debug_xcc_map(int* out, int nblocks, int threads, void* stream
 extern "C" void tm_debug_set_nys_variant(int value);
 extern "C" void tm_debug_set_gemm_variant(int value);
 extern "C" void tm_debug_set_variant(int which, int value) {
-  if (which == 0) g_bmm_variant = value;
   if (which == 1) tm_debug_set_nys_variant(value);
   if (which == 2) tm_debug_set_gemm_variant(value);
-  if (which == 3) g_pinv_team = value;
 }
 
 extern "C" int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream) {
@@ -773,7 +437,7 @@ extern "C" int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, v
 
 // workspace: Zs[iters+1], Ps[iters], T3s[iters], T5s[iters] (each nbh*256*256 fp32) + sums[2][nbh][256] + stats[8]
 extern "C" long long tm_pinv_saved_floats(int nbh, int iters) {
-  return (4LL * iters + 1) * nbh * NL * NL + 2LL * nbh * NL + 8 + TEAM_STATE_FLOATS;  // + barrier block
+  return (4LL * iters + 1) * nbh * NL * NL + 2LL * nbh * NL + 8;
 }
 
 extern "C" int tm_pinv_fwd(const float* X, int nbh, int iters, int prec, float* saved, void* stream) {
@@ -790,20 +454,6 @@ extern "C" int tm_pinv_fwd(const float* X, int nbh, int iters, int prec, float* 
   TM_CHECK_LAUNCH();
   pinv_init_kernel<<<dim3(nbh, NL / 16), 256, 0, st>>>(X, sums, nbh, Zs, stats);
   TM_CHECK_LAUNCH();
-  if (g_pinv_team && iters > 0) {  // the whole chain in one persistent launch
-    TeamState* ts = team_state_at(stats + 8);
-    if (hipMemsetAsync(ts, 0, sizeof(TeamState), st) != hipSuccess) { tm_set_error("pinv_fwd: memset"); return 2; }
-    if (g_pinv_team == 2) (void)hipMemsetAsync(&ts->pad[0], 1, 1, st);
-    if (prec == 1) {
-      tm_allow_smem(pinv_fwd_team_kernel<1>, TEAM_LDS);
-      pinv_fwd_team_kernel<1><<<team_grid(), 512, TEAM_LDS, st>>>(X, nbh, iters, saved, ts);
-    } else {
-      tm_allow_smem(pinv_fwd_team_kernel<0>, TEAM_LDS);
-      pinv_fwd_team_kernel<0><<<team_grid(), 512, TEAM_LDS, st>>>(X, nbh, iters, saved, ts);
-    }
-    TM_CHECK_LAUNCH();
-    return 0;
-  }
   if (iters == 0) return 0;
   {
     tm_bmm_job j = job(X, 0, Zs, 0, Ps, NL, NL, NL, 1.f);              // P_0 = X Z_0
@@ -838,7 +488,7 @@ extern "C" int tm_pinv_fwd(const float* X, int nbh, int iters, int prec, float* 
 
 // workspace: 5 matrices + partial dots (nbh*16) + 1
 extern "C" long long tm_pinv_bwd_workspace_floats(int nbh) {
-  return 5LL * nbh * NL * NL + nbh * 16LL + 16 + TEAM_STATE_FLOATS;
+  return 5LL * nbh * NL * NL + nbh * 16LL + 16;
 }
 
 // dZ (gradient w.r.t. the final Z) is consumed (overwritten).  dX is written (=).
@@ -860,21 +510,7 @@ extern "C" int tm_pinv_bwd(const float* X, int nbh, int iters, int prec, const f
   float* gz = part + nbh * 16;
   float* G = dZ;
   bool first = true;
-  if (g_pinv_team && iters > 0) {  // the iterations in one persistent launch
-    TeamState* ts = team_state_at(gz + 16);
-    if (hipMemsetAsync(ts, 0, sizeof(TeamState), st) != hipSuccess) { tm_set_error("pinv_bwd: memset"); return 2; }
-    if (g_pinv_team == 2) (void)hipMemsetAsync(&ts->pad[0], 1, 1, st);
-    if (prec == 1) {
-      tm_allow_smem(pinv_bwd_team_kernel<1>, TEAM_LDS);
-      pinv_bwd_team_kernel<1><<<team_grid(), 512, TEAM_LDS, st>>>(X, nbh, iters, saved, dZ, work, dX, ts);
-    } else {
-      tm_allow_smem(pinv_bwd_team_kernel<0>, TEAM_LDS);
-      pinv_bwd_team_kernel<0><<<team_grid(), 512, TEAM_LDS, st>>>(X, nbh, iters, saved, dZ, work, dX, ts);
-    }
-    TM_CHECK_LAUNCH();
-    first = false;
-  }
-  for (int it = first ? iters - 1 : -1; it >= 0; --it) {
+  for (int it = iters - 1; it >= 0; --it) {
     const float* Z = Zs + it * mat;
     const float* P = Ps + it * mat;
     const float* T3 = T3s + it * mat;

@@ -98,6 +98,30 @@ class Lookahead(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True):
         self.base_optimizer.zero_grad(set_to_none=set_to_none)
 
+    def state_dict(self):
+        """``{'state': base state, 'slow_state': ..., 'param_groups': ...}`` as the reference
+        wrapper saves it (code/MyOptimizer/lookahead.py:56-68); the slow state is keyed by group
+        index and also carries the device step counter and init flag."""
+        fast = self.base_optimizer.state_dict()
+        slow = {}
+        for (_, gi), st in self.state.items():
+            slow[gi] = {"slow": [t.detach().clone() for t in st["slow"]],
+                        "step": st["step"].detach().clone(), "init": st["init"].detach().clone()}
+        return {"state": fast["state"], "slow_state": slow, "param_groups": fast["param_groups"]}
+
+    def load_state_dict(self, state_dict):
+        """Restores the base optimizer (its moments and the lookahead_* group fields) and the
+        slow weights with their step counter / init flag (lookahead.py:70-88)."""
+        self.base_optimizer.load_state_dict({"state": state_dict["state"],
+                                             "param_groups": state_dict["param_groups"]})
+        self.param_groups = self.base_optimizer.param_groups
+        self.state = defaultdict(dict)
+        for gi, st in state_dict.get("slow_state", {}).items():
+            dev = self.param_groups[int(gi)]["params"][0].device
+            self.state[("group", int(gi))] = {"slow": [t.to(dev).clone() for t in st["slow"]],
+                                              "step": st["step"].to(dev).clone(),
+                                              "init": st["init"].to(dev).clone()}
+
 
 class FusedRAdamLookahead(torch.optim.Optimizer):
     """``Lookahead(torch.optim.RAdam(groups))`` as ONE HIP launch pair per step.

@@ -67,7 +67,8 @@ class _TransMILFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, engine, names, drop_p, seed_dev, holder, x, *params):
         prm = dict(zip(names, params))
-        logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev)
+        with torch.cuda.device(x.device):   # kernels go to x's device and its current stream
+            logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev)
         ctx.engine, ctx.c, ctx.names, ctx.prm = engine, c, names, prm
         if holder is not None:
             holder["ctx"] = c
@@ -75,7 +76,12 @@ class _TransMILFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dlogits):
-        g = ctx.engine.backward(dlogits.float().contiguous(), ctx.c, ctx.prm)
+        if ctx.c is None:
+            raise RuntimeError("TransMIL (fused HIP path): the saved activations were freed by the first "
+                               "backward; retain_graph=True is not supported on the fused path -- set "
+                               "model.fused = False (module-by-module path) to backpropagate twice")
+        with torch.cuda.device(dlogits.device):
+            g = ctx.engine.backward(dlogits.float().contiguous(), ctx.c, ctx.prm)
         ctx.c = None
         return (None, None, None, None, None, None) + tuple(g[n] for n in ctx.names)
 
@@ -173,7 +179,9 @@ class TransMIL(nn.Module):
             raise RuntimeError("TransMIL (HIP) needs a GPU tensor: there is no CPU path")
         layout = self._fc1_layout()
         x = x.float().contiguous()             # :174
-        if not self.fused or self._hooked():
+        if not self.fused or self._hooked() or x.requires_grad:
+            # hooks, or a gradient w.r.t. the input (feature saliency): the module-by-module path,
+            # whose ops also return dL/dx; the fused node returns parameter gradients only
             return self._forward_modules(x, return_attn)
         names = tuple(n for n, _ in self.named_parameters())
         params = tuple(p for _, p in self.named_parameters())

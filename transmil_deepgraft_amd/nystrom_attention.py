@@ -40,7 +40,8 @@ def _check_dtype(dtype):
 class _NystromFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, engine, heads, drop_p, seed_dev, holder, x, wqkv, wo, bo, wconv):
-        out, c = engine.forward(x, wqkv, wo, bo, wconv, heads, drop_p, 0x51ED27, seed_dev)
+        with torch.cuda.device(x.device):
+            out, c = engine.forward(x, wqkv, wo, bo, wconv, heads, drop_p, 0x51ED27, seed_dev)
         ctx.engine, ctx.c = engine, c
         if holder is not None:
             holder["c"] = c
@@ -48,7 +49,8 @@ class _NystromFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        dx, dwqkv, dwo, dbo, dwconv = ctx.engine.backward(dout, ctx.c)
+        with torch.cuda.device(dout.device):
+            dx, dwqkv, dwo, dbo, dwconv = ctx.engine.backward(dout, ctx.c)
         return None, None, None, None, None, dx, dwqkv, dwo, dbo, dwconv
 
 
