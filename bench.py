@@ -13,10 +13,14 @@ optimizer step -> zero_grad.  Bags are resident in HBM before timing starts.
     torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
 Prints ONE JSON line on rank 0.  Extra objects:
-  roofline      -- the dominant kernel's achieved rate (algorithmic bytes or flops
-                   per launch / its mean HIP-event duration over the timed steps)
+  roofline      -- the dominant kernel's achieved rate: by default the pseudo-inverse
+                   forward chain (tm_pinv_fwd_split: 14 launches of pinv_stage_kernel, the
+                   largest share of the step in profiles/r02_*_kernel_summary.txt), its
+                   algorithmic flops / the HIP-event span of the call on its stream
   cpu_baseline  -- the fp32 CPU oracle (oracle/transmil_ref.py, logits path) on a
-                   bounded sample of the same workload, rank 0 only.
+                   bounded sample of the same workload, rank 0 only: median of 5 steps after
+                   2 warm-ups at 8 threads (code/train.py:93) and at the box's CPU share
+  optimizer_ms  -- the Lookahead(RAdam) step alone (inside the timed step too)
 """
 from __future__ import annotations
 
@@ -34,6 +38,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFS = 2500.0       # dense bf16 MFMA spec
+F32_MATRIX_PEAK_TFS = 157.3  # v_mfma_f32_32x32x2_f32 = the fp32 vector rate (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -47,22 +52,32 @@ def parse():
                     help="in_features: 512 (Linear+GELU _fc1, the metric's config) or 2048 (the RCC "
                          "_fc1 branch on RetCCL-width features, config C5 without its encoder)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--probe", default="a1_fwd", help="call site timed for the roofline object")
+    ap.add_argument("--probe", default="pinv_fwd", help="call site timed for the roofline object")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of "
                     "replaying the captured hipGraph of the whole step")
-    ap.add_argument("--cpu-steps", type=int, default=3)
+    ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU steps per thread count (median)")
+    ap.add_argument("--cpu-as-written", action="store_true",
+                    help="also time the CPU oracle as the reference is written (the n'xn' return_attn product)")
     return ap.parse_args()
 
 
 def roofline_model(site, n_patches, dtype_bytes):
-    """Algorithmic bytes / flops of ONE launch of `site`."""
+    """Algorithmic bytes / flops of ONE call of `site`."""
     import math
     G = math.ceil(math.sqrt(n_patches))
     S = G * G + 1
     n = (S + 255) // 256 * 256
     heads, dh, m = 8, 64, 256
     t = dtype_bytes
+    if site == "pinv_fwd":
+        # 24 products of 256^3 per head (S = X X^T, then per iteration R, T5, P', Z; App. A eq. 7);
+        # bytes: every chain matrix read / written once as split bf16 planes (4 B per element)
+        mat = heads * m * m * 4
+        flops = 24 * heads * 2 * m ** 3
+        byts = mat * (1 + 1 + 3 + 6 * 5 + 5 * 5 + 4)   # X; S; A_0 out; B_k/A_k in+out; F
+        return dict(bytes=byts, flops=flops, peak_tfs=F32_MATRIX_PEAK_TFS, units=14,
+                    note="fp32-class products as bf16 hi/lo x3 on the bf16 MFMA; units = launches per call")
     if site == "a1_fwd":
         # read q, v (conv) [n, 512] T; write merged [n, 512] T + lse [8, n] fp32; landmarks/Y fp32
         byts = 3 * n * 512 * t + heads * n * 4 + 2 * heads * m * dh * 4
@@ -94,12 +109,27 @@ def measured_traffic(site, n_patches, dtype):
     return rec.get("traffic_bytes")
 
 
-def cpu_baseline(n_patches, ncls, steps, feat=512):
-    """fp32 CPU oracle, logits path (no unused n'xn' attention product), timed on this host."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(n_patches, ncls, steps, feat=512, as_written=False):
+    """fp32 CPU oracle on this host: fwd + CE + bwd + RAdam, train mode, median of `steps` steps
+    after 2 warm-ups, at 8 threads (code/train.py:93) and at the box's CPU share (16; the
+    machine's physical cores belong to other jobs).  Logits path (no unused n'xn' product)
+    unless `as_written`."""
+    import statistics
     from oracle.transmil_ref import TransMIL as RefTransMIL, TransLayer
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    TransLayer.compute_attn = False
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    counts = sorted({8, max(1, min(share, os.cpu_count() or 1))})
+    TransLayer.compute_attn = as_written
     torch.manual_seed(0)
     model = RefTransMIL(ncls, feat, 512).train()
     opt = torch.optim.RAdam(model.parameters(), lr=2e-4)
@@ -114,15 +144,26 @@ def cpu_baseline(n_patches, ncls, steps, feat=512):
         opt.step()
         opt.zero_grad(set_to_none=True)
 
-    step()  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    dt = time.perf_counter() - t0
-    TransLayer.compute_attn = True
-    return dict(value=steps / dt, unit="slides/sec", cores=threads, kind="port",
-                sample=f"{steps} fwd+bwd+RAdam steps (after 1 warm-up), 1 bag N={n_patches}x{feat}, fp32, "
-                       f"train mode, torch.set_num_threads({threads})")
+    by = {}
+    try:
+        for th in counts:
+            torch.set_num_threads(th)
+            for _ in range(2):
+                step()
+            ts = []
+            for _ in range(steps):
+                t0 = time.perf_counter()
+                step()
+                ts.append(time.perf_counter() - t0)
+            by[th] = 1.0 / statistics.median(ts)
+    finally:
+        TransLayer.compute_attn = True
+    best = max(by, key=by.get)
+    variant = "as written (n'xn' return_attn product)" if as_written else "logits path"
+    return dict(value=by[best], unit="slides/sec", cores=best, kind="port",
+                by_threads={str(k): round(v, 4) for k, v in by.items()}, cpu_model=_cpu_model(),
+                sample=f"median of {steps} fwd+CE+bwd+RAdam steps after 2 warm-ups per thread count, 1 bag "
+                       f"N={n_patches}x{feat}, fp32, train mode, {variant}, torch.set_num_threads in {counts}")
 
 
 def main():
@@ -253,6 +294,25 @@ def main():
         kernel_ms_samples = [s.elapsed_time(e) for s, e in engine.probe.events]
     kernel_ms = sum(kernel_ms_samples) / max(len(kernel_ms_samples), 1)
 
+    # the optimizer step alone (it is also inside every timed step): a graph of opt.step()
+    # replayed 20 times between two events (after the timed region; it advances the state)
+    opt_ms = None
+    if graph is not None:
+        try:
+            og = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(og):
+                opt.step()
+            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            og.replay()
+            s_ev.record()
+            for _ in range(20):
+                og.replay()
+            e_ev.record()
+            torch.cuda.synchronize()
+            opt_ms = s_ev.elapsed_time(e_ev) / 20
+        except Exception as exc:  # noqa: BLE001
+            print(f"# optimizer timing unavailable ({exc})", file=sys.stderr)
+
     if rank == 0:
         slides = args.steps * world
         tb = 2 if args.dtype == "bf16" else 4
@@ -260,7 +320,7 @@ def main():
         sec = kernel_ms / 1e3
         ach_bw = rm["bytes"] / sec / 1e9
         ach_fl = rm["flops"] / sec / 1e12
-        peak_fl = BF16_PEAK_TFS if args.dtype == "bf16" else 157.3
+        peak_fl = rm.get("peak_tfs", BF16_PEAK_TFS if args.dtype == "bf16" else F32_MATRIX_PEAK_TFS)
         hbm_bound = rm["flops"] / rm["bytes"] < peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
         roof = (dict(bound="hbm", achieved=round(ach_bw, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                      frac=round(ach_bw / HBM_PEAK_GBS, 4), traffic=measured_traffic(args.probe, args.n, args.dtype))
@@ -270,11 +330,19 @@ def main():
         if overhead_samples:
             roof.update(event_span_ms=round(sum(span_samples) / len(span_samples), 5),
                         event_pair_overhead_ms=round(sum(overhead_samples) / len(overhead_samples), 5))
-        roof.update(kernel=args.probe, kernel_ms=round(kernel_ms, 5), launches=len(kernel_ms_samples),
+        kname = {"pinv_fwd": "pinv_stage_kernel x14 (tm_pinv_fwd_split)"}.get(args.probe, args.probe)
+        roof.update(kernel=kname, kernel_ms=round(kernel_ms, 5), samples=len(kernel_ms_samples),
                     algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])
+        if "units" in rm:
+            roof.update(launches_per_call=rm["units"], ms_per_launch=round(kernel_ms / rm["units"], 5),
+                        note=rm["note"])
+        base_metric = "slides/sec (fwd+bwd) at N=8192 patches, d=512"
+        if args.features == 512:
+            metric = base_metric if args.n == 8192 else f"slides/sec (fwd+bwd) at N={args.n} patches, d=512"
+        else:
+            metric = f"slides/sec (fwd+bwd) at N={args.n} patches, in_features={args.features}"
         out = {
-            "metric": "slides/sec (fwd+bwd) at N=8192 patches, d=512" if args.features == 512 else
-                      f"slides/sec (fwd+bwd) at N={args.n} patches, in_features={args.features}",
+            "metric": metric,
             "value": round(slides / elapsed, 3),
             "unit": "slides/sec",
             "n_gpus": world,
@@ -291,9 +359,12 @@ def main():
                        "execution": "eager" if args.eager else "hipGraph replay of the whole step",
                        "global_batch": world, "seq_len": args.n, "parallelism": f"dp{world}"},
             "roofline": roof,
+            "optimizer_ms": round(opt_ms, 5) if opt_ms is not None else None,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.n, args.classes, args.cpu_steps, args.features)
+            if args.cpu_as_written:
+                out["cpu_baseline_as_written"] = cpu_baseline(args.n, args.classes, 2, args.features, as_written=True)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -4,8 +4,10 @@
 
 For every kernel: dispatches, mean duration (from the kernel trace of the SQ pass), and per
 dispatch: HBM bytes (FETCH_SIZE doubled for the gfx950 half-count of 16-B reads + WRITE_SIZE,
-MI355X_MICROARCH.md "HBM"), L2 hit rate, MFMA busy fraction = SQ_VALU_MFMA_BUSY_CYCLES /
-(SQ_BUSY_CU_CYCLES * 4 SIMDs) (both summed over the CUs), wave-cycle shares (wait / issue-stall /
+MI355X_MICROARCH.md "HBM"), L2 hit rate, MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES /
+(dispatch cycles x 1024 SIMDs), CU busy = SQ_BUSY_CU_CYCLES / (dispatch cycles x 256 CUs), with
+dispatch cycles = duration x CLOCK_GHZ (rocprofv3's MfmaUtil divides by GRBM_GUI_ACTIVE, which
+reads high on short dispatches), wave-cycle shares (wait / issue-stall /
 active; SQ_WAVE_CYCLES counts quad-cycles like the SQ_WAIT_* counters), and the effective clock
 GRBM_GUI_ACTIVE / 8 XCDs / duration.  Prints one JSON object.
 """
@@ -15,6 +17,8 @@ import csv
 import glob
 import json
 import re
+
+CLOCK_GHZ = 2.0   # in-kernel shader clock under load (s_memtime vs s_memrealtime stamps, pinv stage)
 
 
 def short(name):
@@ -71,8 +75,15 @@ def main():
         if m.get("TCC_HIT_sum") is not None:
             h, mi = m["TCC_HIT_sum"], m["TCC_MISS_sum"]
             row["l2_hit"] = round(h / max(h + mi, 1), 3)
-        if m.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and m.get("SQ_BUSY_CU_CYCLES"):
-            row["mfma_busy"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * m["SQ_BUSY_CU_CYCLES"]), 4)
+        # GRBM_GUI_ACTIVE / 8 reads high on dispatches shorter than ~0.3 ms (MI355X_MICROARCH.md,
+        # DVFS give-back), so the busy fractions use the in-kernel clock measured by s_memtime /
+        # s_memrealtime stamps (CLOCK_GHZ) x the dispatch duration
+        cyc = t * CLOCK_GHZ  # t in ns
+        if m.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
+            row["mfma_busy_cycles"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"])
+            row["mfma_util"] = round(m["SQ_VALU_MFMA_BUSY_CYCLES"] / (cyc * 1024), 4)
+        if m.get("SQ_BUSY_CU_CYCLES") is not None:
+            row["cu_busy"] = round(m["SQ_BUSY_CU_CYCLES"] / (cyc * 256), 4)
         if m.get("SQ_WAVE_CYCLES"):
             w = m["SQ_WAVE_CYCLES"]
             row["wait_any"] = round(m["SQ_WAIT_ANY"] / w, 3)

@@ -232,7 +232,8 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
         a2s = pool(nbh * NL * NL)   # hi + lo bf16 planes = one fp32 matrix's bytes
         saved = pool(_lib.query("tm_pinv_split_saved_floats", nbh, PINV_ITERS))
         _lib.call("tm_nys_sim2_softmax_split", _p(ql), _p(kl), nbh, _p(a2), _p(a2s), st)
-        _lib.call("tm_pinv_fwd_split", _p(a2), _p(a2s), nbh, PINV_ITERS, _p(saved), st)
+        with probe("pinv_fwd"):
+            _lib.call("tm_pinv_fwd_split", _p(a2), _p(a2s), nbh, PINV_ITERS, _p(saved), st)
         z = saved[:nbh * NL * NL].view(nbh, NL, NL)
     else:
         saved = pool(_lib.query("tm_pinv_saved_floats", nbh, PINV_ITERS))
@@ -299,8 +300,9 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         # split operands; the softmax backward is fused into the chain's last launch
         pwork = pool(_lib.query("tm_pinv_bwd_split_workspace_floats", nbh))
         _lib.call("tm_split_f32", _p(dz), _p(pwork), mat, st)
-        _lib.call("tm_pinv_bwd_split", _p(state["a2"]), _p(state["a2s"]), nbh, PINV_ITERS, _p(state["pinv"]),
-                  _p(pwork), 1, _p(ds2), st)
+        with probe("pinv_bwd"):
+            _lib.call("tm_pinv_bwd_split", _p(state["a2"]), _p(state["a2s"]), nbh, PINV_ITERS, _p(state["pinv"]),
+                      _p(pwork), 1, _p(ds2), st)
     else:
         da2 = pool(mat).view(nbh, NL, NL)
         pwork = pool(_lib.query("tm_pinv_bwd_workspace_floats", nbh))
