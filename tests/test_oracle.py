@@ -148,3 +148,39 @@ def test_oracle_branches_match_reference_fixture(name):
             if k.startswith("grad.") and k.endswith(tag) and (tag or not k.endswith(".f64")):
                 pname = k[5:len(k) - len(tag)] if tag else k[5:]
                 np.testing.assert_allclose(grads[pname].grad.numpy(), fx[k], rtol=0, atol=tol * 10)
+
+
+@pytest.mark.parametrize("name", ["d512_b4_n300", "d512_peaky_n1024"])
+def test_oracle_matches_reference_d512_round2(name):
+    """The CPU oracle (fp64) against the reference-run d=512 fixtures of round 2: B = 4 bags in one
+    forward (global-max coupling) and q x 8 (tests/golden/make_golden_r2.py)."""
+    from golden_util import index, load, bag_input
+    from oracle.transmil_ref import TransMIL, deterministic_params_
+    meta = index()[name]
+    fx = load(name)
+    torch.manual_seed(0)
+    m = deterministic_params_(TransMIL(meta["n_classes"], 512, 512), 2021)
+    if "peaky" in name:
+        with torch.no_grad():
+            for layer in (m.layer1, m.layer2):
+                w = layer.attn.to_qkv.weight
+                w[: w.shape[0] // 3] *= 8.0
+    m = m.double().eval()
+    x = torch.from_numpy(bag_input(meta["n"], 512, 2021 + 1000 + meta["n"], meta["batch"])).double()
+    orig = torch.Tensor.float
+    torch.Tensor.float = lambda self, *a, **k: self
+    try:
+        with torch.no_grad():
+            lo = m(x).numpy()
+    finally:
+        torch.Tensor.float = orig
+    np.testing.assert_allclose(lo, fx["logits.f64"], rtol=0, atol=1e-9)
+
+
+def test_c3_oracle_fixture_matches_reference_fixture():
+    """Config C3 (N = 32768): the round-1 oracle-generated fixture and the round-2 fixture from the
+    reference's own TransMIL.py (placeholder return_attn value) hold the same logits."""
+    from golden_util import load
+    a, b = load("d512c3_n32768"), load("d512c3_ref_n32768")
+    np.testing.assert_allclose(a["logits.f64"], b["logits.f64"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(a["logits"], b["logits"], rtol=0, atol=1e-5)
