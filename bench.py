@@ -187,7 +187,7 @@ def main():
     model.set_compute_dtype(torch.bfloat16 if args.dtype == "bf16" else torch.float32)
     task = TransMILTask(model)
     opt = task.configure_optimizers()[0][0]
-    allreduce = GradAllReduce(model.parameters())
+    allreduce = GradAllReduce(model.parameters(), model=model)   # grads = views of a 2-part bucket
 
     g = torch.Generator(device=dev).manual_seed(2021 + rank)
     bags = [torch.rand(1, args.n, args.features, device=dev, generator=g) for _ in range(4)]

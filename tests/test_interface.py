@@ -168,6 +168,71 @@ def test_grad_allreduce_gloo_world2():
         torch.testing.assert_close(res[1][i], mean)
 
 
+def _oracle_task(accumulate):
+    """The oracle TransMIL (oracle/transmil_ref.py, the reference model restated) as the CPU
+    stand-in, split into the same two gradient-bucket parts as the HIP model."""
+    from oracle.transmil_ref import TransMIL as Ref
+    from transmil_deepgraft_amd.interface import TransMILTask
+
+    class Stand(Ref):
+        def grad_bucket_parts(self):
+            first = ("_fc.", "norm.", "layer2.", "pos_layer.")
+            named = list(self.named_parameters())
+            return [[p for n, p in named if n.startswith(first)], [p for n, p in named if not n.startswith(first)]]
+
+    torch.manual_seed(0)
+    m = Stand(2, 24).eval()          # eval: no dropout, so the ranks' gradients are deterministic
+    return TransMILTask(m, accumulate_grad_batches=accumulate)
+
+
+def _micro_batch(rank, i):
+    g = torch.Generator().manual_seed(1000 * rank + i)
+    return torch.rand(1, 30 + 7 * rank + i, 24, generator=g), torch.tensor([(rank + i) % 2]), None
+
+
+def _task_worker(rank, world, port, accumulate, steps, out):
+    import torch.distributed as dist
+    from transmil_deepgraft_amd.interface import GradAllReduce
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    task = _oracle_task(accumulate)
+    opt = task.configure_optimizers()[0][0]
+    ar = GradAllReduce(task.model.parameters(), model=task.model)
+    assert [len(p) for p in task.model.grad_bucket_parts()] == [len(p) for p in ar.bucket.parts_params]
+    for i in range(steps * accumulate):
+        task.optimization_step(_micro_batch(rank, i), opt, ar)
+    out[rank] = [p.detach().clone() for p in task.model.parameters()]
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("accumulate", [1, 3])
+def test_task_ddp_gloo_world2_end_to_end(accumulate):
+    """Two gloo ranks drive TransMILTask.optimization_step + GradAllReduce (two-part bucket)
+    on the oracle model with accumulate_grad_batches = 1 and 3 (code/train.py:199 uses 10):
+    both ranks end bit-close to one process that averages every micro-batch gradient over
+    ranks (loss / (K * world)) and steps Lookahead(RAdam) every K micro-batches."""
+    import torch.multiprocessing as mp
+    steps = 2
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_task_worker, args=(2, port, accumulate, steps, out), nprocs=2, join=True)
+        res = dict(out)
+    task = _oracle_task(accumulate)
+    opt = task.configure_optimizers()[0][0]
+    for s_ in range(steps):
+        for rank in range(2):
+            for i in range(s_ * accumulate, (s_ + 1) * accumulate):
+                (task.training_step(_micro_batch(rank, i)) / (2 * accumulate)).backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    for i, p in enumerate(task.model.parameters()):
+        torch.testing.assert_close(res[0][i], p.detach(), rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(res[1][i], res[0][i], rtol=0, atol=0)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [6, 0])
 def test_fused_radam_lookahead_matches_torch(k):

@@ -507,14 +507,20 @@ class TransMILEngine:
                    inner=inner)
         return logits, ctx
 
-    def backward(self, dlogits, ctx, params):
-        """Returns a dict name -> fp32 gradient with the reference parameter names."""
+    def backward(self, dlogits, ctx, params, out=None, ready=None):
+        """Returns a dict name -> fp32 gradient with the reference parameter names.
+
+        ``out``: name -> preallocated fp32 tensor to write each gradient into (the views of a
+        ``GradBucket``); ``ready(part)``: called once the head, norm, layer2 and PPEG gradients
+        are final (part 0, before layer1's backward is enqueued) and at the end (part 1), so
+        a bucketed all-reduce of part 0 overlaps layer1 / _fc1 backward."""
         geo, prm = ctx["geo"], ctx["prm"]
         dev = dlogits.device
         pool = Pool(dev)
         B, N, F, D, S = geo.B, geo.N, geo.F, geo.D, geo.S
         st = _stream()
-        g = {name: torch.empty_like(p, dtype=torch.float32) for name, p in params.items()}
+        g = out if out is not None else {name: torch.empty_like(p, dtype=torch.float32)
+                                         for name, p in params.items()}
         Ccls = prm["fc_w"].shape[0]
         dH = torch.zeros(B * S, D, dtype=torch.float32, device=dev)
         _lib.call("tm_head_bwd", _p(dlogits.contiguous()), B, Ccls, S, D, _p(ctx["xhat"]), _p(ctx["hrstd"]),
@@ -536,6 +542,8 @@ class TransMILEngine:
                           _p(g["pos_layer.proj1.weight"]), _p(g["pos_layer.proj1.bias"]),
                           _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), st)
                 dH = dH1
+                if ready is not None:
+                    ready(0)
         # _fc1 backward (GELU + grid-pad fold) and the class token
         dpre = pool(B * N * D, self.tdtype).view(B * N, D)
         _lib.call("tm_fc1_gelu_bwd", self.dt_code, _p(dH), _p(ctx["pre"]), B, N, S, geo.add, D, _p(dpre),
@@ -562,6 +570,8 @@ class TransMILEngine:
             weight_grad(dpre0, inner["xt"], g[w0n + ".weight"], Fm, Fin, B * N, ldy=Fm, ldx=Fin, dtype=self.dt_code,
                         work_pool=pool)
             colsum(dpre0, B * N, Fm, Fm, self.dt_code, g[w0n + ".bias"], pool)
+        if ready is not None:
+            ready(1)
         return g
 
 

@@ -11,9 +11,10 @@ it on MI355X:
                            wrapped in Lookahead (code/MyOptimizer/optim_factory.py:25-123)
 * ``Lookahead``         -- k-step slow-weight wrapper (alpha 0.5, k 6; multi-tensor ops)
 * ``FusedRAdamLookahead`` -- RAdam + Lookahead for the GPU as one HIP elementwise launch
-* ``GradAllReduce``     -- the DDP gradient all-reduce (Lightning DDP, code/train.py:178-201):
-                           one flat fp32 bucket, averaged over ranks with one RCCL
-                           all_reduce over xGMI (the model is 9.64 MB of fp32 grads)
+* ``GradBucket`` / ``GradAllReduce`` -- the DDP gradient all-reduce (Lightning DDP,
+                           code/train.py:178-201): gradients live as views of one flat fp32
+                           bucket in two parts, each averaged with one RCCL all_reduce over
+                           xGMI, part 0 overlapping layer1's backward (9.64 MB of fp32 grads)
 * ``TransMILTask``      -- ``training_step`` / ``configure_optimizers`` with the reference's
                            batch format ``(bags[B,n,F], labels[B], (names, patients))``
 """
@@ -253,45 +254,146 @@ def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float =
     return base
 
 
+class GradBucket:
+    """One flat fp32 buffer that holds every parameter gradient as a view, laid out in parts in
+    the order the fused backward finishes them (``TransMIL.grad_bucket_parts``).
+
+    The fused backward writes its gradient kernels' outputs straight into these views and
+    sets ``p.grad`` to them (models/TransMIL.py ``_TransMILFn.backward``), so the bucket IS
+    the gradient storage: no copy in or out around the all-reduce, and the addresses are
+    stable across steps (a captured hipGraph and the fused optimizer's pointer table stay
+    valid).  ``ready(i)`` is called by the backward when part ``i`` is final; ``hooks`` get it."""
+
+    def __init__(self, parts, device=None):
+        self.parts_params = [list(part) for part in parts if part]
+        self.params = [p for part in self.parts_params for p in part]
+        if len({id(p) for p in self.params}) != len(self.params):
+            raise ValueError("GradBucket: a parameter appears in two parts")
+        dev = device if device is not None else self.params[0].device
+        self._off = {}
+        self.ranges = []
+        off = 0
+        for part in self.parts_params:
+            start = off
+            for p in part:
+                self._off[id(p)] = (off, p.numel())
+                off += p.numel()
+            self.ranges.append((start, off))
+        self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.hooks = []
+
+    def view(self, p):
+        """A fresh view of ``p``'s slice (fresh, so autograd could steal it without a clone)."""
+        o, n = self._off[id(p)]
+        return self.flat[o:o + n].view_as(p)
+
+    def owns(self, p):
+        """True when ``p.grad`` is this bucket's view of ``p``."""
+        g = p.grad
+        if g is None or id(p) not in self._off:
+            return False
+        o, _ = self._off[id(p)]
+        return g.data_ptr() == self.flat.data_ptr() + 4 * o and g.shape == p.shape
+
+    def part(self, i):
+        a, b = self.ranges[i]
+        return self.flat[a:b]
+
+    def bind(self):
+        """Make every ``p.grad`` the bucket's view (keeps existing values by copying them in)."""
+        with torch.no_grad():
+            for p in self.params:
+                if not self.owns(p):
+                    v = self.view(p)
+                    if p.grad is None:
+                        v.zero_()
+                    else:
+                        v.copy_(p.grad)
+                    p.grad = v
+
+    def ready(self, i):
+        for h in self.hooks:
+            h(i)
+
+
 class GradAllReduce:
-    """Average gradients over ranks: one flat fp32 bucket, one all_reduce (RCCL on ROCm).
+    """Average gradients over ranks: the DDP gradient all-reduce on a ``GradBucket``.
 
     Replaces the Lightning DDP reducer (``strategy='ddp_find_unused_parameters_true'``,
-    code/train.py:184).  Every TransMIL parameter receives a gradient each step, so
-    the unused-parameter search is unnecessary; the bucket is sized to the whole
-    model (9.64 MB fp32 for 2 classes) because xGMI ring steps are per-link
-    bound and one large message beats several small ones.
-    """
+    code/train.py:184).  Every TransMIL parameter receives a gradient each step, so the
+    unused-parameter search is unnecessary.  With ``model=`` (a TransMIL with
+    ``grad_bucket_parts``) the bucket has two parts: part 0 (head, norm, layer2, PPEG; 4.4 MB
+    fp32) is final before layer1's backward is enqueued and, with ``overlap``, its RCCL
+    all_reduce is issued right then on RCCL's stream, overlapping layer1 + _fc1 backward on
+    the compute stream; part 1 (layer1, class token, _fc1; 5.2 MB) follows at the end.  Two
+    messages of ~5 MB keep each xGMI ring step large (per-link bound) while hiding part 0.
 
-    def __init__(self, params, group=None):
+    ``sync = False`` skips the reduction (Lightning's no-sync micro-batches under
+    ``accumulate_grad_batches``, code/train.py:199); ``force`` runs the collective even at
+    world size 1 (tests of the RCCL path inside a captured hipGraph)."""
+
+    def __init__(self, params, group=None, model=None, overlap=True, force=False):
         self.params = [p for p in params if p.requires_grad]
-        self.group = group
-        n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device
-        self.flat = torch.empty(n, dtype=torch.float32, device=dev)
-        self.views = []
-        off = 0
-        for p in self.params:
-            self.views.append(self.flat[off:off + p.numel()].view_as(p))
-            off += p.numel()
+        self.group, self.overlap, self.force = group, overlap, force
+        parts = [self.params]
+        if model is not None and hasattr(model, "grad_bucket_parts"):
+            mp = model.grad_bucket_parts()
+            if {id(p) for part in mp for p in part} == {id(p) for p in self.params}:
+                parts = mp
+        self.bucket = GradBucket(parts, self.params[0].device)
+        self.flat = self.bucket.flat
+        if model is not None and hasattr(model, "attach_grad_bucket"):
+            model.attach_grad_bucket(self.bucket)
+        self.bucket.hooks.append(self._on_ready)
+        self.sync = True
+        self._works = {}
+
+    def _world(self):
+        if not (dist.is_available() and dist.is_initialized()):
+            return 0
+        return dist.get_world_size(self.group)
+
+    def _active(self):
+        w = self._world()
+        return self.sync and (w > 1 or (w == 1 and self.force))
+
+    def _on_ready(self, i):
+        """Backward hook: issue part ``i``'s all_reduce now (async, on RCCL's stream)."""
+        if not (self.overlap and self._active()) or i in self._works:
+            return
+        self._works[i] = dist.all_reduce(self.bucket.part(i), op=dist.ReduceOp.SUM, group=self.group,
+                                         async_op=True)
 
     def __call__(self):
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(self.group) == 1:
+        if not self._active():
+            self._works.clear()
             return
-        grads = [p.grad for p in self.params]
-        torch._foreach_copy_(self.views, grads)
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.mul_(1.0 / dist.get_world_size(self.group))
-        torch._foreach_copy_(grads, self.views)
+        owned = all(self.bucket.owns(p) for p in self.params)
+        if not owned:
+            # gradients produced outside the fused backward (module-by-module path): bind them
+            self._works.clear()
+            self.bucket.bind()
+        for i in range(len(self.bucket.ranges)):
+            if i not in self._works:
+                self._works[i] = dist.all_reduce(self.bucket.part(i), op=dist.ReduceOp.SUM, group=self.group,
+                                                 async_op=True)
+        for i in sorted(self._works):
+            self._works[i].wait()       # the compute stream waits on RCCL's stream
+        self._works.clear()
+        self.flat.mul_(1.0 / self._world())
 
 
 class TransMILTask(nn.Module):
     """``ModelInterface`` training-step subset for the feature-bag path."""
 
     def __init__(self, model: nn.Module, lr: float = 2e-4, opt: str = "lookahead_radam",
-                 weight_decay: float = 0.01, loss: str = "CrossEntropyLoss"):
+                 weight_decay: float = 0.01, loss: str = "CrossEntropyLoss", accumulate_grad_batches: int = 1):
         super().__init__()
+        if accumulate_grad_batches < 1:
+            raise ValueError("accumulate_grad_batches >= 1")
         self.model = model
+        self.accumulate_grad_batches = accumulate_grad_batches
+        self._micro = 0
         self.n_classes = model.n_classes
         self.loss = create_loss(loss)
         self.lr, self.opt, self.weight_decay = lr, opt, weight_decay
@@ -316,6 +418,26 @@ class TransMILTask(nn.Module):
         # the reference logs loss.item() with sync_dist every step (model_interface.py:364),
         # a host sync + scalar all-reduce per step; here the value stays on the device.
         self._last_loss = loss.detach()
+        return loss
+
+    def optimization_step(self, batch, opt, allreduce=None):
+        """One micro-batch of Lightning's automatic optimization with
+        ``accumulate_grad_batches = K`` (code/train.py:199 uses K = 10 under DDP): the closure
+        loss is ``training_step / K``, backward accumulates into the gradient bucket, and only
+        every K-th micro-batch all-reduces (DDP no-sync before it), steps the optimizer and
+        zeroes the gradients.  Returns the un-normalised training_step loss."""
+        k = self.accumulate_grad_batches
+        self._micro += 1
+        boundary = self._micro % k == 0
+        if allreduce is not None:
+            allreduce.sync = boundary
+        loss = self.training_step(batch)
+        (loss / k if k > 1 else loss).backward()
+        if boundary:
+            if allreduce is not None:
+                allreduce()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
         return loss
 
     def configure_optimizers(self):

@@ -65,11 +65,11 @@ class PPEG(nn.Module):
 
 class _TransMILFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine, names, drop_p, seed_dev, holder, x, *params):
+    def forward(ctx, engine, names, drop_p, seed_dev, holder, bucket, x, *params):
         prm = dict(zip(names, params))
         with torch.cuda.device(x.device):   # kernels go to x's device and its current stream
             logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev)
-        ctx.engine, ctx.c, ctx.names, ctx.prm = engine, c, names, prm
+        ctx.engine, ctx.c, ctx.names, ctx.prm, ctx.bucket = engine, c, names, prm, bucket
         if holder is not None:
             holder["ctx"] = c
         return logits
@@ -80,10 +80,30 @@ class _TransMILFn(torch.autograd.Function):
             raise RuntimeError("TransMIL (fused HIP path): the saved activations were freed by the first "
                                "backward; retain_graph=True is not supported on the fused path -- set "
                                "model.fused = False (module-by-module path) to backpropagate twice")
+        head = (None,) * 7
+        bucket, prm = ctx.bucket, ctx.prm
+        dl = dlogits.float().contiguous()
         with torch.cuda.device(dlogits.device):
-            g = ctx.engine.backward(dlogits.float().contiguous(), ctx.c, ctx.prm)
-        ctx.c = None
-        return (None, None, None, None, None, None) + tuple(g[n] for n in ctx.names)
+            if bucket is not None and all(p.grad is None for p in prm.values()):
+                # first micro-batch after zero_grad: the kernels write straight into the bucket and
+                # the parameters' .grad become its views (stable addresses: hipGraph-safe, no copy)
+                views = {n: bucket.view(p) for n, p in prm.items()}
+                ctx.engine.backward(dl, ctx.c, prm, out=views, ready=bucket.ready)
+                ctx.c = None
+                with torch.no_grad():
+                    for n, p in prm.items():
+                        p.grad = views[n]
+                return head + (None,) * len(ctx.names)
+            g = ctx.engine.backward(dl, ctx.c, prm)
+            ctx.c = None
+            if bucket is not None and all(bucket.owns(p) for p in prm.values()):
+                # gradient accumulation (accumulate_grad_batches > 1): add into the bucket views
+                with torch.no_grad():
+                    torch._foreach_add_([p.grad for p in prm.values()], [g[n] for n in ctx.names])
+                bucket.ready(0)
+                bucket.ready(1)
+                return head + (None,) * len(ctx.names)
+        return head + tuple(g[n] for n in ctx.names)
 
 
 class TransMIL(nn.Module):
@@ -110,6 +130,7 @@ class TransMIL(nn.Module):
 
     # False: always run module by module (what a hook on a submodule switches to by itself)
     fused = True
+    _grad_bucket = None   # interface.GradBucket the fused backward writes into (attach_grad_bucket)
     _head = "_fc"     # class-token Linear (code/models/TransMIL.py:155)
 
     def _fc1_layout(self):
@@ -124,6 +145,18 @@ class TransMIL(nn.Module):
         raise NotImplementedError(
             f"in_features={self.in_features}: only the Linear+GELU (code/models/TransMIL.py:128-133) and "
             "in_features=2048 (:100-111) _fc1 branches run on the HIP path")
+
+    def grad_bucket_parts(self):
+        """Parameters in the order their gradients become final in the fused backward: part 0 =
+        head, norm, layer2, PPEG (ready before layer1's backward starts), part 1 = layer1,
+        class token, _fc1."""
+        first = (self._head + ".", "norm.", "layer2.", "pos_layer.")
+        named = list(self.named_parameters())
+        return [[p for n, p in named if n.startswith(first)], [p for n, p in named if not n.startswith(first)]]
+
+    def attach_grad_bucket(self, bucket):
+        """Route the fused backward's parameter gradients into ``bucket`` (interface.GradBucket)."""
+        self._grad_bucket = bucket
 
     def _hooked(self):
         """A forward / backward hook on any submodule (GradCAM on model.norm or
@@ -192,7 +225,7 @@ class TransMIL(nn.Module):
             seed_dev = self._dropout_counter.clone()   # snapshot for this forward's backward
         holder = {} if return_attn else None
         engine = TransMILEngine(self.compute_dtype, fc1=layout, head=self._head)
-        logits = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, x, *params)
+        logits = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, self._grad_bucket, x, *params)
         if return_attn:
             c = holder["ctx"]
             S = c["geo"].S
