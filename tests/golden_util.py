@@ -32,3 +32,9 @@ def oracle_model(fx, dtype=torch.float64):
     m = TransMIL(n_classes=ncls, in_features=feat, out_features=feat)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in meta.items()})
     return m.to(dtype).eval()
+
+
+def sibling_input(name):
+    """Input of a make_golden_siblings.py case: PCG64(seed).random(input_shape) (float32)."""
+    meta = index()[name]
+    return np.random.default_rng(meta["seed"]).random(tuple(meta["input_shape"]), dtype=np.float32)

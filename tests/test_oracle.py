@@ -10,7 +10,7 @@ import torch
 
 from golden_util import index, load, oracle_model, bag_input
 
-SMALL = [k for k, v in index().items() if v["feat"] == 64]
+SMALL = [k for k, v in index().items() if v.get("feat") == 64]
 
 
 def _forward(model, x, grad=False, label=None, ncls=2):
@@ -184,3 +184,39 @@ def test_c3_oracle_fixture_matches_reference_fixture():
     a, b = load("d512c3_n32768"), load("d512c3_ref_n32768")
     np.testing.assert_allclose(a["logits.f64"], b["logits.f64"], rtol=0, atol=1e-9)
     np.testing.assert_allclose(a["logits"], b["logits"], rtol=0, atol=1e-5)
+
+
+SIBLINGS = ["transmil768_n300", "ctmil_c64_g20_b2", "ctmil_c128_g36", "transformermil768_n200_b2",
+            "transformermil2048_n64", "attmil2048_n500", "attmil1024_n300"]
+
+
+def sibling_oracle(name, dtype=torch.float32):
+    """The oracle model of a make_golden_siblings.py case, deterministic weights, eval mode."""
+    from oracle import siblings_ref
+    from oracle.transmil_ref import TransMIL, deterministic_params_
+    meta = index()[name]
+    klass = TransMIL if meta["model"] == "TransMIL" else getattr(siblings_ref, meta["model"])
+    torch.manual_seed(0)
+    m = klass(**meta["ctor"])
+    deterministic_params_(m, 2021)
+    return m.to(dtype).eval()
+
+
+@pytest.mark.parametrize("name", SIBLINGS)
+def test_sibling_oracles_match_reference_fixture(name):
+    """oracle/siblings_ref.py (and the 768 branch of oracle/transmil_ref.py) against logits of
+    the reference's own CTMIL.py / TransformerMIL.py / AttMIL.py / TransMIL.py (fp32 within
+    summation-order noise; fp64 to 1e-10)."""
+    from golden_util import sibling_input
+    ref = load(name)
+    x = torch.from_numpy(sibling_input(name))
+    orig = torch.Tensor.float
+    with torch.no_grad():
+        out = sibling_oracle(name)(x).numpy()
+        torch.Tensor.float = lambda self, *a, **k: self     # TransMIL casts the bag to fp32 (:174)
+        try:
+            out64 = sibling_oracle(name, torch.float64)(x.double()).numpy()
+        finally:
+            torch.Tensor.float = orig
+    np.testing.assert_allclose(out, ref["logits"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(out64, ref["logits.f64"], rtol=1e-10, atol=1e-12)

@@ -374,6 +374,9 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
 # grid-padded (``main``) and the optional Linear + GELU + LayerNorm stage before it (``inner``)
 FC1_PLAIN = {"main": "_fc1.0", "inner": None}                                  # TransMIL.py:128-133
 FC1_RCC2048 = {"main": "_fc1.3", "inner": ("_fc1.0", "_fc1.2")}               # TransMIL.py:100-111
+# input already embedded to D (the 768 _fc1 branch run by ops, TransMIL.py:122-126; CTMIL's conv
+# stack, CTMIL.py:137-141): grid pad + class token only, and the backward returns dL/dx
+FC1_EMBED = {"main": None, "inner": None}
 
 
 class TransMILEngine:
@@ -423,16 +426,19 @@ class TransMILEngine:
         D = params["norm.weight"].shape[0]
         p = {"D": D}
         main, inner = self.fc1["main"], self.fc1["inner"]
-        ws = [params[main + ".weight"], params["layer1.attn.to_qkv.weight"], params["layer1.attn.to_out.0.weight"],
+        ws = [params["layer1.attn.to_qkv.weight"], params["layer1.attn.to_out.0.weight"],
               params["layer2.attn.to_qkv.weight"], params["layer2.attn.to_out.0.weight"]]
+        if main is not None:
+            ws.append(params[main + ".weight"])
         if inner is not None:
             ws.append(params[inner[0] + ".weight"])
         ws = self._cast_many(ws, pool)
-        w1, wqkv1, wo1, wqkv2, wo2 = ws[:5]
-        p["w1"] = w1
-        p["b1"] = params[main + ".bias"]
+        wqkv1, wo1, wqkv2, wo2 = ws[:4]
+        if main is not None:
+            p["w1"] = ws[4]
+            p["b1"] = params[main + ".bias"]
         if inner is not None:
-            p["w0"], p["b0"] = ws[5], params[inner[0] + ".bias"]
+            p["w0"], p["b0"] = ws[5], params[inner[0] + ".bias"]   # inner implies main
             p["ln0_w"], p["ln0_b"] = params[inner[1] + ".weight"], params[inner[1] + ".bias"]
         p["cls"] = params["cls_token"]
         for li, (wqkv, wo) in ((1, (wqkv1, wo1)), (2, (wqkv2, wo2))):
@@ -471,7 +477,12 @@ class TransMILEngine:
         geo = Geometry(B, N, F, D, heads)
         prm = self.prepare(params, pool)
         st = _stream()
-        xt = self._cast(x.reshape(B * N, F), pool) if self.dt_code == BF16 else x.reshape(B * N, F).contiguous()
+        if self.fc1["main"] is None:
+            xt = None
+        elif self.dt_code == BF16:
+            xt = self._cast(x.reshape(B * N, F), pool)
+        else:
+            xt = x.reshape(B * N, F).contiguous()
         inner = None
         if self.fc1["inner"] is not None:
             # inner stage: y0 = GELU(x W0^T + b0) (fp32, pre-activation kept), then LayerNorm -> T,
@@ -489,9 +500,18 @@ class TransMILEngine:
             xt, F = xln, Fm
         # _fc1: Linear + GELU, grid pad (duplicate the first `add` rows) and class token
         H0 = pool(B * geo.S * D).view(B * geo.S, D)
-        pre = pool(B * N * D).view(B * N, D)   # fp32 pre-activation for the GELU backward
-        gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
-             bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
+        if self.fc1["main"] is None:
+            if F != D:
+                raise ValueError(f"pre-embedded input must be [B, N, {D}], got F={F}")
+            pre = None
+            H0v, xe = H0.view(B, geo.S, D), x.reshape(B, N, D)
+            H0v[:, 1:N + 1].copy_(xe)
+            if geo.add:
+                H0v[:, N + 1:].copy_(xe[:, :geo.add])
+        else:
+            pre = pool(B * N * D).view(B * N, D)   # fp32 pre-activation for the GELU backward
+            gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
+                 bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
         _lib.call("tm_put_cls", _p(prm["cls"]), B, geo.S, D, _p(H0), st)
         H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0], seed_dev)
         H2 = pool(B * geo.S * D).view(B * geo.S, D)
@@ -544,6 +564,17 @@ class TransMILEngine:
                 dH = dH1
                 if ready is not None:
                     ready(0)
+        if self.fc1["main"] is None:
+            # pre-embedded input: dL/dx = the token rows + the duplicated pad rows folded back
+            dHv = dH.view(B, S, D)
+            dx = dHv[:, 1:N + 1].clone()
+            if geo.add:
+                dx[:, :geo.add] += dHv[:, N + 1:]
+            torch.sum(dHv[:, 0], dim=0, out=g["cls_token"].view(D))
+            g["__dx__"] = dx
+            if ready is not None:
+                ready(1)
+            return g
         # _fc1 backward (GELU + grid-pad fold) and the class token
         dpre = pool(B * N * D, self.tdtype).view(B * N, D)
         _lib.call("tm_fc1_gelu_bwd", self.dt_code, _p(dH), _p(ctx["pre"]), B, N, S, geo.add, D, _p(dpre),

@@ -28,7 +28,7 @@ import math
 import torch
 import torch.nn as nn
 
-from ..engine import TransMILEngine, NystromEngine, FC1_PLAIN, FC1_RCC2048
+from ..engine import TransMILEngine, NystromEngine, FC1_PLAIN, FC1_RCC2048, FC1_EMBED
 from ..nystrom_attention import NystromAttention, AttentionMap
 from .. import ops
 
@@ -88,13 +88,14 @@ class _TransMILFn(torch.autograd.Function):
                 # first micro-batch after zero_grad: the kernels write straight into the bucket and
                 # the parameters' .grad become its views (stable addresses: hipGraph-safe, no copy)
                 views = {n: bucket.view(p) for n, p in prm.items()}
-                ctx.engine.backward(dl, ctx.c, prm, out=views, ready=bucket.ready)
+                dx = ctx.engine.backward(dl, ctx.c, prm, out=views, ready=bucket.ready).pop("__dx__", None)
                 ctx.c = None
                 with torch.no_grad():
                     for n, p in prm.items():
                         p.grad = views[n]
-                return head + (None,) * len(ctx.names)
+                return head[:6] + (dx,) + (None,) * len(ctx.names)
             g = ctx.engine.backward(dl, ctx.c, prm)
+            dx = g.pop("__dx__", None)
             ctx.c = None
             if bucket is not None and all(bucket.owns(p) for p in prm.values()):
                 # gradient accumulation (accumulate_grad_batches > 1): add into the bucket views
@@ -102,8 +103,8 @@ class _TransMILFn(torch.autograd.Function):
                     torch._foreach_add_([p.grad for p in prm.values()], [g[n] for n in ctx.names])
                 bucket.ready(0)
                 bucket.ready(1)
-                return head + (None,) * len(ctx.names)
-        return head + tuple(g[n] for n in ctx.names)
+                return head[:6] + (dx,) + (None,) * len(ctx.names)
+        return head[:6] + (dx,) + tuple(g[n] for n in ctx.names)
 
 
 class TransMIL(nn.Module):
@@ -138,13 +139,33 @@ class TransMIL(nn.Module):
             return FC1_PLAIN
         if self.in_features == 2048 and len(self._fc1) == 5:
             return FC1_RCC2048
+        if self.in_features == 768 and len(self._fc1) == 8:
+            return FC1_EMBED
         if self.in_features == 1024:
             raise NotImplementedError(
                 "in_features=1024: the reference's branch (code/models/TransMIL.py:117-121) applies "
                 "LayerNorm(out_features=512) to a 1024-wide activation and fails; it has no HIP path")
         raise NotImplementedError(
-            f"in_features={self.in_features}: only the Linear+GELU (code/models/TransMIL.py:128-133) and "
-            "in_features=2048 (:100-111) _fc1 branches run on the HIP path")
+            f"in_features={self.in_features}: only the Linear+GELU (code/models/TransMIL.py:128-133), "
+            "in_features=2048 (:100-111) and in_features=768 (:122-126) _fc1 branches run on the HIP path")
+
+    def _embed_768(self, x):
+        """The 768 branch (code/models/TransMIL.py:122-126) on the HIP ops: Linear(768,768)+GELU,
+        Dropout(0.6), LayerNorm(768), Linear(768,512)+GELU, Dropout(0.6), LayerNorm(512)."""
+        f = self._fc1
+        h = ops.linear_gelu(f[0], x)
+        h = f[2](h)
+        h = f[3](h)
+        h = ops.linear_gelu(f[4], h)
+        h = f[6](h)
+        return f[7](h)
+
+    def _engine_params(self, layout):
+        """(names the engine reads, parameters): every parameter, minus an _fc1 the engine does
+        not run (pre-embedded input)."""
+        named = [(n, p) for n, p in self.named_parameters()
+                 if not (layout is FC1_EMBED and n.startswith("_fc1."))]
+        return tuple(n for n, _ in named), tuple(p for _, p in named)
 
     def grad_bucket_parts(self):
         """Parameters in the order their gradients become final in the fused backward: part 0 =
@@ -155,8 +176,9 @@ class TransMIL(nn.Module):
         return [[p for n, p in named if n.startswith(first)], [p for n, p in named if not n.startswith(first)]]
 
     def attach_grad_bucket(self, bucket):
-        """Route the fused backward's parameter gradients into ``bucket`` (interface.GradBucket)."""
-        self._grad_bucket = bucket
+        """Route the fused backward's parameter gradients into ``bucket`` (interface.GradBucket).
+        Not with a pre-embedded input: its _fc1 gradients come later, from autograd."""
+        self._grad_bucket = None if self._fc1_layout() is FC1_EMBED else bucket
 
     def _hooked(self):
         """A forward / backward hook on any submodule (GradCAM on model.norm or
@@ -177,10 +199,15 @@ class TransMIL(nn.Module):
         class token, layer1, PPEG, layer2, norm (all S tokens), _fc on the class token."""
         B, N, _ = x.shape
         G = int(math.ceil(math.sqrt(N)))
-        if self._fc1_layout() is FC1_RCC2048:           # :101-110 inner Linear + GELU + LayerNorm
+        layout = self._fc1_layout()
+        if layout is FC1_RCC2048:           # :101-110 inner Linear + GELU + LayerNorm
             x = ops.linear_gelu(self._fc1[0], x)
             x = self._fc1[2](x)
             h = ops.embed(self._fc1[3], self.cls_token, x)
+        elif layout is FC1_EMBED:
+            x = self._embed_768(x)
+            add = G * G - N
+            h = torch.cat([self.cls_token.expand(B, -1, -1), x, x[:, :add]], dim=1)
         else:
             h = ops.embed(self._fc1[0], self.cls_token, x)   # :175-186
         h, _ = self.layer1(h)                           # :196
@@ -216,8 +243,9 @@ class TransMIL(nn.Module):
             # hooks, or a gradient w.r.t. the input (feature saliency): the module-by-module path,
             # whose ops also return dL/dx; the fused node returns parameter gradients only
             return self._forward_modules(x, return_attn)
-        names = tuple(n for n, _ in self.named_parameters())
-        params = tuple(p for _, p in self.named_parameters())
+        if layout is FC1_EMBED:
+            x = self._embed_768(x).contiguous()
+        names, params = self._engine_params(layout)
         drop_p = self.layer1.attn.to_out[1].p if self.training else 0.0
         seed_dev = None
         if drop_p > 0:
