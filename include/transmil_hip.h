@@ -183,6 +183,20 @@ int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const floa
                 float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
                 float* db3, void* stream);
 
+/* ---- AttMIL gated attention pooling (attmil.hip) -- code/models/AttMIL.py:88-110 ----
+ * Z [N, 2D] = H [Wv;Wu]^T + [bv;bu] (caller's GEMM), H [N, L], w [D] / b [1] = attention_weights,
+ * Wc [C, L] / bc [C] = classifier.  Forward writes a [N] scores, p [N] softmax weights, M [L] pooled
+ * bag and logits [C]; backward writes dZ [N, 2D], dH [N, L] = p dM (the caller's GEMM then adds
+ * dZ [Wv;Wu]), dM [L], dw [D], db [1], dWc [C, L], dbc [C].  fp32; work sized by the queries. */
+long long tm_attmil_fwd_workspace(int N, int L);
+int tm_attmil_fwd(const float* Z, const float* H, const float* w, const float* b, const float* Wc,
+                  const float* bc, int N, int L, int D, int C, float* work, float* a, float* p, float* M,
+                  float* logits, void* stream);
+long long tm_attmil_bwd_workspace(int N, int L, int D);
+int tm_attmil_bwd(const float* Z, const float* H, const float* w, const float* p, const float* M,
+                  const float* Wc, const float* dlogits, int N, int L, int D, int C, float* work,
+                  float* dZ, float* dH, float* dM, float* dw, float* db, float* dWc, float* dbc, void* stream);
+
 /* ---- glue (glue.hip) -- code/models/TransMIL.py:177-186 ------------------ */
 int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream);
 int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int pad, int D, float p,

@@ -107,6 +107,10 @@ _SIGS = {
     "tm_ppeg_fwd": (I, [P, I, I, I, P, P, P, P]),
     "tm_ppeg_bwd_workspace": (L, [I, I, I]),
     "tm_ppeg_bwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
+    "tm_attmil_fwd_workspace": (L, [I, I]),
+    "tm_attmil_fwd": (I, [P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P]),
+    "tm_attmil_bwd_workspace": (L, [I, I, I]),
+    "tm_attmil_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P, P]),
     "tm_put_cls": (I, [P, I, I, I, P, P]),
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),

@@ -248,9 +248,11 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, int B, int C,
     case 64: { constexpr int VPL = 1; CALL; break; }    \
     case 128: { constexpr int VPL = 2; CALL; break; }   \
     case 256: { constexpr int VPL = 4; CALL; break; }   \
+    case 384: { constexpr int VPL = 6; CALL; break; }   \
     case 512: { constexpr int VPL = 8; CALL; break; }   \
+    case 768: { constexpr int VPL = 12; CALL; break; }  \
     case 1024: { constexpr int VPL = 16; CALL; break; } \
-    default: tm_set_error("layernorm: D must be 64/128/256/512/1024"); return 1; \
+    default: tm_set_error("layernorm: D must be 64/128/256/384/512/768/1024"); return 1; \
   }
 
 extern "C" int tm_layernorm_fwd(const float* x, const float* gamma, const float* beta, float eps, int rows, int D,

@@ -17,9 +17,10 @@ oracle).  There is no CPU / eager fallback: a CPU tensor raises.
 Supported _fc1 branches: ``Linear(in, out) + GELU`` for ``in_features`` not in
 {2048, 1024, 768} (:128-133, every d=512 config), and the RCC ``in_features = 2048``
 branch ``Linear(2048,1024) + GELU + LayerNorm(1024) + Linear(1024,512) + GELU``
-(:100-111, the RetCCL-feature config).  The 1024 branch raises, as the reference's does
-(its LayerNorm(out_features) meets a 1024-wide input, :117-121); the 768 branch raises
-(not on the HIP path).  ``dim_head`` is fixed at 64 by TransLayer (dim // 8, dim = 512).
+(:100-111, the RetCCL-feature config), and the 768 branch (:122-126: two Linear+GELU on the HIP
+GEMM with Dropout and HIP LayerNorms, then the engine's pre-embedded-input mode).  The 1024
+branch raises, as the reference's does (its LayerNorm(out_features) meets a 1024-wide input,
+:117-121).  ``dim_head`` is fixed at 64 by TransLayer (dim // 8, dim = 512).
 """
 from __future__ import annotations
 
@@ -149,7 +150,7 @@ class TransMIL(nn.Module):
             f"in_features={self.in_features}: only the Linear+GELU (code/models/TransMIL.py:128-133), "
             "in_features=2048 (:100-111) and in_features=768 (:122-126) _fc1 branches run on the HIP path")
 
-    def _embed_768(self, x):
+    def _pre_embed(self, x):
         """The 768 branch (code/models/TransMIL.py:122-126) on the HIP ops: Linear(768,768)+GELU,
         Dropout(0.6), LayerNorm(768), Linear(768,512)+GELU, Dropout(0.6), LayerNorm(512)."""
         f = self._fc1
@@ -205,7 +206,7 @@ class TransMIL(nn.Module):
             x = self._fc1[2](x)
             h = ops.embed(self._fc1[3], self.cls_token, x)
         elif layout is FC1_EMBED:
-            x = self._embed_768(x)
+            x = self._pre_embed(x)
             add = G * G - N
             h = torch.cat([self.cls_token.expand(B, -1, -1), x, x[:, :add]], dim=1)
         else:
@@ -244,7 +245,11 @@ class TransMIL(nn.Module):
             # whose ops also return dL/dx; the fused node returns parameter gradients only
             return self._forward_modules(x, return_attn)
         if layout is FC1_EMBED:
-            x = self._embed_768(x).contiguous()
+            x = self._pre_embed(x).contiguous()
+        return self._fused(x, layout, return_attn)
+
+    def _fused(self, x, layout, return_attn):
+        """The fused engine node: x [B, N, F] (F = D for a pre-embedded input) -> logits."""
         names, params = self._engine_params(layout)
         drop_p = self.layer1.attn.to_out[1].p if self.training else 0.0
         seed_dev = None
@@ -265,7 +270,8 @@ class TransMIL(nn.Module):
 
 def _reference_fc1(in_features, out_features, norm_layer):
     """Parameter layout of the other _fc1 branches (:100-126), kept so their
-    checkpoints load; their forward is not on the HIP path yet."""
+    checkpoints load (the 2048 and 768 branches run on the HIP path, the 1024 one raises as in
+    the reference)."""
     if in_features == 2048:
         return nn.Sequential(nn.Linear(in_features, in_features // 2), nn.GELU(), norm_layer(in_features // 2),
                              nn.Linear(in_features // 2, out_features), nn.GELU())

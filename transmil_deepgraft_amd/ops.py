@@ -198,17 +198,20 @@ def linear_gelu(lin, x):
 
 
 class _LinearFn(torch.autograd.Function):
-    """y = x W^T + b (fp32) on the HIP GEMM; backward dX = dY W, dW = dY^T X, db = colsum dY."""
+    """y = x W^T (+ b) (fp32) on the HIP GEMM, x [..., K]; backward dX = dY W, dW = dY^T X,
+    db = colsum dY."""
 
     @staticmethod
     def forward(ctx, x, w, b):
-        M, K = x.shape
-        Nout = w.shape[0]
-        xc = x.contiguous()
+        shp = x.shape
+        K = shp[-1]
+        xc = x.reshape(-1, K).contiguous()
+        M, Nout = xc.shape[0], w.shape[0]
         y = torch.empty(M, Nout, device=x.device)
         gemm(xc, w.contiguous(), y, M, Nout, K, lda=K, ldb=K, ldc=Nout, dtype=F32, c_dtype=F32, bias=b)
         ctx.save_for_backward(xc, w)
-        return y
+        ctx.shp, ctx.has_bias = shp, b is not None
+        return y.view(*shp[:-1], Nout)
 
     @staticmethod
     def backward(ctx, dy):
@@ -218,21 +221,31 @@ class _LinearFn(torch.autograd.Function):
         pool = Pool(dy.device)
         # the GEMM wants 16-B leading dimensions: pad the output features (n_classes) to 4
         Np = (Nout + 3) // 4 * 4
-        dyp = torch.zeros(M, Np, device=dy.device)
-        dyp[:, :Nout] = dy
-        wp = torch.zeros(Np, K, device=dy.device)
-        wp[:Nout] = w
-        dx = torch.empty(M, K, device=dy.device)
-        gemm(dyp, wp, dx, M, K, Np, lda=Np, ldb=K, ldc=K, b_kn=1, dtype=F32, c_dtype=F32)
+        dy2 = dy.float().reshape(M, Nout)
+        if Np != Nout:
+            dyp = torch.zeros(M, Np, device=dy.device)
+            dyp[:, :Nout] = dy2
+            wp = torch.zeros(Np, K, device=dy.device)
+            wp[:Nout] = w
+        else:
+            dyp, wp = dy2.contiguous(), w.contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(M, K, device=dy.device)
+            gemm(dyp, wp, dx, M, K, Np, lda=Np, ldb=K, ldc=K, b_kn=1, dtype=F32, c_dtype=F32)
+            dx = dx.view(ctx.shp)
         dw = torch.empty(Np, K, device=dy.device)
         weight_grad(dyp, x, dw, Np, K, M, ldy=Np, ldx=K, dtype=F32, work_pool=pool)
-        db = torch.empty(Np, device=dy.device)
-        colsum(dyp, M, Np, Np, F32, db, pool)
-        return dx, dw[:Nout], db[:Nout]
+        db = None
+        if ctx.has_bias:
+            db = torch.empty(Np, device=dy.device)
+            colsum(dyp, M, Np, Np, F32, db, pool)
+            db = db[:Nout]
+        return dx, dw[:Nout], db
 
 
 def linear(module, x):
-    """``nn.Linear`` forward on the HIP GEMM (x [M, K] fp32)."""
+    """``nn.Linear`` forward on the HIP GEMM (x [..., K] fp32; bias optional)."""
     if not x.is_cuda:
         raise RuntimeError("HIP Linear needs a GPU tensor")
     return _LinearFn.apply(x.float(), module.weight, module.bias)
