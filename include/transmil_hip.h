@@ -197,6 +197,14 @@ int tm_attmil_bwd(const float* Z, const float* H, const float* w, const float* p
                   const float* Wc, const float* dlogits, int N, int L, int D, int C, float* work,
                   float* dZ, float* dH, float* dM, float* dw, float* db, float* dWc, float* dbc, void* stream);
 
+/* ---- feature-bag sampling (bags.hip) -- code/datasets/feature_dataloader.py:335-431 ----
+ * dst[r] = src[i0[r]] (i1 NULL or i1[r] < 0), (src[i0[r]] * wa[r]) + (src[i1[r]] * wb[r]) (mixup),
+ * or 0 (i0[r] < 0); src [*, F] and dst [nrows, F] of dtype TM_F32 / TM_BF16, i0/i1 int64 row
+ * ids into src (device), nrows <= 65535.  Replaces the per-item indexing of
+ * FeatureBagLoader.__getitem__ (:346-362) and data_interface.simple_collate's stack (:238-246). */
+int tm_gather_rows(int dtype, const void* src, int F, const long long* i0, const long long* i1,
+                   const float* wa, const float* wb, int nrows, void* dst, void* stream);
+
 /* ---- glue (glue.hip) -- code/models/TransMIL.py:177-186 ------------------ */
 int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream);
 int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int pad, int D, float p,
