@@ -1,0 +1,112 @@
+"""BASELINE config C5 on one MI355X: on-GPU RetCCL ResNet-50 tile encoder + TransMIL(2048).
+
+One step = tiles [1, N, 3, 224, 224] (bf16, resident in HBM) -> frozen encoder (train-mode
+BatchNorm as the reference runs it under Lightning, or --encoder-mode eval: BN folded into the
+convolutions) -> features [1, N, 2048] on the device -> TransMIL(2, 2048) fwd (RCC _fc1 branch,
+dropout on) -> CE -> bwd -> Lookahead(RAdam).  Prints one JSON line: slides/sec, ms/step, the
+encoder alone (ms, tiles/s, achieved TFLOP/s against the dense bf16 peak), the MIL part alone.
+
+    python scripts/bench_c5.py [--n 4096] [--steps 5] [--warmup 2] [--encoder-mode train|eval]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+BF16_PEAK_TFS = 2500.0
+R50_GFLOP_PER_TILE = 4.09   # ResNet-50 forward at 224x224, multiply-adds x 2 (conv + fc-free)
+
+
+def timed(fn, steps):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--encoder-mode", default="train", choices=["train", "eval"])
+    ap.add_argument("--chunk", type=int, default=512)
+    ap.add_argument("--graph", action="store_true", help="capture the step in a hipGraph")
+    a = ap.parse_args()
+    from transmil_deepgraft_amd.encoder import ImageBagModel, retccl_resnet50
+    from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
+    from transmil_deepgraft_amd.models import TransMIL
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    enc = retccl_resnet50(chunk=a.chunk).to(dev).set_compute_dtype(torch.bfloat16)
+    enc = enc.to(memory_format=torch.channels_last)
+    enc.train(a.encoder_mode == "train")
+    mil = TransMIL(2, 2048, 512).to(dev).train()
+    model = ImageBagModel(enc, mil)
+    task = TransMILTask(mil)
+    opt = task.configure_optimizers()[0][0]
+    GradAllReduce(mil.parameters(), model=mil)        # gradient bucket (no-op collective at N = 1)
+    g = torch.Generator(device=dev).manual_seed(7)
+    tiles = torch.randn(1, a.n, 3, 224, 224, device=dev, generator=g).to(torch.bfloat16)
+    label = torch.tensor([1], device=dev)
+
+    def step():
+        logits = model(tiles)
+        loss = task.loss(logits, torch.nn.functional.one_hot(label, 2).float())
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+
+    for _ in range(a.warmup):
+        step()
+    run = step
+    if a.graph:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        run = graph.replay
+    t_step = timed(run, a.steps)
+    with torch.no_grad():
+        t_enc = timed(lambda: enc(tiles[0]), a.steps)
+        feats = enc(tiles[0])[None]
+
+    def mil_step():
+        loss = task.loss(mil(feats), torch.nn.functional.one_hot(label, 2).float())
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    t_mil = timed(mil_step, a.steps)
+    enc_tfs = R50_GFLOP_PER_TILE * a.n / t_enc / 1e3
+    print(json.dumps({
+        "metric": f"slides/sec (fwd+bwd) end-to-end, RetCCL ResNet-50 encoder + TransMIL(2048), N={a.n} tiles",
+        "value": round(1.0 / t_step, 3), "unit": "slides/sec", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(t_step * 1e3, 3), "higher_is_better": True, "dtype": "bf16",
+        "data": "synthetic (randn tiles resident in HBM, random-init weights)",
+        "config": {"workload": f"C5: 1 slide x {a.n} tiles 3x224x224 -> ResNet-50 (frozen, BN "
+                               f"{'batch stats' if a.encoder_mode == 'train' else 'folded'}) -> TransMIL 2-class",
+                   "execution": "hipGraph" if a.graph else "eager", "chunk": a.chunk},
+        "encoder": {"ms": round(t_enc * 1e3, 3), "tiles_per_s": round(a.n / t_enc, 1),
+                    "achieved_tfs": round(enc_tfs, 1), "peak_tfs": BF16_PEAK_TFS,
+                    "frac": round(enc_tfs / BF16_PEAK_TFS, 4), "mode": a.encoder_mode,
+                    "flops_note": f"{R50_GFLOP_PER_TILE} GFLOP per 224x224 tile (ResNet-50 forward)"},
+        "mil_ms": round(t_mil * 1e3, 3),
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()

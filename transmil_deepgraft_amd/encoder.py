@@ -1,0 +1,184 @@
+"""On-GPU RetCCL ResNet-50 tile encoder for the image path (BASELINE config 5).
+
+Replaces ``ModelInterface``'s ``backbone == 'retccl'`` feature extractor
+(code/models/model_interface.py:237-247: ``ResNet.resnet50(num_classes=128, mlp=False,
+two_branch=False, normlinear=True)``, checkpoint loaded with ``strict=False``, every parameter
+frozen, ``fc = Identity``) and the image branch of ``ModelInterface.forward`` (:300-316:
+``[B, bag, 3, 224, 224] -> [B*bag, 3, 224, 224] -> model_ft -> [B, bag, 2048] -> model``).
+
+Same module / parameter / buffer names as code/models/ResNet.py (ResNet :130-277, Bottleneck
+:75-117, resnet50 :309), so a RetCCL checkpoint loads unchanged.  MI355X-first execution:
+
+* channels-last bf16 activations (``compute_dtype``), PyTorch-ROCm (MIOpen) convolutions --
+  the encoder is frozen and outside the hand-written NystromAttention/PPEG path;
+* in eval mode every BatchNorm is folded into its convolution once (weights rescaled, bias
+  added) -- 53 conv launches, no separate normalisation passes;
+* in train mode the BatchNorms run as written (batch statistics, running-stat updates), as the
+  reference's frozen-but-train-mode encoder does under Lightning;
+* tiles go through in chunks (``chunk`` tiles, default 512) so the activation peak stays a few
+  GB whatever the bag size, and the [B*bag, 2048] features stay on the device for the fused
+  TransMIL engine (no host round trip).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Bottleneck(nn.Module):
+    """1x1 -> 3x3 (stride) -> 1x1 x4 with BN after each, residual + ReLU (ResNet.py:75-117)."""
+
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, momentum_bn=0.1):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(planes, momentum=momentum_bn)
+        self.conv2 = nn.Conv2d(planes, planes, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(planes, momentum=momentum_bn)
+        self.conv3 = nn.Conv2d(planes, planes * 4, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(planes * 4, momentum=momentum_bn)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+    def forward(self, x):
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        idt = self.downsample(x) if self.downsample is not None else x
+        return self.relu(out + idt)
+
+
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, dtype):
+    """conv followed by eval-mode BN as one conv: (w * g / sqrt(v + eps), b - m * g / sqrt(v + eps))."""
+    s = bn.weight.detach().double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    w = (conv.weight.detach().double() * s[:, None, None, None]).to(dtype)
+    b = (bn.bias.detach().double() - bn.running_mean.double() * s).to(dtype)
+    return w.contiguous(memory_format=torch.channels_last), b
+
+
+class RetCCLResNet50(nn.Module):
+    """``ResNet(Bottleneck, [3, 4, 6, 3])`` with ``fc = Identity``: tiles [n, 3, 224, 224] ->
+    features [n, 2048] fp32."""
+
+    def __init__(self, momentum_bn=0.1, chunk=512):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        self.bn1 = nn.BatchNorm2d(64, momentum=momentum_bn)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.layer1 = self._stage(64, 3, 1, momentum_bn)
+        self.layer2 = self._stage(128, 4, 2, momentum_bn)
+        self.layer3 = self._stage(256, 6, 2, momentum_bn)
+        self.layer4 = self._stage(512, 3, 2, momentum_bn)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Identity()                         # model_interface.py:245
+        self.compute_dtype = torch.bfloat16
+        self.chunk = chunk
+        self._folded = None
+        for p in self.parameters():                     # model_interface.py:243-244
+            p.requires_grad = False
+
+    def _stage(self, planes, blocks, stride, momentum_bn):
+        down = None
+        if stride != 1 or self.inplanes != planes * 4:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes * 4, 1, stride=stride, bias=False),
+                                 nn.BatchNorm2d(planes * 4, momentum=momentum_bn))
+        layers = [Bottleneck(self.inplanes, planes, stride, down, momentum_bn)]
+        self.inplanes = planes * 4
+        layers += [Bottleneck(self.inplanes, planes, momentum_bn=momentum_bn) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def set_compute_dtype(self, dtype):
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("compute dtype must be torch.bfloat16 or torch.float32")
+        self.compute_dtype = dtype
+        self._folded = None
+        return self
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        self._folded = None
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def train(self, mode=True):
+        self._folded = None
+        return super().train(mode)
+
+    def load_retccl_checkpoint(self, path):
+        """``load_state_dict(torch.load(path), strict=False)`` as the reference does (:242), with
+        the safe loader; the 128-way ``fc`` of the checkpoint is dropped (fc is Identity)."""
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+        return self.load_state_dict({k: v for k, v in sd.items() if not k.startswith("fc.")}, strict=False)
+
+    # ------------------------------------------------------------------ eval: folded convolutions
+    def _fold_all(self):
+        dt = self.compute_dtype
+        f = {"stem": _fold(self.conv1, self.bn1, dt), "blocks": []}
+        for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
+            for blk in stage:
+                d = None
+                if blk.downsample is not None:
+                    d = _fold(blk.downsample[0], blk.downsample[1], dt) + (blk.downsample[0].stride,)
+                f["blocks"].append((_fold(blk.conv1, blk.bn1, dt), _fold(blk.conv2, blk.bn2, dt) + (blk.stride,),
+                                    _fold(blk.conv3, blk.bn3, dt), d))
+        self._folded = f
+
+    def _forward_folded(self, x):
+        f = self._folded
+        w, b = f["stem"]
+        x = F.max_pool2d(F.relu(F.conv2d(x, w, b, stride=2, padding=3)), 3, 2, 1)
+        for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
+            y = F.relu(F.conv2d(x, w1, b1))
+            y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
+            y = F.conv2d(y, w3, b3)
+            idt = x if d is None else F.conv2d(x, d[0], d[1], stride=d[2])
+            x = F.relu(y + idt)
+        return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+    def _forward_modules(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+    def forward(self, x):
+        if not x.is_cuda:
+            raise RuntimeError("RetCCL encoder (MI355X path) needs a GPU tensor")
+        dt = self.compute_dtype
+        out = torch.empty(x.shape[0], 2048, dtype=torch.float32, device=x.device)
+        if not self.training and self._folded is None:
+            self._fold_all()
+        grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16,
+                                                          enabled=self.training and dt == torch.bfloat16):
+            for s in range(0, x.shape[0], self.chunk):
+                xc = x[s:s + self.chunk].to(dt if not self.training else torch.float32)
+                xc = xc.contiguous(memory_format=torch.channels_last)
+                y = self._forward_folded(xc) if not self.training else self._forward_modules(xc)
+                out[s:s + self.chunk] = y.float()
+        return out
+
+
+def retccl_resnet50(**kw):
+    """``ResNet.resnet50(num_classes=128, mlp=False, two_branch=False, normlinear=True)`` with
+    ``fc = Identity`` and frozen parameters (model_interface.py:238-245)."""
+    return RetCCLResNet50(**kw)
+
+
+class ImageBagModel(nn.Module):
+    """``ModelInterface.forward``'s image path (model_interface.py:300-316): tiles
+    ``[B, bag, 3, H, W]`` -> frozen encoder -> ``[B, bag, 2048]`` on the device -> the MIL model
+    (TransMIL(n_classes, 2048) runs its RCC-2048 _fc1 branch on the fused engine)."""
+
+    def __init__(self, model_ft: nn.Module, model: nn.Module):
+        super().__init__()
+        self.model_ft = model_ft
+        self.model = model
+        self.n_classes = getattr(model, "n_classes", None)
+
+    def forward(self, x):
+        B, bag = x.shape[0], x.shape[1]
+        feats = self.model_ft(x.reshape(B * bag, *x.shape[2:]))
+        return self.model(feats.view(B, bag, -1))
