@@ -42,14 +42,17 @@ def main():
     ap.add_argument("--encoder-mode", default="train", choices=["train", "eval"])
     ap.add_argument("--chunk", type=int, default=512)
     ap.add_argument("--graph", action="store_true", help="capture the step in a hipGraph")
+    ap.add_argument("--layout", default="nhwc", choices=["nhwc", "nchw"])
+    ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
     a = ap.parse_args()
+    torch.backends.cudnn.benchmark = a.benchmark
     from transmil_deepgraft_amd.encoder import ImageBagModel, retccl_resnet50
     from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
     from transmil_deepgraft_amd.models import TransMIL
     dev = torch.device("cuda", 0)
     torch.manual_seed(1234)
     enc = retccl_resnet50(chunk=a.chunk).to(dev).set_compute_dtype(torch.bfloat16)
-    enc = enc.to(memory_format=torch.channels_last)
+    enc.channels_last = a.layout == "nhwc"
     enc.train(a.encoder_mode == "train")
     mil = TransMIL(2, 2048, 512).to(dev).train()
     model = ImageBagModel(enc, mil)
@@ -99,7 +102,8 @@ def main():
         "data": "synthetic (randn tiles resident in HBM, random-init weights)",
         "config": {"workload": f"C5: 1 slide x {a.n} tiles 3x224x224 -> ResNet-50 (frozen, BN "
                                f"{'batch stats' if a.encoder_mode == 'train' else 'folded'}) -> TransMIL 2-class",
-                   "execution": "hipGraph" if a.graph else "eager", "chunk": a.chunk},
+                   "execution": "hipGraph" if a.graph else "eager", "chunk": a.chunk, "layout": a.layout,
+                   "miopen_find": a.benchmark},
         "encoder": {"ms": round(t_enc * 1e3, 3), "tiles_per_s": round(a.n / t_enc, 1),
                     "achieved_tfs": round(enc_tfs, 1), "peak_tfs": BF16_PEAK_TFS,
                     "frac": round(enc_tfs / BF16_PEAK_TFS, 4), "mode": a.encoder_mode,

@@ -60,7 +60,7 @@ def test_image_path_end_to_end():
     from transmil_deepgraft_amd.encoder import ImageBagModel
     from transmil_deepgraft_amd.models import TransMIL
     torch.manual_seed(0)
-    mil = TransMIL(2, 2048).cuda().set_compute_dtype(torch.float32)
+    mil = TransMIL(2, 2048).cuda().eval().set_compute_dtype(torch.float32)   # eval: no dropout
     enc = _encoder(torch.float32).cuda()
     model = ImageBagModel(enc, mil)
     x = torch.from_numpy(encoder_tiles(6, seed=5)).cuda().view(1, 6, 3, 224, 224)

@@ -22,6 +22,8 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ 
                                                           const float* __restrict__ wa,
                                                           const float* __restrict__ wb, int nrows,
                                                           T* __restrict__ dst) {
+  // two rounded products and one rounded add, as torch evaluates x*a + y*(1-a): no FMA contraction
+#pragma clang fp contract(off)
   constexpr int VEC = 16 / sizeof(T);
   const int r = blockIdx.y;
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) * VEC;
@@ -40,8 +42,8 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ 
       const vt x = *(const vt*)(src + (size_t)a * F + c), y = *(const vt*)(src + (size_t)b * F + c);
       const float fa = wa[r], fb = wb[r];
       for (int e = 0; e < VEC; ++e) {
-        const float p = __fmul_rn(to_f(x[e]), fa), q = __fmul_rn(to_f(y[e]), fb);
-        out[e] = from_f<T>(__fadd_rn(p, q));
+        const float p = to_f(x[e]) * fa, q = to_f(y[e]) * fb;
+        out[e] = from_f<T>(p + q);
       }
     }
     *(vt*)d = out;
@@ -53,8 +55,10 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ 
       d[e] = src[(size_t)a * F + c + e];
       continue;
     }
-    if (a >= 0) v = __fadd_rn(__fmul_rn(to_f(src[(size_t)a * F + c + e]), wa[r]),
-                              __fmul_rn(to_f(src[(size_t)b * F + c + e]), wb[r]));
+    if (a >= 0) {
+      const float p = to_f(src[(size_t)a * F + c + e]) * wa[r], q = to_f(src[(size_t)b * F + c + e]) * wb[r];
+      v = p + q;
+    }
     d[e] = from_f<T>(v);
   }
 }

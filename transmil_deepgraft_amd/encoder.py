@@ -12,7 +12,8 @@ Same module / parameter / buffer names as code/models/ResNet.py (ResNet :130-277
 * channels-last bf16 activations (``compute_dtype``), PyTorch-ROCm (MIOpen) convolutions --
   the encoder is frozen and outside the hand-written NystromAttention/PPEG path;
 * in eval mode every BatchNorm is folded into its convolution once (weights rescaled, bias
-  added) -- 53 conv launches, no separate normalisation passes;
+  added) -- no separate normalisation passes -- and every 1x1 convolution (36 of the 53) runs
+  as a hipBLASLt GEMM over the channels-last [n*h*w, c] rows with the bias (+ ReLU) epilogue;
 * in train mode the BatchNorms run as written (batch statistics, running-stat updates), as the
   reference's frozen-but-train-mode encoder does under Lightning;
 * tiles go through in chunks (``chunk`` tiles, default 512) so the activation peak stays a few
@@ -51,12 +52,12 @@ class Bottleneck(nn.Module):
         return self.relu(out + idt)
 
 
-def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, dtype):
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, dtype, cl=True):
     """conv followed by eval-mode BN as one conv: (w * g / sqrt(v + eps), b - m * g / sqrt(v + eps))."""
     s = bn.weight.detach().double() / torch.sqrt(bn.running_var.double() + bn.eps)
     w = (conv.weight.detach().double() * s[:, None, None, None]).to(dtype)
     b = (bn.bias.detach().double() - bn.running_mean.double() * s).to(dtype)
-    return w.contiguous(memory_format=torch.channels_last), b
+    return w.contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format), b
 
 
 class RetCCLResNet50(nn.Module):
@@ -78,6 +79,7 @@ class RetCCLResNet50(nn.Module):
         self.fc = nn.Identity()                         # model_interface.py:245
         self.compute_dtype = torch.bfloat16
         self.chunk = chunk
+        self.channels_last = True
         self._folded = None
         for p in self.parameters():                     # model_interface.py:243-244
             p.requires_grad = False
@@ -115,22 +117,40 @@ class RetCCLResNet50(nn.Module):
 
     # ------------------------------------------------------------------ eval: folded convolutions
     def _fold_all(self):
-        dt = self.compute_dtype
-        f = {"stem": _fold(self.conv1, self.bn1, dt), "blocks": []}
+        dt, cl = self.compute_dtype, self.channels_last
+        f = {"stem": _fold(self.conv1, self.bn1, dt, cl), "blocks": []}
         for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in stage:
                 d = None
                 if blk.downsample is not None:
-                    d = _fold(blk.downsample[0], blk.downsample[1], dt) + (blk.downsample[0].stride,)
-                f["blocks"].append((_fold(blk.conv1, blk.bn1, dt), _fold(blk.conv2, blk.bn2, dt) + (blk.stride,),
-                                    _fold(blk.conv3, blk.bn3, dt), d))
+                    d = _fold(blk.downsample[0], blk.downsample[1], dt, cl) + (blk.downsample[0].stride,)
+                f["blocks"].append((_fold(blk.conv1, blk.bn1, dt, cl), _fold(blk.conv2, blk.bn2, dt, cl) + (blk.stride,),
+                                    _fold(blk.conv3, blk.bn3, dt, cl), d))
         self._folded = f
+
+    def _conv1x1(self, x, w, b, relu, stride=1):
+        """A 1x1 convolution over a channels-last tensor IS a GEMM over its [n*h*w, c] rows:
+        hipBLASLt with the bias (+ ReLU) epilogue instead of a MIOpen convolution."""
+        if stride != 1:
+            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
+        n, c, h, wd = x.shape
+        X = x.permute(0, 2, 3, 1).reshape(n * h * wd, c)
+        W = w.reshape(w.shape[0], c).t()
+        Y = torch._addmm_activation(b, X, W) if relu else torch.addmm(b, X, W)
+        return Y.view(n, h, wd, -1).permute(0, 3, 1, 2)
 
     def _forward_folded(self, x):
         f = self._folded
+        gemm1x1 = self.channels_last and x.is_cuda
         w, b = f["stem"]
         x = F.max_pool2d(F.relu(F.conv2d(x, w, b, stride=2, padding=3)), 3, 2, 1)
         for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
+            if gemm1x1:
+                y = self._conv1x1(x, w1, b1, True)
+                y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
+                idt = x if d is None else self._conv1x1(x, d[0], d[1], False, d[2][0])
+                x = self._conv1x1(y, w3, b3, False).add_(idt).relu_()
+                continue
             y = F.relu(F.conv2d(x, w1, b1))
             y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
             y = F.conv2d(y, w3, b3)
@@ -150,12 +170,16 @@ class RetCCLResNet50(nn.Module):
         out = torch.empty(x.shape[0], 2048, dtype=torch.float32, device=x.device)
         if not self.training and self._folded is None:
             self._fold_all()
+        if self.training and self.channels_last and \
+                not self.conv1.weight.is_contiguous(memory_format=torch.channels_last):
+            self.to(memory_format=torch.channels_last)
         grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16,
                                                           enabled=self.training and dt == torch.bfloat16):
             for s in range(0, x.shape[0], self.chunk):
                 xc = x[s:s + self.chunk].to(dt if not self.training else torch.float32)
-                xc = xc.contiguous(memory_format=torch.channels_last)
+                xc = xc.contiguous(memory_format=torch.channels_last if self.channels_last
+                                   else torch.contiguous_format)
                 y = self._forward_folded(xc) if not self.training else self._forward_modules(xc)
                 out[s:s + self.chunk] = y.float()
         return out
