@@ -68,6 +68,13 @@ typedef struct tm_gemm_args {
 int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* args, void* stream);
 int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
                      int accumulate, void* stream);
+/* Deferred parameter-gradient reductions: while deferral is on, tm_splitk_reduce (and the
+ * reductions inside tm_colsum / tm_layernorm_bwd / tm_nys_conv_bwd) only queue their
+ * (slab, out) pairs; tm_reduce_flush sums every queued pair in ONE launch on `stream`.  The
+ * queue is per process (one engine per process); nothing may read a queued output before the
+ * flush. */
+int tm_reduce_defer(int on);
+int tm_reduce_flush(void* stream);
 long long tm_colsum_workspace(int rows, int cols, int rows_per_chunk);
 int tm_colsum(const void* X, int dtype, int rows, int cols, int ld, int rows_per_chunk,
               float* work, float* out, int accumulate, void* stream);
@@ -207,6 +214,14 @@ int tm_gather_rows(int dtype, const void* src, int F, const long long* i0, const
 
 /* ---- glue (glue.hip) -- code/models/TransMIL.py:177-186 ------------------ */
 int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream);
+/* CrossEntropyLoss(logits, one_hot(label).float()) mean over B rows + softmax + argmax in one
+ * launch (code/models/model_interface.py:339-347); backward dlogits = g[0] (prob - one_hot) / B.
+ * label int64 [B] on the device, values in [0, C) (not checked on the device).  class_stats
+ * (nullable, int32 [C][2]) accumulates per-class count / correct (:350-356). */
+int tm_ce_fwd(const float* logits, const long long* label, int B, int C, float* loss, float* prob,
+              long long* yhat, int* class_stats, void* stream);
+int tm_ce_bwd(const float* prob, const long long* label, int B, int C, const float* g, float* dlogits,
+              void* stream);
 int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int pad, int D, float p,
                        uint64_t seed, const uint64_t* seed_ptr, void* out, void* stream);
 /* NystromAttention eq. 1 for a raw input: [B*S, D] fp32 -> front-padded [B, n_pad, D] T */

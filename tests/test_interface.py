@@ -277,3 +277,30 @@ def test_fc1_branches_and_mdmil_state_dict_keys():
         b = {k: tuple(v.shape) for k, v in ref.state_dict().items()}
         assert a == b
     assert MDMIL(3)._head == "_fc2" and MDMIL(3).n_classes == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C", [(1, 2), (3, 3), (5, 7)])
+def test_fused_cross_entropy_matches_torch(B, C):
+    """tm_ce_fwd / tm_ce_bwd (TransMILTask.training_step on the GPU) against
+    CrossEntropyLoss(logits, one_hot(label).float()), softmax and argmax (model_interface.py:
+    321-347), and the per-class count / correct bookkeeping (:350-356)."""
+    from transmil_deepgraft_amd.interface import _CrossEntropyOneHot
+    g = torch.Generator().manual_seed(B * 10 + C)
+    logits = (torch.randn(B, C, generator=g) * 3).cuda().requires_grad_(True)
+    label = torch.randint(0, C, (B,), generator=g).cuda()
+    stats = torch.zeros(C, 2, dtype=torch.int32, device="cuda")
+    loss, prob, yhat = _CrossEntropyOneHot.apply(logits, label, stats)
+    (loss * 0.7).backward()
+    ref_logits = logits.detach().clone().requires_grad_(True)
+    ref = torch.nn.CrossEntropyLoss()(ref_logits, torch.nn.functional.one_hot(label, C).float())
+    (ref * 0.7).backward()
+    torch.testing.assert_close(loss, ref, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(prob, torch.softmax(logits.detach(), 1), rtol=1e-6, atol=1e-7)
+    assert torch.equal(yhat, torch.argmax(logits.detach(), 1))
+    torch.testing.assert_close(logits.grad, ref_logits.grad, rtol=1e-6, atol=1e-7)
+    want = torch.zeros(C, 2, dtype=torch.int32)
+    for y, h in zip(label.tolist(), yhat.tolist()):
+        want[y, 0] += 1
+        want[y, 1] += int(y == h)
+    assert torch.equal(stats.cpu(), want)

@@ -113,6 +113,10 @@ _SIGS = {
     "tm_attmil_bwd_workspace": (L, [I, I, I]),
     "tm_attmil_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P, P]),
     "tm_put_cls": (I, [P, I, I, I, P, P]),
+    "tm_reduce_defer": (I, [I]),
+    "tm_reduce_flush": (I, [P]),
+    "tm_ce_fwd": (I, [P, P, I, I, P, P, P, P, P]),
+    "tm_ce_bwd": (I, [P, P, I, I, P, P, P]),
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),

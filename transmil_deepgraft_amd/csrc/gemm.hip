@@ -635,10 +635,75 @@ extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args
 
 extern "C" void tm_debug_set_gemm_variant(int value) { g_gemm_variant = value; }
 
+// ---- deferred reductions: the parameter-gradient slab sums of a backward, queued while the
+// engine has deferral on and summed by ONE launch at tm_reduce_flush (a kernel boundary costs
+// ~4.5 us in graph replay on gfx950; a backward has ~15 such sums that nothing reads before the
+// optimizer).  Same fixed split order as splitk_reduce_kernel, so results are bit-identical.
+constexpr int DEFER_MAX = 48;
+struct ReduceEntry {
+  const float* slab;
+  float* out;
+  long long count;
+  int splits;
+  int accumulate;
+  float alpha;
+};
+struct ReduceTable {
+  ReduceEntry e[DEFER_MAX];
+  long long off[DEFER_MAX + 1];   // prefix sums of count
+  int n;
+};
+static ReduceTable g_defer{};
+static int g_defer_on = 0;
+
+__global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.off[t.n]) return;
+  int e = 0;
+  while (i >= t.off[e + 1]) ++e;
+  const ReduceEntry r = t.e[e];
+  const long long j = i - t.off[e];
+  constexpr int U = 8;
+  float s = 0.f;
+  for (int z0 = 0; z0 < r.splits; z0 += U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = r.slab[(size_t)min(z0 + u, r.splits - 1) * r.count + j];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += (z0 + u < r.splits) ? v[u] : 0.f;
+  }
+  s *= r.alpha;
+  if (r.accumulate) s += r.out[j];
+  r.out[j] = s;
+}
+
+extern "C" int tm_reduce_defer(int on) {
+  g_defer_on = on;
+  return 0;
+}
+
+extern "C" int tm_reduce_flush(void* stream) {
+  if (g_defer.n == 0) return 0;
+  const long long total = g_defer.off[g_defer.n];
+  multi_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(g_defer);
+  g_defer.n = 0;
+  g_defer.off[0] = 0;
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
                                 int accumulate, void* stream) {
   TM_REQUIRE(slab && out && splits >= 1 && count >= 0, "splitk_reduce: bad args");
   if (count == 0) return 0;
+  if (g_defer_on) {
+    if (g_defer.n == DEFER_MAX)
+      if (int rc = tm_reduce_flush(stream)) return rc;
+    g_defer.e[g_defer.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha};
+    g_defer.off[g_defer.n + 1] = g_defer.off[g_defer.n] + count;
+    ++g_defer.n;
+    return 0;
+  }
   hipStream_t st = (hipStream_t)stream;
   // float4 per thread only when that still gives >= 1024 workgroups' worth of threads
   const bool vec4 = count % 4 == 0 && count / 4 >= 256LL * 1024;

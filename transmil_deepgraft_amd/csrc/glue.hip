@@ -100,10 +100,73 @@ __global__ void cls_grad_kernel(const float* __restrict__ dH, int B, int S, int 
 
 }  // namespace
 
+// CrossEntropyLoss(logits, one_hot(label).float()) averaged over the B rows
+// (code/models/model_interface.py:346-347; the soft-target form equals -log_softmax at the label),
+// with Y_prob = softmax(logits) and Y_hat = argmax(logits) (:339-341, first index on ties) in the
+// same pass; one block.  Backward: dlogits = g (prob - one_hot) / B, g = the upstream scalar.
+__global__ void __launch_bounds__(256) ce_fwd_kernel(const float* __restrict__ logits,
+                                                     const long long* __restrict__ label, int B, int C,
+                                                     float* __restrict__ loss, float* __restrict__ prob,
+                                                     long long* __restrict__ yhat, int* __restrict__ stats) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    const float* l = logits + (size_t)b * C;
+    float m = l[0];
+    int am = 0;
+    for (int c = 1; c < C; ++c)
+      if (l[c] > m) { m = l[c]; am = c; }
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += expf(l[c] - m);
+    const float inv = 1.f / s, lse = m + logf(s);
+    for (int c = 0; c < C; ++c) prob[(size_t)b * C + c] = expf(l[c] - m) * inv;
+    acc += lse - l[label[b]];
+    yhat[b] = am;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    loss[0] = (red[0] + red[1] + red[2] + red[3]) / (float)B;
+    // the reference's per-class bookkeeping (self.data[y]["count"/"correct"], :350-356), kept on
+    // the device instead of one host sync per step
+    if (stats)
+      for (int b = 0; b < B; ++b) {
+        const int y = (int)label[b];
+        stats[2 * y] += 1;
+        stats[2 * y + 1] += yhat[b] == y;
+      }
+  }
+}
+
+__global__ void __launch_bounds__(256) ce_bwd_kernel(const float* __restrict__ prob,
+                                                     const long long* __restrict__ label, int B, int C,
+                                                     const float* __restrict__ g, float* __restrict__ dlogits) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i % C;
+  dlogits[i] = g[0] * (prob[i] - (c == (int)label[b] ? 1.f : 0.f)) / (float)B;
+}
+
 #define TM_DTYPE_DISPATCH(dt, CALL)                               \
   if ((dt) == TM_BF16) { using T = bf16; CALL; }                  \
   else if ((dt) == TM_F32) { using T = float; CALL; }             \
   else { tm_set_error("glue: dtype must be TM_F32 or TM_BF16"); return 1; }
+
+extern "C" int tm_ce_fwd(const float* logits, const long long* label, int B, int C, float* loss, float* prob,
+                         long long* yhat, int* class_stats, void* stream) {
+  TM_REQUIRE(B >= 1 && C >= 1, "ce_fwd: empty logits");
+  ce_fwd_kernel<<<1, 256, 0, (hipStream_t)stream>>>(logits, label, B, C, loss, prob, yhat, class_stats);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_ce_bwd(const float* prob, const long long* label, int B, int C, const float* g, float* dlogits,
+                         void* stream) {
+  ce_bwd_kernel<<<(B * C + 255) / 256, 256, 0, (hipStream_t)stream>>>(prob, label, B, C, g, dlogits);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream) {
   put_cls_kernel<<<B, 256, 0, (hipStream_t)stream>>>(cls, S, D, H);

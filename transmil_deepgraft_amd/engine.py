@@ -197,13 +197,41 @@ def bmm(jobs, nbatch, prec=0):
 
 
 class Pool:
-    """Scratch allocator for one forward or backward call (torch caching allocator underneath)."""
+    """Scratch allocator for one forward or backward call (torch caching allocator underneath).
+    Buffers allocated while reductions are deferred are held until the pool dies (their
+    slabs are read by the later flush launch)."""
 
     def __init__(self, device):
         self.device = device
+        self.hold = []
 
     def __call__(self, numel, dtype=torch.float32):
-        return torch.empty(int(numel), dtype=dtype, device=self.device)
+        t = torch.empty(int(numel), dtype=dtype, device=self.device)
+        if _DEFER[0]:
+            self.hold.append(t)
+        return t
+
+
+_DEFER = [False]
+
+
+class defer_reductions:
+    """Queue the parameter-gradient slab sums issued inside the block (tm_reduce_defer); they
+    run as ONE launch at the next ``flush_reductions()``."""
+
+    def __enter__(self):
+        _lib.call("tm_reduce_defer", 1)
+        _DEFER[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _lib.call("tm_reduce_defer", 0)
+        _DEFER[0] = False
+        return False
+
+
+def flush_reductions():
+    _lib.call("tm_reduce_flush", _stream())
 
 
 # ----------------------------------------------------------------------------- NystromAttention core
@@ -267,8 +295,8 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     dk = pool(nbh * n * DH)
     dv = pool(nbh * n * DH)
     d1 = pool(nbh * n)
-    work = pool(_lib.query("tm_nys_conv_bwd_workspace", geo.B, nh, n) // 4)
-    with probe("conv_bwd"):
+    with defer_reductions(), probe("conv_bwd"):
+        work = pool(_lib.query("tm_nys_conv_bwd_workspace", geo.B, nh, n) // 4)
         _lib.call("tm_nys_conv_bwd", dt_code, _p(dmerged), _p(merged), _p(v), _p(wconv), nbh, nh, n, _p(dv),
                   _p(d1), _p(work), _p(dwconv_out), st)
     # A1 product backward: dq (complete), dkl, dY
@@ -350,23 +378,26 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
     _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
               C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(dout), st)
     # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
-    weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code, work_pool=pool)
-    colsum(dout, B * n, D, D, dt_code, grads["bo"], pool)
+    with defer_reductions():
+        weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code, work_pool=pool)
+        colsum(dout, B * n, D, D, dt_code, grads["bo"], pool)
     dmerged = pool(B * n * D, tdtype).view(B, n, D)
     gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     dqkv = nystrom_core_backward(dmerged, saved["merged"], saved["qkv"], saved["core"], geo, prm["wconv"],
                                  tdtype, dt_code, pool, grads["wconv"], DH ** -0.5)
     # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
-    weight_grad(dqkv, saved["xn"], grads["wqkv"], 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
-                work_pool=pool)
+    with defer_reductions():
+        weight_grad(dqkv, saved["xn"], grads["wqkv"], 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
+                    work_pool=pool)
     dxn = pool(B * n * D, tdtype).view(B, n, D)
     gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     # LayerNorm backward, accumulated into dH (residual branch already there)
     rpb = 32
-    work = pool(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4)
-    _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
-              _p(saved["rstd"]), B * S, D, S, n, pad, rpb, _p(dH), _p(work), _p(grads["norm_w"]),
-              _p(grads["norm_b"]), st)
+    with defer_reductions():
+        work = pool(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4)
+        _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
+                  _p(saved["rstd"]), B * S, D, S, n, pad, rpb, _p(dH), _p(work), _p(grads["norm_w"]),
+                  _p(grads["norm_b"]), st)
 
 
 # ----------------------------------------------------------------------------- whole model
@@ -562,6 +593,7 @@ class TransMILEngine:
                           _p(g["pos_layer.proj1.weight"]), _p(g["pos_layer.proj1.bias"]),
                           _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), st)
                 dH = dH1
+                flush_reductions()     # head, norm, layer2 and PPEG parameter gradients final
                 if ready is not None:
                     ready(0)
         if self.fc1["main"] is None:
@@ -572,6 +604,7 @@ class TransMILEngine:
                 dx[:, :geo.add] += dHv[:, N + 1:]
             torch.sum(dHv[:, 0], dim=0, out=g["cls_token"].view(D))
             g["__dx__"] = dx
+            flush_reductions()
             if ready is not None:
                 ready(1)
             return g
@@ -581,9 +614,10 @@ class TransMILEngine:
                   _p(g["cls_token"]), st)
         main, inner = self.fc1["main"], ctx["inner"]
         Fx = F if inner is None else prm["w0"].shape[0]
-        weight_grad(dpre, ctx["xt"], g[main + ".weight"], D, Fx, B * N, ldy=D, ldx=Fx, dtype=self.dt_code,
-                    work_pool=pool)
-        colsum(dpre, B * N, D, D, self.dt_code, g[main + ".bias"], pool)
+        with defer_reductions():
+            weight_grad(dpre, ctx["xt"], g[main + ".weight"], D, Fx, B * N, ldy=D, ldx=Fx, dtype=self.dt_code,
+                        work_pool=pool)
+            colsum(dpre, B * N, D, D, self.dt_code, g[main + ".bias"], pool)
         if inner is not None:
             # d LN-out = dpre W1 ; LayerNorm backward ; GELU backward ; W0 / b0 gradients
             w0n, lnn = self.fc1["inner"]
@@ -601,6 +635,7 @@ class TransMILEngine:
             weight_grad(dpre0, inner["xt"], g[w0n + ".weight"], Fm, Fin, B * N, ldy=Fm, ldx=Fin, dtype=self.dt_code,
                         work_pool=pool)
             colsum(dpre0, B * N, Fm, Fm, self.dt_code, g[w0n + ".bias"], pool)
+        flush_reductions()
         if ready is not None:
             ready(1)
         return g
@@ -669,4 +704,5 @@ class NystromEngine:
         dx = torch.empty(B, S, D, dtype=torch.float32, device=dout.device)
         gemm(dqkv, ctx["wqkv_t"], dx, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=self.dt_code,
              c_dtype=F32, rowmap=(n, pad, S, 0, 0, 0))
+        flush_reductions()      # the res_conv weight gradient queued by nystrom_core_backward
         return dx, dwqkv, dwo, dbo, dwconv

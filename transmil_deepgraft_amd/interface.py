@@ -383,6 +383,36 @@ class GradAllReduce:
         self.flat.mul_(1.0 / self._world())
 
 
+class _CrossEntropyOneHot(torch.autograd.Function):
+    """CE(logits, one_hot(label).float()) + softmax + argmax as one HIP launch (tm_ce_fwd) and its
+    backward as one (tm_ce_bwd), instead of ~17 small PyTorch kernels per step."""
+
+    @staticmethod
+    def forward(ctx, logits, label, stats):
+        from . import _lib
+        from .engine import _p, _stream
+        B, C = logits.shape
+        lg = logits.float().contiguous()
+        lab = label.to(torch.int64).contiguous()
+        loss = torch.empty((), device=logits.device)
+        prob = torch.empty(B, C, device=logits.device)
+        yhat = torch.empty(B, dtype=torch.int64, device=logits.device)
+        _lib.call("tm_ce_fwd", _p(lg), _p(lab), B, C, _p(loss), _p(prob), _p(yhat), _p(stats), _stream())
+        ctx.save_for_backward(prob, lab)
+        ctx.mark_non_differentiable(prob, yhat)
+        return loss, prob, yhat
+
+    @staticmethod
+    def backward(ctx, gloss, _gprob, _gyhat):
+        from . import _lib
+        from .engine import _p, _stream
+        prob, lab = ctx.saved_tensors
+        B, C = prob.shape
+        dl = torch.empty(B, C, device=prob.device)
+        _lib.call("tm_ce_bwd", _p(prob), _p(lab), B, C, _p(gloss.float().contiguous()), _p(dl), _stream())
+        return dl, None, None
+
+
 class TransMILTask(nn.Module):
     """``ModelInterface`` training-step subset for the feature-bag path."""
 
@@ -392,6 +422,7 @@ class TransMILTask(nn.Module):
         if accumulate_grad_batches < 1:
             raise ValueError("accumulate_grad_batches >= 1")
         self.model = model
+        self.class_stats = None     # int32 [C][2] per-class count / correct (model_interface.py:350-356)
         self.accumulate_grad_batches = accumulate_grad_batches
         self._micro = 0
         self.n_classes = model.n_classes
@@ -410,9 +441,17 @@ class TransMILTask(nn.Module):
 
     def training_step(self, batch):
         bags, label, _ = batch
-        logits, y_prob, y_hat = self.step(bags)
-        one_hot = F.one_hot(label, num_classes=self.n_classes).float()
-        loss = self.loss(logits, one_hot)
+        if bags.is_cuda and isinstance(self.loss, nn.CrossEntropyLoss):
+            # fused: loss, Y_prob, Y_hat and the per-class count/correct of :350-356 in one launch
+            logits = self(bags.float().contiguous())
+            if self.class_stats is None or self.class_stats.device != logits.device:
+                self.class_stats = torch.zeros(self.n_classes, 2, dtype=torch.int32, device=logits.device)
+            loss, y_prob, y_hat = _CrossEntropyOneHot.apply(logits, label, self.class_stats)
+        else:
+            logits, y_prob, y_hat = self.step(bags)
+            one_hot = F.one_hot(label, num_classes=self.n_classes).float()
+            loss = self.loss(logits, one_hot)
+        self._last_outputs = (y_prob, y_hat)
         if loss.ndim == 0:
             loss = loss.unsqueeze(0)
         # the reference logs loss.item() with sync_dist every step (model_interface.py:364),
