@@ -149,6 +149,10 @@ typedef struct tm_bmm_job {
   /* optional second output of the same product (C's layout): C2 = c2_alpha*(products)
    * + c2_diag*I + c2_e1*E1 (null: none) */
   float* C2; float c2_alpha, c2_diag, c2_e1;
+  /* optional bf16 form of C (C's layout, written beside it): ct_mode 1 = bf16(C) at Ct,
+   * 2 = split planes hi = bf16(C) at Ct and lo = bf16(C - hi) at Ct + ct_plane elements
+   * (the operand format of tm_pinv_bwd_split), 0 = none */
+  void* Ct; long long ct_plane; int ct_mode; int ct_reserved;
 } tm_bmm_job;
 /* prec 0: exact fp32 MFMA; prec 1: bf16x3 (hi/lo split, ~16-bit operands, fp32 accumulate) */
 int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream);
@@ -243,6 +247,14 @@ typedef struct tm_cast_table {
   long long offset[TM_CAST_MAX + 1];
 } tm_cast_table;
 int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* stream);
+/* One launch per forward: the cast table (as tm_cast_f32_many, 0..8 tensors), the PPEG fold
+ * (as tm_ppeg_fold; skipped when w7 is NULL), when counter is non-NULL counter[0] += 1 with the
+ * new value written to seed_out[0] (the dropout stream of a captured step), and when cls is
+ * non-NULL the class-token rows H[b*S][0..D) = cls (as tm_put_cls). */
+int tm_step_prepare(int dtype, const tm_cast_table* table, const float* w7, const float* b7,
+                    const float* w5, const float* b5, const float* w3, const float* b3, int D,
+                    float* wfold, float* bfold, long long* counter, long long* seed_out,
+                    const float* cls, float* H, int B, int S, void* stream);
 
 /* ---- optimizer step (optim.hip) ----------------------------------------
  * torch.optim.RAdam (L2 decay, code/MyOptimizer/optim_factory.py:77-79) + the

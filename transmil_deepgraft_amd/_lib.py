@@ -38,7 +38,8 @@ class BmmJob(C.Structure):
                 ("A2", P), ("B2", P), ("ta2", I), ("tb2", I), ("lda2", I), ("ldb2", I), ("sa2", L), ("sb2", L),
                 ("E1", P), ("e1", Fl), ("E2", P), ("e2", Fl), ("alpha", Fl), ("diag", Fl),
                 ("C", P), ("ldc", I), ("sc", L), ("M", I), ("N", I), ("K", I),
-                ("C2", P), ("c2_alpha", Fl), ("c2_diag", Fl), ("c2_e1", Fl)]
+                ("C2", P), ("c2_alpha", Fl), ("c2_diag", Fl), ("c2_e1", Fl),
+                ("Ct", P), ("ct_plane", L), ("ct_mode", I), ("ct_reserved", I)]
 
 
 OPTIM_MAX_TENSORS = 40
@@ -113,6 +114,7 @@ _SIGS = {
     "tm_attmil_bwd_workspace": (L, [I, I, I]),
     "tm_attmil_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P, P]),
     "tm_put_cls": (I, [P, I, I, I, P, P]),
+    "tm_step_prepare": (I, [I, C.POINTER(CastTable), P, P, P, P, P, P, I, P, P, P, P, P, P, I, I, P]),
     "tm_reduce_defer": (I, [I]),
     "tm_reduce_flush": (I, [P]),
     "tm_ce_fwd": (I, [P, P, I, I, P, P, P, P, P]),

@@ -20,6 +20,56 @@ __global__ void cast_many_kernel(tm_cast_table tab) {
   for (int e = 0; e < 4 && j + e < n; ++e) dst[j + e] = from_f<T>(src[j + e]);
 }
 
+// The per-step preparation of the fused forward as ONE launch: blocks [0, cast_blocks) convert
+// the cast table (GEMM weights + the bag to T), the next ceil(D/256) blocks fold PPEG's
+// 7x7 + 5x5 + 3x3 + identity into one 7x7 kernel (code/models/TransMIL.py:72), and the last
+// block advances the dropout counter and writes this forward's seed snapshot.
+template <typename T>
+__global__ void __launch_bounds__(256) step_prepare_kernel(tm_cast_table tab, long long cast_blocks,
+                                                           const float* __restrict__ w7, const float* __restrict__ b7,
+                                                           const float* __restrict__ w5, const float* __restrict__ b5,
+                                                           const float* __restrict__ w3, const float* __restrict__ b3,
+                                                           int D, float* __restrict__ wf, float* __restrict__ bf,
+                                                           long long* __restrict__ counter,
+                                                           long long* __restrict__ seed_out,
+                                                           const float* __restrict__ cls, float* __restrict__ H,
+                                                           int B, int S) {
+  if (blockIdx.x < cast_blocks) {
+    const long long i4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i4 >= tab.offset[tab.count]) return;
+    int t = 0;
+    while (i4 >= tab.offset[t + 1]) ++t;
+    const long long j = i4 - tab.offset[t], n = tab.offset[t + 1] - tab.offset[t];
+    const float* src = tab.src[t];
+    T* dst = (T*)tab.dst[t];
+    for (int e = 0; e < 4 && j + e < n; ++e) dst[j + e] = from_f<T>(src[j + e]);
+    return;
+  }
+  const long long fb = blockIdx.x - cast_blocks;
+  const int nfold = w7 ? (D + 255) / 256 : 0;
+  if (fb < nfold) {
+    const int ch = (int)fb * 256 + threadIdx.x;
+    if (ch >= D) return;
+    for (int dy = 0; dy < 7; ++dy)
+      for (int dx = 0; dx < 7; ++dx) {
+        float v = w7[(size_t)ch * 49 + dy * 7 + dx];
+        if (dy >= 1 && dy <= 5 && dx >= 1 && dx <= 5) v += w5[(size_t)ch * 25 + (dy - 1) * 5 + (dx - 1)];
+        if (dy >= 2 && dy <= 4 && dx >= 2 && dx <= 4) v += w3[(size_t)ch * 9 + (dy - 2) * 3 + (dx - 2)];
+        if (dy == 3 && dx == 3) v += 1.0f;
+        wf[(size_t)ch * 49 + dy * 7 + dx] = v;
+      }
+    bf[ch] = b7[ch] + b5[ch] + b3[ch];
+    return;
+  }
+  if (threadIdx.x == 0 && counter) {
+    const long long c = counter[0] + 1;
+    counter[0] = c;
+    seed_out[0] = c;
+  }
+  if (cls)   // the class-token rows H[b*S + 0][:] (code/models/TransMIL.py:184-186)
+    for (int i = threadIdx.x; i < B * D; i += blockDim.x) H[(size_t)(i / D) * S * D + i % D] = cls[i % D];
+}
+
 // H[b*S + 0][:] = cls[:]; grid (B), block 256
 __global__ void put_cls_kernel(const float* __restrict__ cls, int S, int D, float* __restrict__ H) {
   for (int c = threadIdx.x; c < D; c += blockDim.x) H[(size_t)blockIdx.x * S * D + c] = cls[c];
@@ -212,6 +262,29 @@ extern "C" int tm_gelu_bwd(int dtype, const float* dy, const float* pre, long lo
   const unsigned blocks = (unsigned)(((count + 3) / 4 + 255) / 256);
   hipStream_t st = (hipStream_t)stream;
   TM_DTYPE_DISPATCH(dtype, (gelu_bwd_kernel<T><<<blocks, 256, 0, st>>>(dy, pre, (size_t)count, (T*)dpre)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_step_prepare(int dtype, const tm_cast_table* table, const float* w7, const float* b7,
+                               const float* w5, const float* b5, const float* w3, const float* b3, int D,
+                               float* wfold, float* bfold, long long* counter, long long* seed_out,
+                               const float* cls, float* H, int B, int S, void* stream) {
+  TM_REQUIRE(table && table->count >= 0 && table->count <= TM_CAST_MAX, "step_prepare: 0..8 tensors");
+  TM_REQUIRE(!cls || (H && B >= 1 && S >= 1), "step_prepare: class-token rows need H, B, S");
+  TM_REQUIRE(!counter || seed_out, "step_prepare: the counter needs a seed output");
+  long long off = 0;
+  for (int i = 0; i < table->count; ++i) {
+    TM_REQUIRE(table->src[i] && table->dst[i], "step_prepare: null tensor");
+    TM_REQUIRE(table->offset[i] == off && table->offset[i + 1] >= off && table->offset[i + 1] % 4 == 0,
+               "step_prepare: offsets must be a prefix sum of multiples of 4");
+    off = table->offset[i + 1];
+  }
+  const long long cast_blocks = ((off + 3) / 4 + 255) / 256;
+  const long long blocks = cast_blocks + (w7 ? (D + 255) / 256 : 0) + 1;
+  TM_DTYPE_DISPATCH(dtype, (step_prepare_kernel<T><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
+                               *table, cast_blocks, w7, b7, w5, b5, w3, b3, D, wfold, bfold, counter, seed_out,
+                               cls, H, B, S)));
   TM_CHECK_LAUNCH();
   return 0;
 }

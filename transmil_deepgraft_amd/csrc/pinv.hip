@@ -32,6 +32,15 @@ constexpr int NL = 256;
 
 struct JobPair { tm_bmm_job j[2]; int tiles0; };
 
+// the bf16 form of an output element (tm_bmm_job.ct_mode): a copy, or split hi / lo planes
+TM_DEV void store_ct(const tm_bmm_job& J, size_t off, float v) {
+  if (J.ct_mode == 0) return;
+  bf16* t = (bf16*)J.Ct;
+  const bf16 hi = (bf16)v;
+  t[off] = hi;
+  if (J.ct_mode == 2) t[off + J.ct_plane] = (bf16)(v - (float)hi);
+}
+
 
 
 TM_DEV f32x8 frag_a(const float* A, int ta, int lda, int m, int k) {
@@ -131,6 +140,7 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
     if (J.E2) v += J.e2 * J.E2[off];
     J.C[off] = v;
     if (J.C2) J.C2[off] = J.c2_alpha * s + (row == col ? J.c2_diag : 0.f) + J.c2_e1 * e1v;
+    store_ct(J, off, v);
   }
 }
 
@@ -318,6 +328,7 @@ TM_DEV void bmm_tile(const tm_bmm_job& J, int bh, int tile, float (*red)[16][64]
     v += J.e1 * ev1[q] + J.e2 * ev2[q];
     J.C[off[q]] = v;
     if (J.C2) J.C2[off[q]] = J.c2_alpha * sum + (row[q] == col[q] ? J.c2_diag : 0.f) + J.c2_e1 * ev1[q];
+    store_ct(J, off[q], v);
   }
 }
 

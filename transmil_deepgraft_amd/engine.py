@@ -171,7 +171,8 @@ def colsum(X, rows, cols, ld, dtype, out, work_pool, accumulate=False):
     _lib.call("tm_colsum", _p(X), dtype, rows, cols, ld, rpc, _p(work), _p(out), int(accumulate), _stream())
 
 
-def bmm_job(A, ta, B, tb, Cout, M, N, K, alpha=1.0, diag=0.0, E1=None, e1=0.0, E2=None, e2=0.0):
+def bmm_job(A, ta, B, tb, Cout, M, N, K, alpha=1.0, diag=0.0, E1=None, e1=0.0, E2=None, e2=0.0, Ct=None,
+            ct_mode=0, ct_plane=0):
     j = BmmJob()
     j.A, j.B = A.data_ptr(), B.data_ptr()
     j.ta, j.tb = ta, tb
@@ -187,6 +188,8 @@ def bmm_job(A, ta, B, tb, Cout, M, N, K, alpha=1.0, diag=0.0, E1=None, e1=0.0, E
     j.C = Cout.data_ptr()
     j.ldc, j.sc = N, M * N
     j.M, j.N, j.K = M, N, K
+    j.Ct = Ct.data_ptr() if Ct is not None else None
+    j.ct_mode, j.ct_plane = (ct_mode, ct_plane) if Ct is not None else (0, 0)
     return j
 
 
@@ -269,9 +272,12 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
         _lib.call("tm_pinv_fwd", _p(a2), nbh, PINV_ITERS, prec, _p(saved), st)
         z = saved[PINV_ITERS * nbh * NL * NL:(PINV_ITERS + 1) * nbh * NL * NL].view(nbh, NL, NL)
     y = pool(nbh * NL * DH).view(nbh, NL, DH)
-    bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh, prec)
-    y_t = pool(nbh * NL * DH, tdtype)
-    _lib.call("tm_cast_f32", dt_code, _p(y), _p(y_t), nbh * NL * DH, st)
+    if dt_code == BF16:     # Y and its bf16 operand copy from the same launch
+        y_t = pool(nbh * NL * DH, tdtype)
+        bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL, Ct=y_t, ct_mode=1)], nbh, prec)
+    else:
+        bmm([bmm_job(z, 0, w, 0, y, NL, DH, NL)], nbh, prec)
+        y_t = y
     merged = pool(geo.B * n * nh * DH, tdtype).view(geo.B, n, nh * DH)
     lse1 = pool(nbh * n)
     with probe("a1_fwd"):
@@ -306,13 +312,21 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     dy = pool(nbh * NL * DH).view(nbh, NL, DH)
     work = pool(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, qpw) // 4)
     with probe("a1_bwd"):
-        _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t), _p(state["lse1"]),
-                  _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, st)
+        with defer_reductions():     # its dk~ and dY slab sums as one launch
+            _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t),
+                      _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, st)
+        flush_reductions()
     # Y = Z W
     dz = pool(mat).view(nbh, NL, NL)
     dw = pool(nbh * NL * DH).view(nbh, NL, DH)
-    bmm([bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH),
-         bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh, prec)
+    pwork = None
+    if state["a2s"] is not None:
+        # the split bf16 hi / lo planes of dZ (work[0] of tm_pinv_bwd_split) from the same launch
+        pwork = pool(_lib.query("tm_pinv_bwd_split_workspace_floats", nbh))
+        dz_job = bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH, Ct=pwork, ct_mode=2, ct_plane=mat)
+    else:
+        dz_job = bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH)
+    bmm([dz_job, bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh, prec)
     # A3 product backward: dk (=), dv (+=), dql3 (=)
     d3 = pool(nbh * NL)
     dw_t = pool(nbh * NL * DH, tdtype)
@@ -326,8 +340,6 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     ds2 = pool(mat).view(nbh, NL, NL)
     if state["a2s"] is not None:
         # split operands; the softmax backward is fused into the chain's last launch
-        pwork = pool(_lib.query("tm_pinv_bwd_split_workspace_floats", nbh))
-        _lib.call("tm_split_f32", _p(dz), _p(pwork), mat, st)
         with probe("pinv_bwd"):
             _lib.call("tm_pinv_bwd_split", _p(state["a2"]), _p(state["a2s"]), nbh, PINV_ITERS, _p(state["pinv"]),
                       _p(pwork), 1, _p(ds2), st)
@@ -452,8 +464,11 @@ class TransMILEngine:
         _lib.call("tm_cast_f32_many", self.dt_code, C.byref(tab), _stream())
         return outs
 
-    def prepare(self, params, pool):
-        """fp32 master parameters -> the per-call operand set (T copies of GEMM weights)."""
+    def prepare(self, params, pool, x2d=None, counter=None, seed_out=None, cls_rows=None):
+        """fp32 master parameters -> the per-call operand set (T copies of the GEMM weights and,
+        when given, of the bag ``x2d``), the folded PPEG kernel, and the dropout counter
+        advanced into ``seed_out`` and (``cls_rows = (H, B, S)``) the class-token rows -- all in ONE
+        launch (tm_step_prepare)."""
         D = params["norm.weight"].shape[0]
         p = {"D": D}
         main, inner = self.fc1["main"], self.fc1["inner"]
@@ -463,13 +478,27 @@ class TransMILEngine:
             ws.append(params[main + ".weight"])
         if inner is not None:
             ws.append(params[inner[0] + ".weight"])
-        ws = self._cast_many(ws, pool)
-        wqkv1, wo1, wqkv2, wo2 = ws[:4]
+        tab = _lib.CastTable()
+        if self.dt_code == F32:
+            outs = [w.contiguous() for w in ws]
+            p["xt"] = None if x2d is None else x2d.contiguous()
+        else:
+            srcs = [w.contiguous() for w in ws] + ([x2d.contiguous()] if x2d is not None else [])
+            outs, off = [], 0
+            for i, w in enumerate(srcs):
+                o = pool(w.numel(), self.tdtype).view(w.shape)
+                tab.src[i], tab.dst[i], tab.offset[i] = w.data_ptr(), o.data_ptr(), off
+                off += w.numel()
+                outs.append(o)
+            tab.count = len(srcs)
+            tab.offset[len(srcs)] = off
+            p["xt"] = outs.pop() if x2d is not None else None
+        wqkv1, wo1, wqkv2, wo2 = outs[:4]
         if main is not None:
-            p["w1"] = ws[4]
+            p["w1"] = outs[4]
             p["b1"] = params[main + ".bias"]
         if inner is not None:
-            p["w0"], p["b0"] = ws[5], params[inner[0] + ".bias"]   # inner implies main
+            p["w0"], p["b0"] = outs[5], params[inner[0] + ".bias"]   # inner implies main
             p["ln0_w"], p["ln0_b"] = params[inner[1] + ".weight"], params[inner[1] + ".bias"]
         p["cls"] = params["cls_token"]
         for li, (wqkv, wo) in ((1, (wqkv1, wo1)), (2, (wqkv2, wo2))):
@@ -483,21 +512,24 @@ class TransMILEngine:
             }
         wfold = pool(D * 49)
         bfold = pool(D)
-        _lib.call("tm_ppeg_fold", _p(params["pos_layer.proj.weight"]), _p(params["pos_layer.proj.bias"]),
-                  _p(params["pos_layer.proj1.weight"]), _p(params["pos_layer.proj1.bias"]),
-                  _p(params["pos_layer.proj2.weight"]), _p(params["pos_layer.proj2.bias"]), D, _p(wfold),
-                  _p(bfold), _stream())
+        _lib.call("tm_step_prepare", self.dt_code, C.byref(tab), _p(params["pos_layer.proj.weight"]),
+                  _p(params["pos_layer.proj.bias"]), _p(params["pos_layer.proj1.weight"]),
+                  _p(params["pos_layer.proj1.bias"]), _p(params["pos_layer.proj2.weight"]),
+                  _p(params["pos_layer.proj2.bias"]), D, _p(wfold), _p(bfold), _p(counter), _p(seed_out),
+                  _p(params["cls_token"] if cls_rows else None), _p(cls_rows[0] if cls_rows else None),
+                  cls_rows[1] if cls_rows else 0, cls_rows[2] if cls_rows else 0, _stream())
         p["wfold"], p["bfold"] = wfold, bfold
         p["norm_w"], p["norm_b"] = params["norm.weight"], params["norm.bias"]
         p["fc_w"], p["fc_b"] = params[self.head + ".weight"], params[self.head + ".bias"]
         return p
 
-    def forward(self, x, params, drop_p=0.0, seeds=(0x1F123BB5, 0x2A9F4C61), seed_dev=None):
+    def forward(self, x, params, drop_p=0.0, seeds=(0x1F123BB5, 0x2A9F4C61), seed_dev=None, counter=None):
         """x [B, N, F] fp32 (on the GPU) -> logits [B, C] fp32 and the saved context.
 
         Dropout (train mode) hashes (row, col) with a per-layer seed; with ``seed_dev``
         (a 1-element int64 device tensor) the seed is read on the device, so a
-        captured hipGraph draws a fresh mask every replay."""
+        captured hipGraph draws a fresh mask every replay; with ``counter`` as well, the
+        preparation launch first advances the counter and writes it into ``seed_dev``."""
         dev = x.device
         pool = Pool(dev)
         B, N, F = x.shape
@@ -506,14 +538,12 @@ class TransMILEngine:
         if D != heads * DH:
             raise NotImplementedError(f"HIP NystromAttention needs dim_head == 64 (D={D}, heads={heads})")
         geo = Geometry(B, N, F, D, heads)
-        prm = self.prepare(params, pool)
+        H0 = pool(B * geo.S * D).view(B * geo.S, D)
+        prm = self.prepare(params, pool, None if self.fc1["main"] is None else x.reshape(B * N, F),
+                           counter=counter if seed_dev is not None else None, seed_out=seed_dev,
+                           cls_rows=(H0, B, geo.S))
         st = _stream()
-        if self.fc1["main"] is None:
-            xt = None
-        elif self.dt_code == BF16:
-            xt = self._cast(x.reshape(B * N, F), pool)
-        else:
-            xt = x.reshape(B * N, F).contiguous()
+        xt = prm["xt"]
         inner = None
         if self.fc1["inner"] is not None:
             # inner stage: y0 = GELU(x W0^T + b0) (fp32, pre-activation kept), then LayerNorm -> T,
@@ -529,8 +559,8 @@ class TransMILEngine:
                       N, N, 0, self.dt_code, _p(xln), _p(mean0), _p(rstd0), st)
             inner = dict(xt=xt, y0=y0, pre0=pre0, mean0=mean0, rstd0=rstd0, F=F)
             xt, F = xln, Fm
-        # _fc1: Linear + GELU, grid pad (duplicate the first `add` rows) and class token
-        H0 = pool(B * geo.S * D).view(B * geo.S, D)
+        # _fc1: Linear + GELU, grid pad (duplicate the first `add` rows); the class-token rows
+        # were written by the preparation launch
         if self.fc1["main"] is None:
             if F != D:
                 raise ValueError(f"pre-embedded input must be [B, N, {D}], got F={F}")
@@ -543,7 +573,6 @@ class TransMILEngine:
             pre = pool(B * N * D).view(B * N, D)   # fp32 pre-activation for the GELU backward
             gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
                  bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
-        _lib.call("tm_put_cls", _p(prm["cls"]), B, geo.S, D, _p(H0), st)
         H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0], seed_dev)
         H2 = pool(B * geo.S * D).view(B * geo.S, D)
         _lib.call("tm_ppeg_fwd", _p(H1), B, geo.G, D, _p(prm["wfold"]), _p(prm["bfold"]), _p(H2), st)

@@ -66,10 +66,10 @@ class PPEG(nn.Module):
 
 class _TransMILFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, engine, names, drop_p, seed_dev, holder, bucket, x, *params):
+    def forward(ctx, engine, names, drop_p, seed_dev, holder, bucket, counter, x, *params):
         prm = dict(zip(names, params))
         with torch.cuda.device(x.device):   # kernels go to x's device and its current stream
-            logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev)
+            logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev, counter=counter)
         ctx.engine, ctx.c, ctx.names, ctx.prm, ctx.bucket = engine, c, names, prm, bucket
         if holder is not None:
             holder["ctx"] = c
@@ -81,7 +81,7 @@ class _TransMILFn(torch.autograd.Function):
             raise RuntimeError("TransMIL (fused HIP path): the saved activations were freed by the first "
                                "backward; retain_graph=True is not supported on the fused path -- set "
                                "model.fused = False (module-by-module path) to backpropagate twice")
-        head = (None,) * 7
+        head = (None,) * 8
         bucket, prm = ctx.bucket, ctx.prm
         dl = dlogits.float().contiguous()
         with torch.cuda.device(dlogits.device):
@@ -94,7 +94,7 @@ class _TransMILFn(torch.autograd.Function):
                 with torch.no_grad():
                     for n, p in prm.items():
                         p.grad = views[n]
-                return head[:6] + (dx,) + (None,) * len(ctx.names)
+                return head[:7] + (dx,) + (None,) * len(ctx.names)
             g = ctx.engine.backward(dl, ctx.c, prm)
             dx = g.pop("__dx__", None)
             ctx.c = None
@@ -104,8 +104,8 @@ class _TransMILFn(torch.autograd.Function):
                     torch._foreach_add_([p.grad for p in prm.values()], [g[n] for n in ctx.names])
                 bucket.ready(0)
                 bucket.ready(1)
-                return head[:6] + (dx,) + (None,) * len(ctx.names)
-        return head[:6] + (dx,) + tuple(g[n] for n in ctx.names)
+                return head[:7] + (dx,) + (None,) * len(ctx.names)
+        return head[:7] + (dx,) + tuple(g[n] for n in ctx.names)
 
 
 class TransMIL(nn.Module):
@@ -254,11 +254,13 @@ class TransMIL(nn.Module):
         drop_p = self.layer1.attn.to_out[1].p if self.training else 0.0
         seed_dev = None
         if drop_p > 0:
-            self._dropout_counter.add_(1)
-            seed_dev = self._dropout_counter.clone()   # snapshot for this forward's backward
+            # this forward's seed: the engine's preparation launch advances the device counter and
+            # writes the new value here (the snapshot its backward replays)
+            seed_dev = torch.empty(1, dtype=torch.int64, device=x.device)
         holder = {} if return_attn else None
         engine = TransMILEngine(self.compute_dtype, fc1=layout, head=self._head)
-        logits = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, self._grad_bucket, x, *params)
+        logits = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, self._grad_bucket,
+                                   self._dropout_counter if drop_p > 0 else None, x, *params)
         if return_attn:
             c = holder["ctx"]
             S = c["geo"].S
