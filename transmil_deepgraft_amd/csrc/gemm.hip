@@ -647,34 +647,52 @@ struct ReduceEntry {
   int splits;
   int accumulate;
   float alpha;
+  int vec;   // 1: 16-B units (count % 4 == 0, both pointers 16-B aligned)
 };
 struct ReduceTable {
   ReduceEntry e[DEFER_MAX];
-  long long off[DEFER_MAX + 1];   // prefix sums of count
+  long long off[DEFER_MAX + 1];   // prefix sums of the entries' thread counts
   int n;
 };
 static ReduceTable g_defer{};
 static int g_defer_on = 0;
 
+// one thread = one 16-B unit (4 floats; entries whose count is not a multiple of 4 go element by
+// element), the splits summed in index order with 12 loads in flight per thread
 __global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= t.off[t.n]) return;
   int e = 0;
   while (i >= t.off[e + 1]) ++e;
   const ReduceEntry r = t.e[e];
-  const long long j = i - t.off[e];
-  constexpr int U = 8;
+  const long long u = i - t.off[e];
+  constexpr int U = 12;
+  if (r.vec) {
+    const size_t j = (size_t)u * 4;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int z0 = 0; z0 < r.splits; z0 += U) {
+      f32x4 v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = *(const f32x4*)(r.slab + (size_t)min(z0 + k, r.splits - 1) * r.count + j);
+#pragma unroll
+      for (int k = 0; k < U; ++k) s += (z0 + k < r.splits) ? v[k] : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    s *= r.alpha;
+    if (r.accumulate) s += *(const f32x4*)(r.out + j);
+    *(f32x4*)(r.out + j) = s;
+    return;
+  }
   float s = 0.f;
   for (int z0 = 0; z0 < r.splits; z0 += U) {
     float v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = r.slab[(size_t)min(z0 + u, r.splits - 1) * r.count + j];
+    for (int k = 0; k < U; ++k) v[k] = r.slab[(size_t)min(z0 + k, r.splits - 1) * r.count + u];
 #pragma unroll
-    for (int u = 0; u < U; ++u) s += (z0 + u < r.splits) ? v[u] : 0.f;
+    for (int k = 0; k < U; ++k) s += (z0 + k < r.splits) ? v[k] : 0.f;
   }
   s *= r.alpha;
-  if (r.accumulate) s += r.out[j];
-  r.out[j] = s;
+  if (r.accumulate) s += r.out[u];
+  r.out[u] = s;
 }
 
 extern "C" int tm_reduce_defer(int on) {
@@ -699,8 +717,10 @@ extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long 
   if (g_defer_on) {
     if (g_defer.n == DEFER_MAX)
       if (int rc = tm_reduce_flush(stream)) return rc;
-    g_defer.e[g_defer.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha};
-    g_defer.off[g_defer.n + 1] = g_defer.off[g_defer.n] + count;
+    const int vec = count % 4 == 0 && ((uintptr_t)slab % 16) == 0 && ((uintptr_t)out % 16) == 0;
+    g_defer.e[g_defer.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha, vec};
+    // offsets count threads: one per 16-B unit when the entry allows it
+    g_defer.off[g_defer.n + 1] = g_defer.off[g_defer.n] + (vec ? count / 4 : count);
     ++g_defer.n;
     return 0;
   }

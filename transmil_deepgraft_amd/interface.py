@@ -277,7 +277,7 @@ class GradBucket:
             start = off
             for p in part:
                 self._off[id(p)] = (off, p.numel())
-                off += p.numel()
+                off += (p.numel() + 15) // 16 * 16     # every view 64-B aligned (vector stores)
             self.ranges.append((start, off))
         self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
         self.hooks = []
