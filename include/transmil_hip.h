@@ -260,8 +260,9 @@ int tm_step_prepare(int dtype, const tm_cast_table* table, const float* w7, cons
  * torch.optim.RAdam (L2 decay, code/MyOptimizer/optim_factory.py:77-79) + the
  * Lookahead sync (code/MyOptimizer/lookahead.py, wrapped at optim_factory.py:118-121)
  * over up to 40 parameter tensors in one launch.  exp_avg / exp_avg_sq / slow are
- * flat fp32 buffers indexed by the table's prefix offsets; counters (int32[2], device)
- * hold the RAdam and Lookahead step counts and are advanced by the call itself.
+ * flat 16-B aligned fp32 buffers indexed by the table's offsets (prefix sums of numel, each
+ * rounded up to a multiple of 4); counters (int32[3], device, zero-initialised) hold the
+ * RAdam and Lookahead step counts (advanced by the call itself) and a scratch count.
  * lookahead_k == 0 disables the sync (plain RAdam). */
 #define TM_OPTIM_MAX_TENSORS 40
 typedef struct tm_optim_tensor {

@@ -22,9 +22,10 @@ def _rel(a, b):
 
 
 # ----------------------------------------------------------------------------- GEMM
-@pytest.fixture(params=[0, 1, 2], ids=["1buf", "2buf", "ring"])
+@pytest.fixture(params=[0, 1, 2, 4], ids=["1buf", "2buf", "ring", "persist"])
 def gemm_variant(request):
-    """Every GEMM main loop (register-staged 1 / 2 LDS buffers, global_load_lds ring)."""
+    """Every GEMM main loop (register-staged 1 / 2 LDS buffers, per-tile global_load_lds ring,
+    persistent ring)."""
     from transmil_deepgraft_amd import _lib
     _lib.lib().tm_debug_set_variant(2, request.param)
     yield request.param
@@ -50,6 +51,36 @@ def test_gemm_layouts(dtype, a_trans, b_kn, K, gemm_variant):
     gemm(As, Bs, out, M, N, K, lda=M if a_trans else K, ldb=N if b_kn else K, ldc=N, a_trans=a_trans,
          b_kn=b_kn, dtype=code, c_dtype=F32)
     torch.cuda.synchronize()
+    assert _rel(out.cpu(), ref) < 1e-5
+
+
+@pytest.mark.parametrize("a_trans,b_kn", [(0, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("variant", [0, 4])
+def test_gemm_persistent_many_tiles(a_trans, b_kn, variant):
+    """More tiles than workgroups (every workgroup walks several tiles, the DMA ring runs across
+    tile boundaries) in the QKV / dX layouts and the split-K weight gradient (6 splits x 48 tiles)."""
+    from transmil_deepgraft_amd.engine import gemm, weight_grad, Pool
+    from transmil_deepgraft_amd._lib import BF16, F32
+    from transmil_deepgraft_amd import _lib
+    _lib.lib().tm_debug_set_variant(2, variant)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    if a_trans:     # dW[M, N] = sum_k dY[k, m] X[k, n]
+        M, N, K = 1536, 512, 4224
+        dY = torch.randn(K, M, generator=g).to(torch.bfloat16)
+        X = torch.randn(K, N, generator=g).to(torch.bfloat16)
+        ref = dY.double().t() @ X.double()
+        out = torch.empty(M, N, device=DEV)
+        weight_grad(dY.to(DEV), X.to(DEV), out, M, N, K, ldy=M, ldx=N, dtype=BF16, work_pool=Pool(DEV))
+    else:
+        M, N, K = 4136, 1536, 512
+        A = torch.randn(M, K, generator=g).to(torch.bfloat16)
+        B = torch.randn(K, N, generator=g).to(torch.bfloat16)
+        ref = A.double() @ B.double()
+        Bs = (B.contiguous() if b_kn else B.t().contiguous()).to(DEV)
+        out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        gemm(A.to(DEV), Bs, out, M, N, K, lda=K, ldb=N if b_kn else K, ldc=N, b_kn=b_kn, dtype=BF16, c_dtype=F32)
+    torch.cuda.synchronize()
+    _lib.lib().tm_debug_set_variant(2, 0)
     assert _rel(out.cpu(), ref) < 1e-5
 
 

@@ -159,7 +159,8 @@ constexpr int tile_elems() {
 // TransMIL row maps (grid duplication, QKV head-major scatter, split-K slabs).
 // The caller guarantees every wave is past its last read of the staging buffers.
 template <typename OutT>
-TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows);
+TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows,
+                               int split = -1);
 
 // accumulator tile (32x32 at rows rb, cols cb of the block tile) -> epilogue image
 TM_DEV void stage_acc(float* ep, const f32x16& acc, int rb, int cb, int lane) {
@@ -191,11 +192,12 @@ TM_DEV void gemm_epilogue(const f32x16 (&acc)[2][2], char* smem, OutT* __restric
 
 // the chunk phase: every thread of the block walks 8-column row chunks of the staged tile
 template <typename OutT>
-TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows) {
+TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows,
+                               int split) {
   const int tid = threadIdx.x;
   const float* ep = (const float*)smem;
   const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
-  const size_t slab = (size_t)blockIdx.z * g.M * g.N;
+  const size_t slab = (size_t)(split < 0 ? (int)blockIdx.z : split) * g.M * g.N;
   for (int c = tid; c < rows * (BN / 8); c += blockDim.x) {
     const int lr = c >> 4, lc = (c & 15) * 8;
     const int m = m0 + lr, n = n0 + lc;
@@ -436,11 +438,84 @@ TM_DEV bf16x8 frag_kstr_sw(const char* img, int mb, int kb, int lane) {
 template <int N>
 TM_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// LDS fragment reads as inline asm: hipcc puts an `s_waitcnt vmcnt(0)` in front of every LDS
+// read it cannot prove independent of an in-flight global_load_lds, which drains the prefetch
+// ring at every k-step (the reason this ring lost to the register-staged loop in round 1).  The
+// asm reads are ordered by explicit lgkmcnt waits + sched_barrier instead.
+TM_DEV unsigned lds_u32(const void* p) { return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p; }
+template <int OFF> TM_DEV void ds_b128(bf16x8& d, unsigned a) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+template <int OFF> TM_DEV void ds_tr64(bf16x4& d, unsigned a) {
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(d) : "v"(a), "n"(OFF) : "memory");
+}
+template <int N> TM_DEV void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+TM_DEV bf16x8 join4(const bf16x4& a, const bf16x4& b) { return (bf16x8){a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]}; }
+
+// lane addresses (relative to the operand image) of the 32-row x 8-k fragments of a 64-deep tile:
+//   k-contiguous image (128 B rows, chunk c at slot c ^ ((r >> 1) & 7)): one address per k-step
+//   k-strided image (256 B k-rows, chunk c at slot c ^ (2 (k & 3))): k-step s = +4096 s, the
+//   second 4 k-rows +1024 (the swizzle depends on k & 3 only, fixed per lane)
+TM_DEV void kc_addrs(unsigned (&a)[4], int rb, int lane) {
+  const int r = rb + (lane & 31);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int c = 2 * s + (lane >> 5);
+    a[s] = r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+  }
+}
+TM_DEV unsigned ks_addr(int mb, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int m = mb + (g & 1) * 16 + 4 * p;
+  const int k = 8 * (g >> 1) + q;
+  return k * 256 + (((m >> 3) ^ (2 * (k & 3))) << 4) + ((m >> 2) & 1) * 8;
+}
+template <bool KS, int S>
+TM_DEV void rd_frag(bf16x8& f, unsigned base, const unsigned (&kc)[4]) {
+  if constexpr (KS) {
+    bf16x4 lo, hi;
+    ds_tr64<S * 4096>(lo, base);
+    ds_tr64<S * 4096 + 1024>(hi, base);
+    f = join4(lo, hi);
+  } else {
+    ds_b128<0>(f, base + kc[S]);
+  }
+}
+
+// one 64-deep k-tile of one wave's 32 x 64 subtile: 4 k-steps of 2 MFMAs, the LDS reads of
+// step s+1 in flight while step s multiplies
+template <bool A_KS, bool B_KS>
+TM_DEV void ring_tile_mma(f32x16 (&acc)[2], unsigned abase, unsigned b0, unsigned b1, const unsigned (&akc)[4],
+                          const unsigned (&bkc0)[4], const unsigned (&bkc1)[4]) {
+  constexpr int RS = (A_KS ? 2 : 1) + 2 * (B_KS ? 2 : 1);   // LDS reads per k-step
+  bf16x8 a[2], b[2][2];
+  rd_frag<A_KS, 0>(a[0], abase, akc); rd_frag<B_KS, 0>(b[0][0], b0, bkc0); rd_frag<B_KS, 0>(b[0][1], b1, bkc1);
+  rd_frag<A_KS, 1>(a[1], abase, akc); rd_frag<B_KS, 1>(b[1][0], b0, bkc0); rd_frag<B_KS, 1>(b[1][1], b1, bkc1);
+  wait_lgkm<RS>();
+  mma16(acc[0], a[0], b[0][0]);
+  mma16(acc[1], a[0], b[0][1]);
+  rd_frag<A_KS, 2>(a[0], abase, akc); rd_frag<B_KS, 2>(b[0][0], b0, bkc0); rd_frag<B_KS, 2>(b[0][1], b1, bkc1);
+  wait_lgkm<RS>();
+  mma16(acc[0], a[1], b[1][0]);
+  mma16(acc[1], a[1], b[1][1]);
+  rd_frag<A_KS, 3>(a[1], abase, akc); rd_frag<B_KS, 3>(b[1][0], b0, bkc0); rd_frag<B_KS, 3>(b[1][1], b1, bkc1);
+  wait_lgkm<RS>();
+  mma16(acc[0], a[0], b[0][0]);
+  mma16(acc[1], a[0], b[0][1]);
+  wait_lgkm<0>();
+  mma16(acc[0], a[1], b[1][0]);
+  mma16(acc[1], a[1], b[1][1]);
+}
+
 template <typename OutT, bool A_T, bool B_KN>
 __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                         OutT* __restrict__ C, tm_gemm_args g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;  // 4 (M) x 2 (N) waves of 32 x 64
   int m0, n0;
   tile_of_block(m0, n0);
@@ -451,6 +526,20 @@ __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__
   f32x16 acc[2];
   acc[0] = (f32x16){};
   acc[1] = (f32x16){};
+  // fragment addresses relative to a stage: A at +0, B at +STAGE_BYTES/2
+  unsigned akc[4] = {0, 0, 0, 0}, bkc0[4] = {0, 0, 0, 0}, bkc1[4] = {0, 0, 0, 0};
+  unsigned aks = 0, bks0 = 0, bks1 = 0;
+  if constexpr (A_T) aks = ks_addr(wm * 32, lane); else kc_addrs(akc, wm * 32, lane);
+  if constexpr (B_KN) {
+    bks0 = ks_addr(wn * 64, lane) + STAGE_BYTES / 2;
+    bks1 = ks_addr(wn * 64 + 32, lane) + STAGE_BYTES / 2;
+  } else {
+    kc_addrs(bkc0, wn * 64, lane);
+    kc_addrs(bkc1, wn * 64 + 32, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { bkc0[s] += STAGE_BYTES / 2; bkc1[s] += STAGE_BYTES / 2; }
+  }
+  const unsigned ring = lds_u32(smem);
 
   auto issue = [&](int kt) {
     char* st = smem + (kt % NSTAGE) * STAGE_BYTES;
@@ -469,18 +558,9 @@ __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__
     __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave done reading tile kt-1
     asm volatile("" ::: "memory");
     if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1);  // overwrites tile kt-1's buffer
-    const char* sa = smem + (kt % NSTAGE) * STAGE_BYTES;
-    const char* sb = sa + STAGE_BYTES / 2;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 af = A_T ? frag_kstr_sw(sa, wm * 32, s * 16, lane) : frag_rows_sw(sa, wm * 32, s * 16, lane);
-      bf16x8 bfr[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        bfr[j] = B_KN ? frag_kstr_sw(sb, wn * 64 + j * 32, s * 16, lane) : frag_rows_sw(sb, wn * 64 + j * 32, s * 16, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) mma16(acc[j], af, bfr[j]);
-    }
+    const unsigned sb = ring + (kt % NSTAGE) * STAGE_BYTES;
+    ring_tile_mma<A_T, B_KN>(acc, (A_T ? aks : 0) + sb, (B_KN ? bks0 : 0) + sb, (B_KN ? bks1 : 0) + sb,
+                             akc, bkc0, bkc1);
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the ring
   float* ep = (float*)smem;
@@ -490,6 +570,116 @@ __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__
   gemm_epilogue_rows<OutT>(smem, C, g, m0, n0, BM);
 }
 
+// ---------------------------------------------------------------------------
+// Persistent bf16 GEMM: one 512-thread workgroup per CU walks its tiles (t = blockIdx.x +
+// i * gridDim.x, XCD-clustered) as ONE stream of 64-deep k-steps, so the global_load_lds ring
+// keeps prefetching across tile boundaries: the next tile's first k-tiles are in flight while
+// the current tile's epilogue runs (from its own LDS region).  Ring: 3 stages x 32 KB; epilogue
+// image 64 rows x EP_ROW fp32 (two halves per tile).  Same fragment reads and epilogue as the
+// ring kernel above; the split-K index rides in the tile id.
+constexpr int PSTAGE = 3;
+constexpr int PERSIST_LDS = PSTAGE * STAGE_BYTES + 64 * EP_ROW * 4;
+
+struct PTile {
+  int i, t, m0, n0, split, kbeg, nk, kt;
+};
+
+TM_DEV void ptile_set(PTile& c, int ntiles, int tiles_m, int tiles_n, const tm_gemm_args& g) {
+  c.t = blockIdx.x + c.i * gridDim.x;
+  c.kt = 0;
+  if (c.t >= ntiles) { c.nk = 0; return; }
+  // XCD clustering: workgroup b runs on XCD b % 8 and owns tiles t = b (mod gridDim.x); renumber
+  // so each XCD's tiles form contiguous row-major runs (shared A panels stay in its L2)
+  const int per = tiles_m * tiles_n;
+  const int x = c.t % 8, q = ntiles / 8, r = ntiles % 8;
+  const int id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + c.t / 8;
+  c.split = id / per;
+  const int rr = id % per;
+  c.m0 = (rr / tiles_n) * BM;
+  c.n0 = (rr % tiles_n) * BN;
+  c.kbeg = c.split * g.k_per_split;
+  c.nk = (min(g.K, c.kbeg + g.k_per_split) - c.kbeg) / 64;
+}
+
+template <typename OutT, bool A_T, bool B_KN>
+__global__ __launch_bounds__(512) void gemm_persist_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           OutT* __restrict__ C, tm_gemm_args g, int tiles_m,
+                                                           int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* epi = smem + PSTAGE * STAGE_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntiles = tiles_m * tiles_n * g.splits;
+
+  unsigned akc[4] = {0, 0, 0, 0}, bkc0[4] = {0, 0, 0, 0}, bkc1[4] = {0, 0, 0, 0};
+  unsigned aks = 0, bks0 = 0, bks1 = 0;
+  if constexpr (A_T) aks = ks_addr(wm * 32, lane); else kc_addrs(akc, wm * 32, lane);
+  if constexpr (B_KN) {
+    bks0 = ks_addr(wn * 64, lane) + STAGE_BYTES / 2;
+    bks1 = ks_addr(wn * 64 + 32, lane) + STAGE_BYTES / 2;
+  } else {
+    kc_addrs(bkc0, wn * 64, lane);
+    kc_addrs(bkc1, wn * 64 + 32, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { bkc0[s] += STAGE_BYTES / 2; bkc1[s] += STAGE_BYTES / 2; }
+  }
+  const unsigned ring = lds_u32(smem);
+
+  PTile is{}, cs{};
+  is.i = 0;
+  ptile_set(is, ntiles, tiles_m, tiles_n, g);
+  while (is.nk == 0 && is.t < ntiles) { ++is.i; ptile_set(is, ntiles, tiles_m, tiles_n, g); }  // empty splits
+  cs = is;
+  int issued = 0, done = 0;
+  auto issue = [&]() {
+    char* st = smem + (issued % PSTAGE) * STAGE_BYTES;
+    const int k0 = is.kbeg + is.kt * 64;
+    glds_tile<A_T>(st, A, g.lda, is.m0, g.M, k0, wave, lane);
+    glds_tile<B_KN>(st + STAGE_BYTES / 2, B, g.ldb, is.n0, g.N, k0, wave, lane);
+    ++issued;
+    if (++is.kt == is.nk) {
+      do { ++is.i; ptile_set(is, ntiles, tiles_m, tiles_n, g); } while (is.nk == 0 && is.t < ntiles);
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < PSTAGE - 1; ++p)
+    if (is.t < ntiles) issue();
+
+  f32x16 acc[2];
+  acc[0] = (f32x16){};
+  acc[1] = (f32x16){};
+  while (cs.t < ntiles) {
+    // step `done` landed once at most (issued - done - 1) younger steps (4 loads each) remain
+    if (issued - done - 1 >= 1) wait_vm<4>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave done with step done-1
+    asm volatile("" ::: "memory");
+    if (is.t < ntiles) issue();    // overwrites step done-1's slot
+    const unsigned sb = ring + (done % PSTAGE) * STAGE_BYTES;
+    ring_tile_mma<A_T, B_KN>(acc, (A_T ? aks : 0) + sb, (B_KN ? bks0 : 0) + sb, (B_KN ? bks1 : 0) + sb,
+                             akc, bkc0, bkc1);
+    ++done;
+    if (++cs.kt == cs.nk) {
+      // epilogue of this tile from the epilogue image (two 64-row halves); the next tile's
+      // first k-steps are already in flight
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        if ((wm >> 1) == half) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) stage_acc((float*)epi, acc[j], (wm & 1) * 32, wn * 64 + j * 32, lane);
+        }
+        __syncthreads();
+        gemm_epilogue_rows<OutT>(epi, C, g, cs.m0 + half * 64, cs.n0, 64, cs.split);
+        __syncthreads();
+      }
+      wait_vm<0>();   // the epilogue's own loads / stores (their count is data dependent)
+      acc[0] = (f32x16){};
+      acc[1] = (f32x16){};
+      do { ++cs.i; ptile_set(cs, ntiles, tiles_m, tiles_n, g); } while (cs.nk == 0 && cs.t < ntiles);
+    }
+  }
+}
+
 template <typename T, bool A_T, bool B_KN, int NBUF = 2>
 constexpr size_t gemm_smem() {
   constexpr size_t main = NBUF * (tile_elems<T, A_T>() + tile_elems<T, B_KN>()) * sizeof(T);
@@ -497,11 +687,14 @@ constexpr size_t gemm_smem() {
   return main > epi ? main : epi;
 }
 
-int g_gemm_variant = 0;  // debug: 0/1 = register-staged loop (1 / 2 LDS buffers), 2 = global_load_lds ring
+// 0 = register-staged loop, 1 LDS buffer (the default: fastest measured, scripts/microbench.py
+// --gemm-ab: QKV 34.3 us vs 42.6 persistent ring, 36.8 per-tile ring); 1 = register-staged,
+// 2 LDS buffers; 2 = per-tile DMA ring; 4 = persistent DMA ring
+int g_gemm_variant = 0;
 
 template <typename OutT>
 bool ring_ok(const tm_gemm_args& g) {
-  if (g_gemm_variant != 2) return false;
+  if (g_gemm_variant != 2 && g_gemm_variant != 4) return false;
   // whole 64-deep k-tiles in every split; k-strided operands need >= 8 rows/cols (clamped 16-B pieces)
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if ((g.a_trans && g.M < 8) || (g.b_kn && g.N < 8)) return false;
@@ -514,6 +707,21 @@ template <typename T, typename OutT>
 int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.splits);
   if constexpr (sizeof(T) == 2) {
+    if (ring_ok<OutT>(g) && g_gemm_variant == 4) {
+      const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+      const int ntiles = tiles_m * tiles_n * g.splits;
+      const int nwg = ntiles < 256 ? ntiles : 256;
+#define TM_PERSIST_CASE(AT, BKN)                                                                \
+      if (g.a_trans == AT && g.b_kn == BKN) {                                                   \
+        tm_allow_smem(gemm_persist_kernel<OutT, AT, BKN>, PERSIST_LDS);                         \
+        gemm_persist_kernel<OutT, AT, BKN><<<nwg, 512, PERSIST_LDS, st>>>((const bf16*)A, (const bf16*)B, \
+                                                                        (OutT*)C, g, tiles_m, tiles_n); \
+        TM_CHECK_LAUNCH();                                                                      \
+        return 0;                                                                               \
+      }
+      TM_PERSIST_CASE(0, 0) TM_PERSIST_CASE(0, 1) TM_PERSIST_CASE(1, 0) TM_PERSIST_CASE(1, 1)
+#undef TM_PERSIST_CASE
+    }
     if (ring_ok<OutT>(g)) {
       constexpr size_t epi = (size_t)BM * EP_ROW * sizeof(float);
       constexpr size_t sm = RING_BYTES > epi ? RING_BYTES : epi;

@@ -157,18 +157,18 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
                 if g[key] != self.param_groups[0][key]:
                     raise ValueError(f"fused RAdam: '{key}' must be equal across groups")
         self._params = plist
-        total = sum(p.numel() for p in plist)
+        total = sum((p.numel() + 3) // 4 * 4 for p in plist)
         dev = plist[0].device
         self._flat = torch.zeros(3, total, dtype=torch.float32, device=dev)  # exp_avg, exp_avg_sq, slow
-        self._counters = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._counters = torch.zeros(3, dtype=torch.int32, device=dev)   # steps + the kernel's scratch count
         self._offsets = [0]
-        for p in plist:
-            self._offsets.append(self._offsets[-1] + p.numel())
+        for p in plist:     # each tensor's flat state padded to a multiple of 4 (16-B vectors)
+            self._offsets.append(self._offsets[-1] + (p.numel() + 3) // 4 * 4)
         self._bind_state()
 
     def _bind_state(self):
         for i, p in enumerate(self._params):
-            a, b = self._offsets[i], self._offsets[i + 1]
+            a, b = self._offsets[i], self._offsets[i] + p.numel()
             self.state[p] = {"exp_avg": self._flat[0, a:b].view_as(p),
                              "exp_avg_sq": self._flat[1, a:b].view_as(p),
                              "slow_buffer": self._flat[2, a:b].view_as(p)}
@@ -213,12 +213,13 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
         with torch.no_grad():
             for i, p in enumerate(self._params):
                 st = self.state[p]
-                a, b = self._offsets[i], self._offsets[i + 1]
+                a, b = self._offsets[i], self._offsets[i] + p.numel()
                 for row, key in enumerate(("exp_avg", "exp_avg_sq", "slow_buffer")):
                     if key in st:
                         self._flat[row, a:b].copy_(st[key].reshape(-1))
             if counters is not None:
-                self._counters.copy_(counters)
+                self._counters.zero_()
+                self._counters[:2].copy_(counters[:2])
         self._bind_state()
 
 
