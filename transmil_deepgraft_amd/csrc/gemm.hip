@@ -158,7 +158,7 @@ constexpr int tile_elems() {
 // loads/stores: bias, pre-activation store, GELU, dropout, residual, accumulate, and the
 // TransMIL row maps (grid duplication, QKV head-major scatter, split-K slabs).
 // The caller guarantees every wave is past its last read of the staging buffers.
-template <typename OutT>
+template <typename OutT, int TBN = BN>
 TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows,
                                int split = -1);
 
@@ -191,20 +191,22 @@ TM_DEV void gemm_epilogue(const f32x16 (&acc)[2][2], char* smem, OutT* __restric
 }
 
 // the chunk phase: every thread of the block walks 8-column row chunks of the staged tile
-template <typename OutT>
+// (image rows of TBN + 8 floats)
+template <typename OutT, int TBN>
 TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows,
                                int split) {
+  constexpr int CPR = TBN / 8, ROWF = TBN + 8;
   const int tid = threadIdx.x;
   const float* ep = (const float*)smem;
   const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
   const size_t slab = (size_t)(split < 0 ? (int)blockIdx.z : split) * g.M * g.N;
-  for (int c = tid; c < rows * (BN / 8); c += blockDim.x) {
-    const int lr = c >> 4, lc = (c & 15) * 8;
+  for (int c = tid; c < rows * CPR; c += blockDim.x) {
+    const int lr = c / CPR, lc = (c % CPR) * 8;
     const int m = m0 + lr, n = n0 + lc;
     if (m >= g.M || n >= g.N) continue;
     float v[8];
     {
-      const f32x4 lo = *(const f32x4*)(ep + lr * EP_ROW + lc), hi = *(const f32x4*)(ep + lr * EP_ROW + lc + 4);
+      const f32x4 lo = *(const f32x4*)(ep + lr * ROWF + lc), hi = *(const f32x4*)(ep + lr * ROWF + lc + 4);
       v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
     }
     const int ne = min(8, g.N - n);  // valid columns in this chunk
@@ -680,6 +682,188 @@ __global__ __launch_bounds__(512) void gemm_persist_kernel(const bf16* __restric
   }
 }
 
+// ---------------------------------------------------------------------------
+// Big-tile bf16 GEMM: 256 x TBN (256 or 128) per 512-thread workgroup.  A 128 x 128 tile moves
+// 32 KB of operands per 64-deep k-step for 2 MFLOP (64 flop/B): at 2.5 PF that needs ~39 TB/s of
+// L2 -> CU operand bandwidth, which the chip does not have (the 128-tile kernels above run at
+// 15 % of the MFMA peak).  256 x 256 halves the bytes per flop (128 flop/B); 256 x 128 serves
+// the N = 512 shapes with twice the workgroups.  8 waves: 2 (M) x 4 (N) of 128 x 64 (TBN 256)
+// or 4 x 2 of 64 x 64 (TBN 128); operands by global_load_lds into a 2- / 3-stage ring of
+// swizzled images (k-contiguous: 128-B rows; k-strided: 64 k-rows of 2 x TBM / TBN bytes), LDS
+// fragment reads as inline asm (no vmcnt(0) drains), epilogue staged 64 rows at a time.
+constexpr int GBM = 256;
+
+template <int ROWS>
+TM_DEV void glds_big(char* img, const bf16* X, int ld, int r0, int rmax, int k0, bool kstr, int wave, int lane) {
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
+  constexpr int PIECES = ROWS * 128 / 1024;          // 1-KB pieces per image (32 or 16)
+  constexpr int PPW = PIECES / 8;                    // per wave
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int j = wave * PPW + i;
+    const bf16* src;
+    if (!kstr) {                 // 8 rows x 128 B per piece, chunk c of row r at slot c ^ ((r >> 1) & 7)
+      const int r = j * 8 + (lane >> 3), slot = lane & 7;
+      const int c = slot ^ ((r >> 1) & 7);
+      const int gr = min(r0 + r, rmax - 1);
+      src = X + (size_t)gr * ld + k0 + c * 8;
+    } else {                     // k-rows of ROWS*2 bytes: 1024 / (ROWS*2) k-rows per piece
+      constexpr int CH = ROWS / 8;                     // 16-B chunks per k-row (32 or 16)
+      constexpr int KPP = 64 / CH;                     // k-rows per piece (2 or 4)
+      const int k = j * KPP + lane / CH, slot = lane % CH;
+      const int c = slot ^ (2 * (k & 3));
+      const int gm = min(r0 + c * 8, rmax - 8);
+      src = X + (size_t)(k0 + k) * ld + gm;
+    }
+    __builtin_amdgcn_global_load_lds((glb_t*)src, (lds_t*)(img + j * 1024), 16, 0, 0);
+  }
+}
+
+// k-strided image lane address (k-step 0, first 4 k-rows) for a 32-wide fragment at mb
+template <int ROWS>
+TM_DEV unsigned ks_addr_big(int mb, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int m = mb + (g & 1) * 16 + 4 * p;
+  const int k = 8 * (g >> 1) + q;
+  return k * (ROWS * 2) + (((m >> 3) ^ (2 * (k & 3))) << 4) + ((m >> 2) & 1) * 8;
+}
+
+template <bool KS, int ROWS, int S>
+TM_DEV void rd_big(bf16x8& f, unsigned base, unsigned kc_s) {
+  if constexpr (KS) {
+    bf16x4 lo, hi;
+    ds_tr64<S * 16 * ROWS * 2>(lo, base);
+    ds_tr64<S * 16 * ROWS * 2 + 4 * ROWS * 2>(hi, base);
+    f = join4(lo, hi);
+  } else {
+    ds_b128<0>(f, base + kc_s);
+  }
+}
+
+template <typename OutT, bool A_T, bool B_KN, int TBN>
+__global__ __launch_bounds__(512) void gemm_big_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                       OutT* __restrict__ C, tm_gemm_args g) {
+  constexpr int WM = TBN == 256 ? 2 : 4, WN = 8 / WM;
+  constexpr int FM = GBM / WM / 32, FN = TBN / WN / 32;      // 32x32 MFMA tiles per wave
+  constexpr int A_BYTES = GBM * 128, B_BYTES = TBN * 128, STG = A_BYTES + B_BYTES;
+  constexpr int NS = TBN == 256 ? 2 : 3;
+  constexpr int RS = FM * (A_T ? 2 : 1) + FN * (B_KN ? 2 : 1);   // LDS reads per k-step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  // XCD-aware tile order (as tile_of_block, 256 x TBN tiles)
+  int m0, n0;
+  {
+    const int ntx = gridDim.x, nwg = gridDim.x * gridDim.y;
+    const int orig = blockIdx.y * ntx + blockIdx.x;
+    const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+    m0 = (id / ntx) * GBM;
+    n0 = (id % ntx) * TBN;
+  }
+  const int kbeg = blockIdx.z * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = kend > kbeg ? (kend - kbeg) / 64 : 0;
+
+  // per-lane fragment addresses relative to a stage
+  unsigned ab[FM], bb[FN];
+  unsigned akc[FM][4], bkc[FN][4];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int rb = wm * (GBM / WM) + i * 32;
+    if constexpr (A_T) ab[i] = ks_addr_big<GBM>(rb, lane);
+    else { ab[i] = 0; kc_addrs(akc[i], rb, lane); }
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int cb = wn * (TBN / WN) + j * 32;
+    if constexpr (B_KN) bb[j] = ks_addr_big<TBN>(cb, lane) + A_BYTES;
+    else {
+      bb[j] = A_BYTES;
+      kc_addrs(bkc[j], cb, lane);
+    }
+  }
+  const unsigned ring = lds_u32(smem);
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = (f32x16){};
+
+  auto issue = [&](int kt) {
+    char* st = smem + (kt % NS) * STG;
+    const int k0 = kbeg + kt * 64;
+    glds_big<GBM>(st, A, g.lda, m0, g.M, k0, A_T, wave, lane);
+    glds_big<TBN>(st + A_BYTES, B, g.ldb, n0, g.N, k0, B_KN, wave, lane);
+  };
+  constexpr int LPW = (GBM + TBN) * 128 / 1024 / 8;       // loads per wave per stage
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(t);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(NS - 2, nk - 1 - kt);
+    if (ahead >= 1) wait_vm<LPW>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);
+    const unsigned sb = ring + (kt % NS) * STG;
+    bf16x8 af[2][FM], bf[2][FN];
+#define TM_BIG_READ(BUF, S)                                                                       \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i) rd_big<A_T, GBM, S>(af[BUF][i], ab[i] + sb, A_T ? 0u : akc[i][S]); \
+    _Pragma("unroll") for (int j = 0; j < FN; ++j) rd_big<B_KN, TBN, S>(bf[BUF][j], bb[j] + sb, B_KN ? 0u : bkc[j][S]);
+#define TM_BIG_MMA(BUF)                                                                           \
+    _Pragma("unroll") for (int i = 0; i < FM; ++i)                                                \
+      _Pragma("unroll") for (int j = 0; j < FN; ++j) mma16(acc[i][j], af[BUF][i], bf[BUF][j]);
+    TM_BIG_READ(0, 0)
+    TM_BIG_READ(1, 1)
+    wait_lgkm<RS>();
+    TM_BIG_MMA(0)
+    TM_BIG_READ(0, 2)
+    wait_lgkm<RS>();
+    TM_BIG_MMA(1)
+    TM_BIG_READ(1, 3)
+    wait_lgkm<RS>();
+    TM_BIG_MMA(0)
+    wait_lgkm<0>();
+    TM_BIG_MMA(1)
+#undef TM_BIG_READ
+#undef TM_BIG_MMA
+  }
+  __syncthreads();   // every fragment read done: the ring becomes the epilogue image
+  float* ep = (float*)smem;
+  constexpr int ROWF = TBN + 8;
+#pragma unroll
+  for (int qtr = 0; qtr < GBM / 64; ++qtr) {
+    // rows 64 qtr .. +63: wave row wm covers rows wm * GBM/WM .. ; its frags i with 32-row blocks inside
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int rb = wm * (GBM / WM) + i * 32;
+      if (rb / 64 == qtr) {
+        const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int cb = wn * (TBN / WN) + j * 32;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) ep[(rb - 64 * qtr + acc_row(r, h)) * ROWF + cb + l32] = acc[i][j][r];
+        }
+      }
+    }
+    __syncthreads();
+    gemm_epilogue_rows<OutT, TBN>((char*)smem, C, g, m0 + qtr * 64, n0, 64);
+    __syncthreads();
+  }
+}
+
+template <typename OutT, int TBN>
+constexpr int big_lds() {
+  constexpr int ring = (TBN == 256 ? 2 : 3) * (GBM + TBN) * 128;
+  constexpr int epi = 64 * (TBN + 8) * 4;
+  return ring > epi ? ring : epi;
+}
+
 template <typename T, bool A_T, bool B_KN, int NBUF = 2>
 constexpr size_t gemm_smem() {
   constexpr size_t main = NBUF * (tile_elems<T, A_T>() + tile_elems<T, B_KN>()) * sizeof(T);
@@ -687,9 +871,10 @@ constexpr size_t gemm_smem() {
   return main > epi ? main : epi;
 }
 
-// 0 = register-staged loop, 1 LDS buffer (the default: fastest measured, scripts/microbench.py
-// --gemm-ab: QKV 34.3 us vs 42.6 persistent ring, 36.8 per-tile ring); 1 = register-staged,
-// 2 LDS buffers; 2 = per-tile DMA ring; 4 = persistent DMA ring
+// 0 = big-tile DMA kernel (bf16, where it applies; else the register-staged loop with 1 LDS
+// buffer); 1 = register-staged, 2 LDS buffers; 2 = per-tile 128 x 128 DMA ring; 3 = register-
+// staged, 1 LDS buffer; 4 = persistent 128 x 128 DMA ring (QKV: 34.3 us register-staged, 36.8
+// per-tile ring, 42.6 persistent ring -- the 128-tiles are operand-bandwidth bound)
 int g_gemm_variant = 0;
 
 template <typename OutT>
@@ -703,10 +888,36 @@ bool ring_ok(const tm_gemm_args& g) {
   return true;
 }
 
+template <typename OutT>
+bool big_ok(const tm_gemm_args& g) {
+  if (g_gemm_variant != 0) return false;
+  if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
+  if (g.a_trans && (g.M % 8 != 0 || g.M < 8)) return false;
+  if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
+  return g.M >= 128;
+}
+
 template <typename T, typename OutT>
 int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.splits);
   if constexpr (sizeof(T) == 2) {
+    if (big_ok<OutT>(g)) {
+#define TM_BIG_CASE(AT, BKN, TBN)                                                                  \
+      if (g.a_trans == AT && g.b_kn == BKN) {                                                      \
+        constexpr int sm = big_lds<OutT, TBN>();                                                   \
+        tm_allow_smem(gemm_big_kernel<OutT, AT, BKN, TBN>, sm);                                   \
+        const dim3 gb((g.N + TBN - 1) / TBN, (g.M + GBM - 1) / GBM, g.splits);                      \
+        gemm_big_kernel<OutT, AT, BKN, TBN><<<gb, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        TM_CHECK_LAUNCH();                                                                         \
+        return 0;                                                                                  \
+      }
+      if (g.N >= 1024) {
+        TM_BIG_CASE(0, 0, 256) TM_BIG_CASE(0, 1, 256) TM_BIG_CASE(1, 0, 256) TM_BIG_CASE(1, 1, 256)
+      } else {
+        TM_BIG_CASE(0, 0, 128) TM_BIG_CASE(0, 1, 128) TM_BIG_CASE(1, 0, 128) TM_BIG_CASE(1, 1, 128)
+      }
+#undef TM_BIG_CASE
+    }
     if (ring_ok<OutT>(g) && g_gemm_variant == 4) {
       const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
       const int ntiles = tiles_m * tiles_n * g.splits;
