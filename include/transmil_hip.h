@@ -134,6 +134,14 @@ int tm_nys_attn_row(int dtype, const void* q, const void* k, const float* ql, co
                     const float* lse3, int nbh, int n, int row, float* out, void* stream);
 int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const float* dk, const float* dkl,
                          const float* dv, int nbags, int nh, int n, float scale, void* dqkv, void* stream);
+/* bf16 mode, fused key side: the A3 backward writes the final bf16 k / v parts of dqkv
+ * (k = dK + dk~[t/l]/l, v = dv_conv + dV) and dql (=) from its slabs; then tm_nys_assemble_q
+ * writes the q part, scale * (dq + (dql_a + dql_b)[t/l]/l). */
+int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v, const float* lse3,
+                        const float* d3, int nbh, int nh, int n, const float* dv_conv, const float* dkl,
+                        float* work, float* dql, void* dqkv, void* stream);
+int tm_nys_assemble_q(int dtype, const float* dq, const float* dql_a, const float* dql_b, int nbags, int nh,
+                      int n, float scale, void* dqkv, void* stream);
 
 /* ---- pseudo-inverse + small fp32 batched products (pinv.hip) -------------
  * moore_penrose_iter_pinv of nystrom_attention (App. A eq. 7).

@@ -90,6 +90,8 @@ _SIGS = {
     "tm_nys_a3_bwd_workspace": (L, [I, I]),
     "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, I, P]),
     "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
+    "tm_nys_a3_bwd_fused": (I, [P, P, P, P, P, P, I, I, I, P, P, P, P, P, P]),
+    "tm_nys_assemble_q": (I, [I, P, P, P, I, I, I, Fl, P, P]),
     "tm_nys_attn_row": (I, [I, P, P, P, P, P, P, I, I, I, P, P]),
     "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
     "tm_debug_set_variant": (None, [I, I]),

@@ -894,7 +894,10 @@ bool big_ok(const tm_gemm_args& g) {
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if (g.a_trans && (g.M % 8 != 0 || g.M < 8)) return false;
   if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
-  return g.M >= 128;
+  // only where it measured faster: N >= 1024 (the QKV projection, 256 x 256 tiles: 33.1 vs 35.3 us);
+  // the N = 512 shapes on 256 x 128 tiles leave half the CUs idle (to_out / fc1 30.1 vs 27.5,
+  // dmerged ~29 vs 21.6 us) and stay on the register-staged loop
+  return g.M >= 128 && g.N >= 1024;
 }
 
 template <typename T, typename OutT>

@@ -912,6 +912,9 @@ struct BwdArgs {
   long long slab_stride;                                // per block partial slab stride (MODE dependent)
   int nh, n_queries_per_wg, n_key_rows;
   int q_total;  // bf16 A1 kernel: > 0 = split the q_total / 32 query chunks evenly over gridDim.x
+  // bf16 A3 kernel, fused key side: non-null = write the FINAL k / v parts of dqkv (bf16,
+  // [bag][n][3 nh 64]): k = dK + dk~[t / l] / l, v = dv (the conv backward's, read) + dV
+  void* dqkv; const float* dkl; float inv_l; int l;
 };
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
@@ -1096,6 +1099,23 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
       }
     }
     __syncthreads();
+    if (MODE == MODE_A3 && a.dqkv) {
+      // fused: the final bf16 k / v rows of dqkv (no fp32 key-side slabs, no assemble pass for them)
+      const int bag = bh / nh, hh = bh % nh, inner = nh * DH;
+      bf16* out = (bf16*)a.dqkv + ((size_t)bag * a.n_key_rows + key0) * 3 * inner + (which == 0 ? 2 : 1) * inner + hh * DH;
+      const float* dvc = a.dv + bh * a.dv_bh + (size_t)key0 * DH;
+      const float* dkl = a.dkl + (size_t)bh * NL * DH;
+      for (int i = tid; i < NL * DH / 4; i += 512) {
+        const int key = i >> 4, d4 = (i & 15) * 4;
+        f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
+        if (which == 0) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
+        else val += *(const f32x4*)(dkl + (size_t)((key0 + key) / a.l) * DH + d4) * a.inv_l;
+        *(bf16x4*)(out + (size_t)key * 3 * inner + d4) =
+            (bf16x4){(bf16)val[0], (bf16)val[1], (bf16)val[2], (bf16)val[3]};
+      }
+      __syncthreads();
+      continue;
+    }
     float* dst;
     bool add = false;
     if (MODE == MODE_A3) {
@@ -1313,6 +1333,23 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
             (f32x4){accv[4 * g4], accv[4 * g4 + 1], accv[4 * g4 + 2], accv[4 * g4 + 3]};
     }
     __syncthreads();
+    if (MODE == MODE_A3 && a.dqkv) {
+      // fused: the final bf16 k / v rows of dqkv (no fp32 key-side slabs, no assemble pass for them)
+      const int bag = bh / nh, hh = bh % nh, inner = nh * DH;
+      bf16* out = (bf16*)a.dqkv + ((size_t)bag * a.n_key_rows + key0) * 3 * inner + (which == 0 ? 2 : 1) * inner + hh * DH;
+      const float* dvc = a.dv + bh * a.dv_bh + (size_t)key0 * DH;
+      const float* dkl = a.dkl + (size_t)bh * NL * DH;
+      for (int i = tid; i < NL * DH / 4; i += 512) {
+        const int key = i >> 4, d4 = (i & 15) * 4;
+        f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
+        if (which == 0) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
+        else val += *(const f32x4*)(dkl + (size_t)((key0 + key) / a.l) * DH + d4) * a.inv_l;
+        *(bf16x4*)(out + (size_t)key * 3 * inner + d4) =
+            (bf16x4){(bf16)val[0], (bf16)val[1], (bf16)val[2], (bf16)val[3]};
+      }
+      __syncthreads();
+      continue;
+    }
     float* dst;
     bool add = false;
     if (MODE == MODE_A3) {
@@ -1373,6 +1410,29 @@ __global__ void assemble_dqkv_kernel(const float* __restrict__ dq, const float* 
     else val = a[e];
     out[e] = from_f<T>(val);
   }
+  store8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c, out);
+}
+
+// q part of dqkv only (the k / v parts written by the fused A3 backward):
+// q = scale * (dq + (dql_a + dql_b)[t / l] / l); grid (ceil(n * nh * 8 / 256), nbags), block 256
+template <typename T>
+__global__ void assemble_q_kernel(const float* __restrict__ dq, const float* __restrict__ dql_a,
+                                  const float* __restrict__ dql_b, int n, int l, int nh, float scale,
+                                  T* __restrict__ dqkv) {
+  const int inner = nh * DH, per_row = inner / 8;
+  const long long item = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (item >= (long long)n * per_row) return;
+  const int c = (int)(item % per_row) * 8;
+  const int t = (int)(item / per_row), bag = blockIdx.y;
+  const int head = c / DH, d = c % DH;
+  const size_t bh = (size_t)bag * nh + head;
+  const size_t row = (bh * n + t) * DH + d;
+  const size_t lrow = (bh * NL + t / l) * DH + d;
+  const float inv_l = 1.0f / (float)l;
+  const f32x8 a = load8<float>(dq + row), b0 = load8<float>(dql_a + lrow), b1 = load8<float>(dql_b + lrow);
+  vec8<T> out;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) out[e] = from_f<T>(scale * (a[e] + (b0[e] + b1[e]) * inv_l));
   store8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c, out);
 }
 
@@ -1596,6 +1656,44 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
   }
   TM_CHECK_LAUNCH();
   return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, accumulate, stream);
+}
+
+// bf16 A3 backward with the fused key-side epilogue: the final k / v parts of dqkv from dK, dV,
+// the conv backward's dv (fp32, read) and dk~ (fp32 [bh][256][64], after the pseudo-inverse
+// backward); dql3 (=) from the per-key-block slabs.
+extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v,
+                                   const float* lse3, const float* d3, int nbh, int nh, int n, const float* dv_conv,
+                                   const float* dkl, float* work, float* dql, void* dqkv, void* stream) {
+  TM_REQUIRE(n % NL == 0 && nbh % nh == 0, "a3_bwd_fused: n must be a multiple of 256");
+  TM_REQUIRE(dv_conv && dkl && dqkv, "a3_bwd_fused: null operand");
+  const int nkb = n / NL;
+  BwdArgs a{};
+  a.q = ql_t; a.q_bag = (long long)nh * NL * DH; a.q_head = (long long)NL * DH; a.q_row = DH;
+  a.dO = dw_t; a.o_bag = a.q_bag; a.o_head = a.q_head; a.o_row = DH;
+  a.k = k; a.k_bag = (long long)nh * n * DH; a.k_head = (long long)n * DH;
+  a.v = v; a.v_bag = a.k_bag; a.v_head = a.k_head;
+  a.lse = lse3; a.lse_bh = NL; a.dd = d3; a.dd_bh = NL;
+  a.dq = work; a.dq_bh = (long long)NL * DH;
+  a.slab_stride = (long long)nbh * NL * DH;
+  a.dv = (float*)dv_conv; a.dv_bh = (long long)n * DH;
+  a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
+  a.dqkv = dqkv; a.dkl = dkl; a.l = n / NL; a.inv_l = 1.0f / (float)(n / NL);
+  hipStream_t st = (hipStream_t)stream;
+  tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3>, BwdLay16::BYTES);
+  attn_bwd_bf16_kernel<MODE_A3><<<dim3(nkb, nbh), 512, BwdLay16::BYTES, st>>>(a);
+  TM_CHECK_LAUNCH();
+  return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, 0, stream);
+}
+
+extern "C" int tm_nys_assemble_q(int dtype, const float* dq, const float* dql_a, const float* dql_b, int nbags,
+                                 int nh, int n, float scale, void* dqkv, void* stream) {
+  TM_REQUIRE(n % NL == 0, "assemble_q: n must be a multiple of 256");
+  const long long items = (long long)n * nh * DH / 8;
+  TM_DTYPE_DISPATCH(dtype, (assemble_q_kernel<T><<<dim3((unsigned)((items + 255) / 256), nbags), 256, 0,
+                                                    (hipStream_t)stream>>>(dq, dql_a, dql_b, n, n / NL, nh, scale,
+                                                                           (T*)dqkv)));
+  TM_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const float* dk, const float* dkl,

@@ -327,15 +327,17 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     else:
         dz_job = bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH)
     bmm([dz_job, bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh, prec)
-    # A3 product backward: dk (=), dv (+=), dql3 (=)
     d3 = pool(nbh * NL)
     dw_t = pool(nbh * NL * DH, tdtype)
     dql3 = pool(nbh * NL * DH).view(nbh, NL, DH)
     work3 = pool(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4)
     _lib.call("tm_nys_rowdot_cast", dt_code, _p(dw), _p(state["w"]), nbh * NL, _p(d3), _p(dw_t), st)
-    with probe("a3_bwd"):
-        _lib.call("tm_nys_a3_bwd", dt_code, _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]),
-                  _p(d3), nbh, nh, n, _p(dk), _p(dv), _p(work3), _p(dql3), 0, st)
+    fused = state["a2s"] is not None     # bf16 mode: the A3 backward writes the final k / v parts
+    if not fused:
+        # A3 product backward: dk (=), dv (+=), dql3 (=)
+        with probe("a3_bwd"):
+            _lib.call("tm_nys_a3_bwd", dt_code, _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]),
+                      _p(d3), nbh, nh, n, _p(dk), _p(dv), _p(work3), _p(dql3), 0, st)
     # pseudo-inverse backward -> dA2, then softmax backward
     ds2 = pool(mat).view(nbh, NL, NL)
     if state["a2s"] is not None:
@@ -350,9 +352,20 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
                   _p(da2), st)
         _lib.call("tm_softmax_bwd_rows256", _p(state["a2"]), _p(da2), _p(ds2), nbh * NL, st)
     dql = pool(nbh * NL * DH).view(nbh, NL, DH)
+    dqkv = pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH)
+    if fused:
+        # dq~ (landmark path, without the A3 part) and the final dk~ (+= the A1 part) first; the
+        # fused A3 backward then writes k / v of dqkv and dq~3; assemble_q writes q
+        bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL),
+             bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
+        with probe("a3_bwd"):
+            _lib.call("tm_nys_a3_bwd_fused", _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]), _p(d3),
+                      nbh, nh, n, _p(dv), _p(dkl), _p(work3), _p(dql3), _p(dqkv), st)
+        _lib.call("tm_nys_assemble_q", dt_code, _p(dq), _p(dql), _p(dql3), geo.B, nh, n, C.c_float(scale),
+                  _p(dqkv), st)
+        return dqkv
     bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL, E1=dql3, e1=1.0),
          bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
-    dqkv = pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH)
     _lib.call("tm_nys_assemble_dqkv", dt_code, _p(dq), _p(dql), _p(dk), _p(dkl), _p(dv), geo.B, nh, n,
               C.c_float(scale), _p(dqkv), st)
     return dqkv
