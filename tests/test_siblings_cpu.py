@@ -19,3 +19,16 @@ def test_sibling_state_dict_layout(name):
     assert a == b
     with pytest.raises(RuntimeError, match="GPU"):
         ours(torch.zeros(tuple(meta["input_shape"])))
+
+
+def test_attention_map_refuses_huge_materialisation():
+    """The lazy return_attn product raises instead of allocating B*h*n'^2 fp32 above the limit
+    (35 GB per layer at N = 32768); row access stays available."""
+    from transmil_deepgraft_amd.nystrom_attention import AttentionMap
+    qkv = torch.empty(3, 8, 33280, 64, device="meta")
+    attn = AttentionMap(qkv, {}, heads=8)
+    assert tuple(attn.shape) == (1, 8, 33280, 33280)
+    with pytest.raises(RuntimeError, match="GiB"):
+        attn.full()
+    with pytest.raises(RuntimeError, match="GiB"):
+        attn[:, :, 5:7]

@@ -134,7 +134,11 @@ class AttentionMap:
 
     ``attn[b, heads, r, cols]`` with an integer row ``r`` computes that row only
     (``tm_nys_attn_row``); every other index, attribute or tensor use materialises the full
-    product once (``attention_matrix``) and forwards to it."""
+    product once (``attention_matrix``) and forwards to it.  That product is B·h·n'² fp32
+    (35 GB per layer at N = 32768): above ``max_full_bytes`` (default 8 GiB, class attribute)
+    it raises instead of allocating; raise the limit explicitly to materialise anyway."""
+
+    max_full_bytes = 8 << 30
 
     def __init__(self, qkv, core, heads):
         self._qkv, self._core, self._heads = qkv, core, heads
@@ -157,6 +161,12 @@ class AttentionMap:
 
     def full(self):
         if self._full is None:
+            nbytes = 4 * self.shape[0] * self.shape[1] * self.shape[2] * self.shape[3]
+            if nbytes > AttentionMap.max_full_bytes:
+                raise RuntimeError(
+                    f"AttentionMap: materialising the full {tuple(self.shape)} return_attn product needs "
+                    f"{nbytes / 2**30:.1f} GiB; index one row (attn[b, heads, r, cols]) instead, or raise "
+                    "AttentionMap.max_full_bytes to allow it")
             self._full = attention_matrix(self._qkv, self._core, self._heads)
         return self._full
 
