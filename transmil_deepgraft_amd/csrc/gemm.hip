@@ -1074,20 +1074,22 @@ struct ReduceEntry {
 struct ReduceTable {
   ReduceEntry e[DEFER_MAX];
   long long off[DEFER_MAX + 1];   // prefix sums of the entries' thread counts
+  int boff[DEFER_MAX + 1];        // prefix sums of the entries' workgroup counts (256 threads each)
   int n;
 };
 static ReduceTable g_defer{};
 static int g_defer_on = 0;
 
-// one thread = one 16-B unit (4 floats; entries whose count is not a multiple of 4 go element by
-// element), the splits summed in index order with 12 loads in flight per thread
+// one thread = one 16-B unit (4 floats; entries whose count is not a multiple of 4 or whose
+// pointers are not 16-B aligned go element by element); every workgroup lies inside one entry
+// (found once per workgroup through the scalar path), the splits summed in index order with
+// 12 loads in flight per thread
 __global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= t.off[t.n]) return;
   int e = 0;
-  while (i >= t.off[e + 1]) ++e;
+  while ((int)blockIdx.x >= t.boff[e + 1]) ++e;
   const ReduceEntry r = t.e[e];
-  const long long u = i - t.off[e];
+  const long long u = (long long)(blockIdx.x - t.boff[e]) * 256 + threadIdx.x;
+  if (u >= t.off[e + 1] - t.off[e]) return;
   constexpr int U = 12;
   if (r.vec) {
     const size_t j = (size_t)u * 4;
@@ -1124,8 +1126,10 @@ extern "C" int tm_reduce_defer(int on) {
 
 extern "C" int tm_reduce_flush(void* stream) {
   if (g_defer.n == 0) return 0;
-  const long long total = g_defer.off[g_defer.n];
-  multi_reduce_kernel<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(g_defer);
+  g_defer.boff[0] = 0;
+  for (int i = 0; i < g_defer.n; ++i)
+    g_defer.boff[i + 1] = g_defer.boff[i] + (int)((g_defer.off[i + 1] - g_defer.off[i] + 255) / 256);
+  multi_reduce_kernel<<<(unsigned)g_defer.boff[g_defer.n], 256, 0, (hipStream_t)stream>>>(g_defer);
   g_defer.n = 0;
   g_defer.off[0] = 0;
   TM_CHECK_LAUNCH();
