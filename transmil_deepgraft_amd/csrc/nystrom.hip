@@ -77,25 +77,25 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
                                                            float* __restrict__ a2, bf16* __restrict__ a2s) {
   const int bh = blockIdx.x, i0 = blockIdx.y * 16, j = threadIdx.x, lane = j & 63, wave = j >> 6;
   __shared__ float kt[DH][NL + 1];
+  __shared__ float qs[16][DH];
   __shared__ float red[4][16];
   const float* kb = kl + (size_t)bh * NL * DH;
-  // k~ of the head, transposed into LDS with 16-B loads
+  // k~ of the head, transposed into LDS with 16-B loads (q~ rows through LDS as broadcasts: a
+  // scalar-path variant measured 24.7 vs 19.3 us)
   for (int e4 = threadIdx.x; e4 < NL * DH / 4; e4 += 256) {
     const f32x4 v = *(const f32x4*)(kb + 4 * e4);
     const int jj = (4 * e4) / DH, d = (4 * e4) % DH;
     kt[d][jj] = v[0]; kt[d + 1][jj] = v[1]; kt[d + 2][jj] = v[2]; kt[d + 3][jj] = v[3];
   }
+  for (int e = threadIdx.x; e < 16 * DH; e += 256) qs[e / DH][e % DH] = ql[((size_t)bh * NL + i0) * DH + e];
   __syncthreads();
-  // the 16 q~ rows are the same for every lane: read through the scalar path, not LDS
-  const float* qb = ql + ((size_t)bh * NL + i0) * DH;
   float s[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) s[r] = 0.f;
-#pragma unroll 8
   for (int d = 0; d < DH; ++d) {
     const float kv = kt[d][j];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = fmaf(qb[r * DH + d], kv, s[r]);
+    for (int r = 0; r < 16; ++r) s[r] = fmaf(qs[r][d], kv, s[r]);
   }
   // row max
 #pragma unroll
