@@ -22,10 +22,10 @@ def _rel(a, b):
 
 
 # ----------------------------------------------------------------------------- GEMM
-@pytest.fixture(params=[0, 1, 2, 4], ids=["1buf", "2buf", "ring", "persist"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 6, 7], ids=["ring2", "2buf", "ring4", "1buf", "persist", "ring3", "big"])
 def gemm_variant(request):
-    """Every GEMM main loop (register-staged 1 / 2 LDS buffers, per-tile global_load_lds ring,
-    persistent ring)."""
+    """Every GEMM main loop (default 2-stage global_load_lds ring, register-staged 2 / 1 LDS
+    buffers, 4- and 3-stage rings, persistent ring, 256-row big tiles)."""
     from transmil_deepgraft_amd import _lib
     _lib.lib().tm_debug_set_variant(2, request.param)
     yield request.param

@@ -512,7 +512,7 @@ TM_DEV void ring_tile_mma(f32x16 (&acc)[2], unsigned abase, unsigned b0, unsigne
   mma16(acc[1], a[1], b[1][1]);
 }
 
-template <typename OutT, bool A_T, bool B_KN>
+template <typename OutT, bool A_T, bool B_KN, int NS = NSTAGE>
 __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                         OutT* __restrict__ C, tm_gemm_args g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -544,23 +544,23 @@ __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__
   const unsigned ring = lds_u32(smem);
 
   auto issue = [&](int kt) {
-    char* st = smem + (kt % NSTAGE) * STAGE_BYTES;
+    char* st = smem + (kt % NS) * STAGE_BYTES;
     const int k0 = kbeg + kt * 64;
     glds_tile<A_T>(st, A, g.lda, m0, g.M, k0, wave, lane);
     glds_tile<B_KN>(st + STAGE_BYTES / 2, B, g.ldb, n0, g.N, k0, wave, lane);
   };
 #pragma unroll
-  for (int t = 0; t < NSTAGE - 1; ++t)
+  for (int t = 0; t < NS - 1; ++t)
     if (t < nk) issue(t);
 
   for (int kt = 0; kt < nk; ++kt) {
     // this wave's pieces of tile kt have landed once at most (tiles issued after kt) x 4 loads remain
-    const int ahead = min(NSTAGE - 2, nk - 1 - kt);
+    const int ahead = min(NS - 2, nk - 1 - kt);
     if (ahead >= 2) wait_vm<8>(); else if (ahead == 1) wait_vm<4>(); else wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave done reading tile kt-1
     asm volatile("" ::: "memory");
-    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1);  // overwrites tile kt-1's buffer
-    const unsigned sb = ring + (kt % NSTAGE) * STAGE_BYTES;
+    if (kt + NS - 1 < nk) issue(kt + NS - 1);  // overwrites tile kt-1's buffer
+    const unsigned sb = ring + (kt % NS) * STAGE_BYTES;
     ring_tile_mma<A_T, B_KN>(acc, (A_T ? aks : 0) + sb, (B_KN ? bks0 : 0) + sb, (B_KN ? bks1 : 0) + sb,
                              akc, bkc0, bkc1);
   }
@@ -871,15 +871,20 @@ constexpr size_t gemm_smem() {
   return main > epi ? main : epi;
 }
 
-// 0 = big-tile DMA kernel (bf16, where it applies; else the register-staged loop with 1 LDS
-// buffer); 1 = register-staged, 2 LDS buffers; 2 = per-tile 128 x 128 DMA ring; 3 = register-
-// staged, 1 LDS buffer; 4 = persistent 128 x 128 DMA ring (QKV: 34.3 us register-staged, 36.8
-// per-tile ring, 42.6 persistent ring -- the 128-tiles are operand-bandwidth bound)
+// 0 = the 2-stage 128 x 128 DMA ring where it applies (bf16, 64 | K per split), else the
+// register-staged loop with 1 LDS buffer; 1 = register-staged, 2 LDS buffers; 2 = 4-stage ring;
+// 3 = register-staged, 1 LDS buffer; 4 = persistent 128 x 128 DMA ring; 5 = 2-stage ring; 6 =
+// 3-stage ring; 7 = 256 x 256 / 256 x 128 big-tile kernel.  The 2-stage ring (69.6 KB of LDS with
+// its epilogue image) keeps two workgroups per CU, which is what wins on these shapes: at
+// M = 8448 rows 264 tiles of 128 x 128 are a 256-CU wave plus 8 tiles, and the second workgroup
+// on a CU shares its operand intake instead of waiting for a second round (QKV 32.2 vs 36.5 us
+// big-tile; to_out 17.9 vs 21.0 register-staged; dxn 31.1 vs 36.4; fc1 18.3 vs 25.3; weight
+// grads 19.3 / 35.6 / 29.1 vs 21.5 / 39.1 / 38.1; scripts/dev/gemm_shapes.py)
 int g_gemm_variant = 0;
 
 template <typename OutT>
 bool ring_ok(const tm_gemm_args& g) {
-  if (g_gemm_variant != 2 && g_gemm_variant != 4) return false;
+  if (g_gemm_variant != 0 && (g_gemm_variant < 2 || g_gemm_variant > 6 || g_gemm_variant == 3)) return false;
   // whole 64-deep k-tiles in every split; k-strided operands need >= 8 rows/cols (clamped 16-B pieces)
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if ((g.a_trans && g.M < 8) || (g.b_kn && g.N < 8)) return false;
@@ -890,14 +895,11 @@ bool ring_ok(const tm_gemm_args& g) {
 
 template <typename OutT>
 bool big_ok(const tm_gemm_args& g) {
-  if (g_gemm_variant != 0) return false;
+  if (g_gemm_variant != 7) return false;
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if (g.a_trans && (g.M % 8 != 0 || g.M < 8)) return false;
   if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
-  // only where it measured faster: N >= 1024 (the QKV projection, 256 x 256 tiles: 33.1 vs 35.3 us);
-  // the N = 512 shapes on 256 x 128 tiles leave half the CUs idle (to_out / fc1 30.1 vs 27.5,
-  // dmerged ~29 vs 21.6 us) and stay on the register-staged loop
-  return g.M >= 128 && g.N >= 1024;
+  return g.M >= 128 && g.N >= 128;
 }
 
 template <typename T, typename OutT>
@@ -938,11 +940,21 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
     }
     if (ring_ok<OutT>(g)) {
       constexpr size_t epi = (size_t)BM * EP_ROW * sizeof(float);
-      constexpr size_t sm = RING_BYTES > epi ? RING_BYTES : epi;
 #define TM_RING_CASE(AT, BKN)                                                                   \
       if (g.a_trans == AT && g.b_kn == BKN) {                                                   \
-        tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN>, sm);                                     \
-        gemm_ring_kernel<OutT, AT, BKN><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        if (g_gemm_variant == 0 || g_gemm_variant == 5) {                                       \
+          constexpr size_t sm = 2 * STAGE_BYTES > epi ? 2 * STAGE_BYTES : epi;                  \
+          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2>, sm);                                \
+          gemm_ring_kernel<OutT, AT, BKN, 2><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        } else if (g_gemm_variant == 6) {                                                       \
+          constexpr size_t sm = 3 * STAGE_BYTES > epi ? 3 * STAGE_BYTES : epi;                  \
+          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 3>, sm);                                \
+          gemm_ring_kernel<OutT, AT, BKN, 3><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        } else {                                                                                \
+          constexpr size_t sm = RING_BYTES > epi ? RING_BYTES : epi;                            \
+          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN>, sm);                                   \
+          gemm_ring_kernel<OutT, AT, BKN><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        }                                                                                       \
         TM_CHECK_LAUNCH();                                                                      \
         return 0;                                                                               \
       }
