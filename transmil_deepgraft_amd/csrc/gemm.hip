@@ -158,8 +158,10 @@ constexpr int tile_elems() {
 // loads/stores: bias, pre-activation store, GELU, dropout, residual, accumulate, and the
 // TransMIL row maps (grid duplication, QKV head-major scatter, split-K slabs).
 // The caller guarantees every wave is past its last read of the staging buffers.
-template <typename OutT, int TBN = BN>
-TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows,
+// epilogue kinds: 0 any (runtime mode), 1 plain (alpha, bias, store), 2 QKV scatter, 3 split-K slab
+enum { EK_ANY = 0, EK_PLAIN = 1, EK_QKV = 2, EK_SPLITK = 3 };
+template <typename OutT, int TBN, int ROWS, int NT, int KIND = EK_ANY>
+TM_DEV void gemm_epilogue_rows(const char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0,
                                int split = -1);
 
 // accumulator tile (32x32 at rows rb, cols cb of the block tile) -> epilogue image
@@ -185,103 +187,192 @@ TM_DEV void gemm_epilogue(const f32x16 (&acc)[2][2], char* smem, OutT* __restric
         for (int j = 0; j < 2; ++j) stage_acc(ep, acc[i][j], i * 32, wn * 64 + j * 32, lane);
     }
     __syncthreads();
-    gemm_epilogue_rows<OutT>(smem, C, g, m0 + half * 64, n0, 64);
+    gemm_epilogue_rows<OutT, BN, 64, 256>(smem, C, g, m0 + half * 64, n0);
     __syncthreads();
   }
 }
 
-// the chunk phase: every thread of the block walks 8-column row chunks of the staged tile
-// (image rows of TBN + 8 floats)
-template <typename OutT, int TBN>
-TM_DEV void gemm_epilogue_rows(char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0, int rows,
+// the chunk phase: every thread of the block owns IT 8-column row chunks of the staged tile
+// (image rows of TBN + 8 floats), all in the same 8 columns (NT is a multiple of TBN / 8).
+// Rolled loops (`unroll 1`): the epilogue runs once per tile, so its code runs from a cold
+// instruction cache -- unrolled over IT chunks and every mode it was ~5k instructions and took
+// ~8k cycles of a 128 x 128 tile, against ~1.3k for the bare stores (scripts/dev/gemm_epi_probe.py).
+// The addend loads (residual / accumulate source) of chunk it + 1 go out before chunk it's
+// stores: gfx9 counts stores on vmcnt, so a load issued after a store waits for its write-back.
+template <typename OutT, int TBN, int ROWS, int NT, int KIND>
+TM_DEV void gemm_epilogue_rows(const char* smem, OutT* __restrict__ C, const tm_gemm_args& g, int m0, int n0,
                                int split) {
-  constexpr int CPR = TBN / 8, ROWF = TBN + 8;
+  constexpr int CPR = TBN / 8, ROWF = TBN + 8, IT = ROWS * CPR / NT;
+  static_assert(ROWS * CPR % NT == 0 && NT % CPR == 0, "epilogue chunk map");
   const int tid = threadIdx.x;
   const float* ep = (const float*)smem;
-  const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
-  const size_t slab = (size_t)(split < 0 ? (int)blockIdx.z : split) * g.M * g.N;
-  for (int c = tid; c < rows * CPR; c += blockDim.x) {
-    const int lr = c / CPR, lc = (c % CPR) * 8;
-    const int m = m0 + lr, n = n0 + lc;
-    if (m >= g.M || n >= g.N) continue;
-    float v[8];
-    {
-      const f32x4 lo = *(const f32x4*)(ep + lr * ROWF + lc), hi = *(const f32x4*)(ep + lr * ROWF + lc + 4);
-      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-    }
-    const int ne = min(8, g.N - n);  // valid columns in this chunk
-    if (g.mode == TM_EPI_SPLITK) {
+  const int lc = (tid % CPR) * 8, n = n0 + lc, lr0 = tid / CPR;
+  constexpr int LRS = NT / CPR;    // image rows between a thread's chunks
+  const int ne = min(8, g.N - n);  // valid columns of this thread's chunks
+  if (ne <= 0) return;
+  auto chunk = [&](int it, float (&v)[8]) {
+    const int lr = lr0 + it * LRS;
+    const f32x4 lo = *(const f32x4*)(ep + lr * ROWF + lc), hi = *(const f32x4*)(ep + lr * ROWF + lc + 4);
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3]; v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  };
+  if (KIND == EK_SPLITK || (KIND == EK_ANY && g.mode == TM_EPI_SPLITK)) {
+    const size_t slab = (size_t)(split < 0 ? (int)blockIdx.z : split) * g.M * g.N;
+    const bool vec = ne == 8 && g.N % 4 == 0;
+#pragma unroll 1
+    for (int it = 0; it < IT; ++it) {
+      const int m = m0 + lr0 + it * LRS;
+      if (m >= g.M) break;
+      float v[8];
+      chunk(it, v);
       float* dst = (float*)C + slab + (size_t)m * g.N + n;
-      if (ne == 8 && g.N % 4 == 0) {
+      if (vec) {
         *(f32x4*)dst = (f32x4){v[0], v[1], v[2], v[3]};
         *(f32x4*)(dst + 4) = (f32x4){v[4], v[5], v[6], v[7]};
       } else {
         for (int e = 0; e < ne; ++e) dst[e] = v[e];
       }
-      continue;
     }
-    if (g.mode == TM_EPI_QKV) {  // 8 columns never straddle a head (dh % 8 == 0, checked on the host)
+    return;
+  }
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (g.bias) {
+    if (ne == 8 && ((uintptr_t)g.bias & 15) == 0) { const f32x8 t8 = load8<float>(g.bias + n); for (int e = 0; e < 8; ++e) bv[e] = t8[e]; }
+    else { for (int e = 0; e < ne; ++e) bv[e] = g.bias[n + e]; }
+  }
+  if constexpr (KIND == EK_SPLITK) return;
+  if (KIND == EK_QKV || (KIND == EK_ANY && g.mode == TM_EPI_QKV)) {  // 8 columns never straddle a head (dh % 8 == 0, checked on the host)
+    const int inner = g.nh * g.dh;
+    const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
+    const float qs = which == 0 ? g.qscale : 1.f;
+    OutT* base = C + (((long long)which * g.nbags) * g.nh + hh) * g.seq * g.dh + d;
+#pragma unroll 1
+    for (int it = 0; it < IT; ++it) {
+      const int m = m0 + lr0 + it * LRS;
+      if (m >= g.M) break;
       const int bag = m / g.seq, t = m - bag * g.seq;
-      const int inner = g.nh * g.dh;
-      const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
-      OutT* dst = C + (((long long)which * g.nbags + bag) * g.nh + hh) * g.seq * g.dh + (long long)t * g.dh + d;
-      const float qs = which == 0 ? g.qscale : 1.f;
+      OutT* dst = base + (long long)bag * g.nh * g.seq * g.dh + (long long)t * g.dh;
+      float v[8];
+      chunk(it, v);
       vec8<OutT> o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = from_f<OutT>((v[e] * g.alpha + (g.bias ? g.bias[n + e] : 0.f)) * qs);
+      for (int e = 0; e < 8; ++e) o[e] = from_f<OutT>((v[e] * g.alpha + bv[e]) * qs);
       store8<OutT>(dst, o);
-      continue;
     }
-    int row = m, dup_row = -1;
-    if (g.grp_in > 0) {
-      const int bag = m / g.grp_in, t = m - bag * g.grp_in - g.skip;
-      if (t < 0) continue;
-      row = bag * g.grp_out + g.out_off + t;
-      if (t < g.dup_n) dup_row = bag * g.grp_out + g.dup_off + t;
-    }
-    const size_t off = (size_t)row * g.ldc + n;
-    const bool vec = ne == 8 && g.ldc % 8 == 0 && (!g.pre || g.ld_pre % 8 == 0);
-    float bv[8], rv[8], cv[8];
-    if (vec) {
-      if (g.bias) { const f32x8 t8 = load8<float>(g.bias + n); for (int e = 0; e < 8; ++e) bv[e] = t8[e]; }
-      if (g.resid) { const f32x8 t8 = load8<float>(g.resid + off); for (int e = 0; e < 8; ++e) rv[e] = t8[e]; }
-      if (g.accumulate) { const vec8<OutT> t8 = load8<OutT>(C + off); for (int e = 0; e < 8; ++e) cv[e] = to_f(t8[e]); }
-    } else {
-      for (int e = 0; e < ne; ++e) {
-        bv[e] = g.bias ? g.bias[n + e] : 0.f;
-        rv[e] = g.resid ? g.resid[off + e] : 0.f;
-        cv[e] = g.accumulate ? to_f(C[off + e]) : 0.f;
-      }
-    }
-    vec8<OutT> pre8, out8;
+    return;
+  }
+  if constexpr (KIND == EK_QKV) return;
+  if constexpr (KIND == EK_PLAIN) {  // no row map, pre-activation, GELU, dropout or addend
+    const bool pvec = ne == 8 && g.ldc % 8 == 0;
+#pragma unroll 1
+    for (int it = 0; it < IT; ++it) {
+      const int m = m0 + lr0 + it * LRS;
+      if (m >= g.M) break;
+      float v[8];
+      chunk(it, v);
+      vec8<OutT> o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float x = v[e] * g.alpha + (g.bias ? bv[e] : 0.f);
-      pre8[e] = from_f<OutT>(x);
-      if (g.gelu) x = gelu_erf(x);
-      if (g.drop_p > 0.f) {
-        const float u = dropout_u01(seed, (uint32_t)row, (uint32_t)(n + e));
-        x = (u >= g.drop_p) ? x * g.drop_scale : 0.f;
-      }
-      if (g.resid) x += rv[e];
-      if (g.accumulate) x += cv[e];
-      out8[e] = from_f<OutT>(x);
+      for (int e = 0; e < 8; ++e) o[e] = from_f<OutT>(v[e] * g.alpha + bv[e]);
+      OutT* dst = C + (size_t)m * g.ldc + n;
+      if (pvec) store8<OutT>(dst, o);
+      else { for (int e = 0; e < ne; ++e) dst[e] = o[e]; }
     }
-    if (vec) {
-      if (g.pre) store8<OutT>((OutT*)g.pre + (size_t)m * g.ld_pre + n, pre8);
-      store8<OutT>(C + off, out8);
-      if (dup_row >= 0) store8<OutT>(C + (size_t)dup_row * g.ldc + n, out8);
-    } else {
-      for (int e = 0; e < ne; ++e) {
-        if (g.pre) ((OutT*)g.pre)[(size_t)m * g.ld_pre + n + e] = pre8[e];
-        C[off + e] = out8[e];
-        if (dup_row >= 0) C[(size_t)dup_row * g.ldc + n + e] = out8[e];
+    return;
+  }
+  const bool vec = ne == 8 && g.ldc % 8 == 0 && (!g.pre || g.ld_pre % 8 == 0);
+  // output row of chunk it (TransMIL grid duplication / padding skip), -1: none
+  auto out_row = [&](int it, int& dup) {
+    const int m = m0 + lr0 + it * LRS;
+    dup = -1;
+    if (m >= g.M) return -1;
+    if (g.grp_in <= 0) return m;
+    const int bag = m / g.grp_in, t = m - bag * g.grp_in - g.skip;
+    if (t < 0) return -1;
+    if (t < g.dup_n) dup = bag * g.grp_out + g.dup_off + t;
+    return bag * g.grp_out + g.out_off + t;
+  };
+  // the addend (residual, or without one the accumulate source); with both (no caller does)
+  // the accumulate source is read at the store
+  const float* rsrc = g.resid;
+  const OutT* asrc = (g.accumulate && !g.resid) ? C : nullptr;
+  const bool acc_late = g.accumulate && g.resid;
+  auto load_add = [&](int it, float (&a)[8]) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = 0.f;
+    int dd;
+    const int row = out_row(it, dd);
+    if (row < 0) return;
+    const size_t off = (size_t)row * g.ldc + n;
+    if (rsrc) {
+      if (vec) { const f32x8 t8 = load8<float>(rsrc + off); for (int e = 0; e < 8; ++e) a[e] = t8[e]; }
+      else { for (int e = 0; e < ne; ++e) a[e] = rsrc[off + e]; }
+    } else if (asrc) {
+      if (vec) { const vec8<OutT> t8 = load8<OutT>(asrc + off); for (int e = 0; e < 8; ++e) a[e] = to_f(t8[e]); }
+      else { for (int e = 0; e < ne; ++e) a[e] = to_f(asrc[off + e]); }
+    }
+  };
+  const bool has_add = rsrc || asrc;
+  const uint64_t seed = g.drop_p > 0.f ? effective_seed(g.seed, g.seed_ptr) : 0;
+  float av[8];
+  if (has_add) load_add(0, av);
+#pragma unroll 1
+  for (int it = 0; it < IT; ++it) {
+    float an[8];
+    if (has_add && it + 1 < IT) load_add(it + 1, an);
+    int dup;
+    const int row = out_row(it, dup);
+    if (row >= 0) {
+      const size_t off = (size_t)row * g.ldc + n;
+      const int m = m0 + lr0 + it * LRS;
+      float v[8];
+      chunk(it, v);
+      // one uniform branch per feature per chunk (a branch per element made this loop
+      // VALU-bound: ~7k cycles per tile at four waves per SIMD)
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = v[e] * g.alpha + bv[e];
+      vec8<OutT> pre8, out8;
+      if (g.pre) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pre8[e] = from_f<OutT>(x[e]);
       }
+      if (g.gelu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+      }
+      if (g.drop_p > 0.f) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float u = dropout_u01(seed, (uint32_t)row, (uint32_t)(n + e));
+          x[e] = (u >= g.drop_p) ? x[e] * g.drop_scale : 0.f;
+        }
+      }
+      if (has_add) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] += av[e];
+      }
+      if (acc_late) {
+        for (int e = 0; e < ne; ++e) x[e] += to_f(C[off + e]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out8[e] = from_f<OutT>(x[e]);
+      if (vec) {
+        if (g.pre) store8<OutT>((OutT*)g.pre + (size_t)m * g.ld_pre + n, pre8);
+        store8<OutT>(C + off, out8);
+        if (dup >= 0) store8<OutT>(C + (size_t)dup * g.ldc + n, out8);
+      } else {
+        for (int e = 0; e < ne; ++e) {
+          if (g.pre) ((OutT*)g.pre)[(size_t)m * g.ld_pre + n + e] = pre8[e];
+          C[off + e] = out8[e];
+          if (dup >= 0) C[(size_t)dup * g.ldc + n + e] = out8[e];
+        }
+      }
+    }
+    if (has_add) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) av[e] = an[e];
     }
   }
 }
-
-
 
 // XCD-aware tile order: blocks are dealt round-robin over the 8 XCDs, so renumber them
 // so that each XCD gets a contiguous run of row-major tiles (its row panels of A stay in
@@ -512,10 +603,29 @@ TM_DEV void ring_tile_mma(f32x16 (&acc)[2], unsigned abase, unsigned b0, unsigne
   mma16(acc[1], a[1], b[1][1]);
 }
 
-template <typename OutT, bool A_T, bool B_KN, int NS = NSTAGE>
-__global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+// diagnostics (variant 8 only): per-workgroup shader-clock stamps of the ring kernel, read by
+// tm_debug_gemm_stamps: [block][8] = realtime start, t start, first tile landed, k-loop done,
+// accumulators staged, epilogue stores issued, stores retired, realtime end
+__device__ unsigned long long g_gemm_stamps[2048 * 8];
+template <bool ON>
+TM_DEV void ring_stamp(unsigned long long (&ts)[8], int slot, bool real = false) {
+  if constexpr (ON) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    if (real) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    else asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    ts[slot] = t;
+  }
+}
+
+template <typename OutT, bool A_T, bool B_KN, int NS = NSTAGE, bool STAMP = false, int KIND = EK_ANY>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void gemm_ring_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                         OutT* __restrict__ C, tm_gemm_args g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  ring_stamp<STAMP>(ts, 0, true);
+  ring_stamp<STAMP>(ts, 1);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;  // 4 (M) x 2 (N) waves of 32 x 64
@@ -559,17 +669,52 @@ __global__ __launch_bounds__(512) void gemm_ring_kernel(const bf16* __restrict__
     if (ahead >= 2) wait_vm<8>(); else if (ahead == 1) wait_vm<4>(); else wait_vm<0>();
     __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave done reading tile kt-1
     asm volatile("" ::: "memory");
+    if (STAMP && kt == 0) ring_stamp<STAMP>(ts, 2);
     if (kt + NS - 1 < nk) issue(kt + NS - 1);  // overwrites tile kt-1's buffer
     const unsigned sb = ring + (kt % NS) * STAGE_BYTES;
     ring_tile_mma<A_T, B_KN>(acc, (A_T ? aks : 0) + sb, (B_KN ? bks0 : 0) + sb, (B_KN ? bks1 : 0) + sb,
                              akc, bkc0, bkc1);
   }
+  ring_stamp<STAMP>(ts, 3);
   __syncthreads();  // all fragment reads done before the epilogue reuses the ring
   float* ep = (float*)smem;
 #pragma unroll
   for (int j = 0; j < 2; ++j) stage_acc(ep, acc[j], wm * 32, wn * 64 + j * 32, lane);
   __syncthreads();
-  gemm_epilogue_rows<OutT>(smem, C, g, m0, n0, BM);
+  ring_stamp<STAMP>(ts, 4);
+  if (STAMP && g.drop_scale < 0.f) {
+    // diagnostics: image reads only, no global stores (drop_scale -1) or plain bf16/f32 stores of
+    // the image with no other epilogue work (drop_scale -2)
+    const float* ep2 = (const float*)smem;
+    for (int c = tid; c < BM * 16; c += 512) {
+      const int lr = c / 16, lc = (c % 16) * 8;
+      const f32x4 lo = *(const f32x4*)(ep2 + lr * EP_ROW + lc), hi = *(const f32x4*)(ep2 + lr * EP_ROW + lc + 4);
+      if (g.drop_scale < -1.5f) {
+        OutT* dst = C + (size_t)(m0 + lr) * g.ldc + n0 + lc;
+        if (m0 + lr < g.M) {
+          vec8<OutT> o;
+          for (int e = 0; e < 4; ++e) { o[e] = from_f<OutT>(lo[e]); o[e + 4] = from_f<OutT>(hi[e]); }
+          store8<OutT>(dst, o);
+        }
+      } else {
+        asm volatile("" ::"v"(lo), "v"(hi));
+      }
+    }
+  } else
+  gemm_epilogue_rows<OutT, BN, BM, 512, KIND>(smem, C, g, m0, n0);
+  if constexpr (STAMP) {
+    ring_stamp<STAMP>(ts, 5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ring_stamp<STAMP>(ts, 6);
+    ring_stamp<STAMP>(ts, 7, true);
+    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    if (tid < 8 && blk < 2048) {
+      unsigned long long v = ts[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) v = tid == i ? ts[i] : v;
+      g_gemm_stamps[blk * 8 + tid] = v;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -671,7 +816,7 @@ __global__ __launch_bounds__(512) void gemm_persist_kernel(const bf16* __restric
           for (int j = 0; j < 2; ++j) stage_acc((float*)epi, acc[j], (wm & 1) * 32, wn * 64 + j * 32, lane);
         }
         __syncthreads();
-        gemm_epilogue_rows<OutT>(epi, C, g, cs.m0 + half * 64, cs.n0, 64, cs.split);
+        gemm_epilogue_rows<OutT, BN, 64, 512>(epi, C, g, cs.m0 + half * 64, cs.n0, cs.split);
         __syncthreads();
       }
       wait_vm<0>();   // the epilogue's own loads / stores (their count is data dependent)
@@ -852,7 +997,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(const bf16* __restrict__ 
       }
     }
     __syncthreads();
-    gemm_epilogue_rows<OutT, TBN>((char*)smem, C, g, m0 + qtr * 64, n0, 64);
+    gemm_epilogue_rows<OutT, TBN, 64, 512>((char*)smem, C, g, m0 + qtr * 64, n0);
     __syncthreads();
   }
 }
@@ -882,9 +1027,17 @@ constexpr size_t gemm_smem() {
 // grads 19.3 / 35.6 / 29.1 vs 21.5 / 39.1 / 38.1; scripts/dev/gemm_shapes.py)
 int g_gemm_variant = 0;
 
+// the specialised epilogue a launch can use (EK_ANY keeps the runtime-mode one)
+inline int epilogue_kind(const tm_gemm_args& g) {
+  if (g.mode == TM_EPI_SPLITK) return EK_SPLITK;
+  if (g.mode == TM_EPI_QKV) return EK_QKV;
+  if (!g.pre && !g.gelu && g.drop_p <= 0.f && !g.resid && !g.accumulate && g.grp_in <= 0) return EK_PLAIN;
+  return EK_ANY;
+}
+
 template <typename OutT>
 bool ring_ok(const tm_gemm_args& g) {
-  if (g_gemm_variant != 0 && (g_gemm_variant < 2 || g_gemm_variant > 6 || g_gemm_variant == 3)) return false;
+  if (g_gemm_variant != 0 && g_gemm_variant != 8 && (g_gemm_variant < 2 || g_gemm_variant > 6 || g_gemm_variant == 3)) return false;
   // whole 64-deep k-tiles in every split; k-strided operands need >= 8 rows/cols (clamped 16-B pieces)
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if ((g.a_trans && g.M < 8) || (g.b_kn && g.N < 8)) return false;
@@ -944,8 +1097,24 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
       if (g.a_trans == AT && g.b_kn == BKN) {                                                   \
         if (g_gemm_variant == 0 || g_gemm_variant == 5) {                                       \
           constexpr size_t sm = 2 * STAGE_BYTES > epi ? 2 * STAGE_BYTES : epi;                  \
-          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2>, sm);                                \
-          gemm_ring_kernel<OutT, AT, BKN, 2><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+          const int kind = epilogue_kind(g);                                                    \
+          if (kind == EK_PLAIN) {                                                               \
+            tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2, false, EK_PLAIN>, sm);             \
+            gemm_ring_kernel<OutT, AT, BKN, 2, false, EK_PLAIN><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+          } else if (kind == EK_QKV) {                                                          \
+            tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2, false, EK_QKV>, sm);               \
+            gemm_ring_kernel<OutT, AT, BKN, 2, false, EK_QKV><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+          } else if (kind == EK_SPLITK) {                                                       \
+            tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2, false, EK_SPLITK>, sm);            \
+            gemm_ring_kernel<OutT, AT, BKN, 2, false, EK_SPLITK><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+          } else {                                                                              \
+            tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2>, sm);                              \
+            gemm_ring_kernel<OutT, AT, BKN, 2><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+          }                                                                                     \
+        } else if (g_gemm_variant == 8) {                                                       \
+          constexpr size_t sm = 2 * STAGE_BYTES > epi ? 2 * STAGE_BYTES : epi;                  \
+          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2, true>, sm);                          \
+          gemm_ring_kernel<OutT, AT, BKN, 2, true><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
         } else if (g_gemm_variant == 6) {                                                       \
           constexpr size_t sm = 3 * STAGE_BYTES > epi ? 3 * STAGE_BYTES : epi;                  \
           tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 3>, sm);                                \
@@ -1068,6 +1237,16 @@ extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args
 }
 
 extern "C" void tm_debug_set_gemm_variant(int value) { g_gemm_variant = value; }
+
+// copy the variant-8 ring stamps ([block][8] u64) to a host buffer (diagnostics only)
+extern "C" int tm_debug_gemm_stamps(unsigned long long* host, int count) {
+  TM_REQUIRE(count > 0 && count <= 2048 * 8, "gemm_stamps: bad count");
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gemm_stamps), count * sizeof(unsigned long long)) != hipSuccess) {
+    tm_set_error("gemm_stamps: copy");
+    return 1;
+  }
+  return 0;
+}
 
 // ---- deferred reductions: the parameter-gradient slab sums of a backward, queued while the
 // engine has deferral on and summed by ONE launch at tm_reduce_flush (a kernel boundary costs
