@@ -424,3 +424,62 @@ def test_a1_fwd_bf16_kernels(nbh, n):
         assert (lse.cpu().double() - ref_l).abs().max().item() < 1e-4, variant
         outs.append(merged.cpu().float())
     assert _rel(outs[0], outs[1].double()) < 2e-2
+
+
+# ----------------------------------------------------------------------------- conv33 backward
+def _conv_bwd_ref(dO, O, v, wconv, nh):
+    """fp64: dv = conv33^T(dO), c_tau(t) = dO[t].v[t + tau - 16], D1 = dO.O - sum_tau w c_tau,
+    dw[head][tau] = sum over bags and rows of c_tau."""
+    nbags, n, _ = dO.shape
+    nbh = nbags * nh
+    g = dO.double().view(nbags, n, nh, 64).permute(0, 2, 1, 3).reshape(nbh, n, 64)
+    o = O.double().view(nbags, n, nh, 64).permute(0, 2, 1, 3).reshape(nbh, n, 64)
+    vv = v.double()
+    w = wconv.double().view(nh, 33)[torch.arange(nbh) % nh]          # [nbh, 33]
+    gp = torch.nn.functional.pad(g, (0, 0, 16, 16))
+    vp = torch.nn.functional.pad(vv, (0, 0, 16, 16))
+    dv = torch.zeros_like(vv)
+    c = torch.zeros(nbh, n, 33, dtype=torch.float64)
+    for tau in range(33):
+        dv += w[:, tau].view(nbh, 1, 1) * gp[:, 32 - tau:32 - tau + n]
+        c[:, :, tau] = (g * vp[:, tau:tau + n]).sum(-1)
+    d1 = (g * o).sum(-1) - (c * w.view(nbh, 1, 33)).sum(-1)
+    dw = c.sum(1).view(nbags, nh, 33).sum(0)
+    return dv, d1, dw
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbags,n", [(1, 100), (1, 8448), (2, 1000), (4, 300)])
+def test_conv_bwd_bf16_mfma(nbags, n):
+    """The MFMA conv33 backward (bf16 mode) and the fp32-LDS kernel (variant 7) against fp64."""
+    L = _lib()
+    from transmil_deepgraft_amd._lib import BF16
+    from transmil_deepgraft_amd.engine import _p, _stream
+    nh = 8
+    nbh = nbags * nh
+    g = torch.Generator(device="cpu").manual_seed(n * 7 + nbags)
+    dO = (torch.randn(nbags, n, nh * 64, generator=g) * 0.5).to(torch.bfloat16)
+    O = torch.randn(nbags, n, nh * 64, generator=g).to(torch.bfloat16)
+    v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16)
+    wconv = torch.randn(nh, 33, generator=g) * 0.1
+    ref_dv, ref_d1, ref_dw = _conv_bwd_ref(dO, O, v, wconv, nh)
+    outs = []
+    for variant in (0, 7):
+        L.lib().tm_debug_set_variant(1, variant)
+        try:
+            dv = torch.full((nbh, n, 64), float("nan"), device=DEV)
+            d1 = torch.full((nbh, n), float("nan"), device=DEV)
+            dw = torch.full((nh * 33,), float("nan"), device=DEV)
+            work = torch.empty(L.query("tm_nys_conv_bwd_workspace", nbags, nh, n) // 4 + 16, device=DEV)
+            dOd, Od, vd, wd = (t.to(DEV).contiguous() for t in (dO, O, v, wconv))
+            L.call("tm_nys_conv_bwd", BF16, _p(dOd), _p(Od), _p(vd), _p(wd), nbh, nh, n, _p(dv), _p(d1), _p(work),
+                   _p(dw), _stream())
+            torch.cuda.synchronize()
+        finally:
+            L.lib().tm_debug_set_variant(1, 0)
+        assert torch.isfinite(dv).all() and torch.isfinite(d1).all() and torch.isfinite(dw).all(), variant
+        assert _rel(dv.cpu(), ref_dv) < 1e-5, variant
+        assert (d1.cpu().double() - ref_d1).abs().max().item() < 1e-3 * ref_d1.abs().max().item(), variant
+        assert _rel(dw.cpu().view(nh, 33), ref_dw) < 1e-5, variant
+        outs.append(dv.cpu())
+    assert _rel(outs[0], outs[1].double()) < 1e-5

@@ -896,6 +896,185 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_kernel(const T* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// bf16 conv33 backward on the MFMA.  One workgroup = one head x R rows, R = n * nbh / 256
+// rounded up to 8 (<= 288): 256 workgroups at N = 8192 (the fp32-LDS kernel above runs 1056
+// workgroups of 64 rows, three rounds deep, bound by its LDS reads: 30 us).  Windows of 320
+// rows (t0 - 16 ..) of dO and v as bf16 row-major LDS images; per 32-row tile i (wave w takes
+// tiles w, w + 8):
+//   S  = dO[tile] v_win[32i .. 32i + 63]^T (2 MFMA tiles, K = 64)  ->  c_tau(t) = S[r][r + tau]
+//   dv = Toep(w) dO_win[32i .. 32i + 63],  Toep[r][k] = w[r + 32 - k]  (w as bf16 hi + lo, so
+//        the taps keep ~16 bits; the products of bf16 operands are exact in the fp32 sums)
+constexpr int CB_ROWS = 288, CB_WIN = CB_ROWS + 2 * HALF, CB_ROW = DH + 8, CB_ST = 66;
+struct CbLay {
+  static constexpr size_t DO_OFF = 0;
+  static constexpr size_t V_OFF = DO_OFF + (size_t)CB_WIN * CB_ROW * 2;
+  static constexpr size_t ST_OFF = V_OFF + (size_t)CB_WIN * CB_ROW * 2;  // [8 waves][32][66] fp32
+  static constexpr size_t W_OFF = ST_OFF + 8 * 32 * CB_ST * 4;            // taps fp32
+  static constexpr size_t CS_OFF = W_OFF + 64 * 4;                        // [8 waves][36] tap sums
+  static constexpr size_t BYTES = CS_OFF + 8 * 36 * 4;                    // 161152
+};
+
+// rows per workgroup of the bf16 conv backward (256 workgroups over all heads when possible)
+inline int conv_bwd_rows(int nbh, int n) {
+  const long long want = ((long long)n * nbh + 255) / 256;
+  const int r = (int)((want + 7) / 8 * 8);
+  return r < 32 ? 32 : (r > CB_ROWS ? CB_ROWS : r);
+}
+
+// standard B fragment (lane: col = mb + (lane & 31), k = kb + 8 (lane >> 5) + j) of a row-major
+// [k][ldr] bf16 LDS image, by two transposing reads
+TM_DEV bf16x8 frag_tr_rows(const bf16* S, int ldr, int mb, int kb, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int m = mb + (g & 1) * 16 + 4 * p;
+  const int k = kb + 8 * (g >> 1) + q;
+  typedef __attribute__((address_space(3))) bf16x4 lds_v4;
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(S + k * ldr + m));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(S + (k + 4) * ldr + m));
+  return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__global__ __launch_bounds__(512) void conv_bwd_mfma_kernel(const bf16* __restrict__ dmerged,
+                                                            const bf16* __restrict__ merged,
+                                                            const bf16* __restrict__ v,
+                                                            const float* __restrict__ wconv, int n, int nh, int R,
+                                                            float* __restrict__ dv, float* __restrict__ d1,
+                                                            float* __restrict__ dw_part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16* dos = (bf16*)(smem + CbLay::DO_OFF);
+  bf16* vws = (bf16*)(smem + CbLay::V_OFF);
+  float* ws = (float*)(smem + CbLay::W_OFF);
+  float* csum = (float*)(smem + CbLay::CS_OFF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r32 = lane & 31, h = lane >> 5;
+  const int bh = blockIdx.y, blk = blockIdx.x, nblk = gridDim.x;
+  const int head = bh % nh, bag = bh / nh, ld = nh * DH;
+  const int t0 = blk * R;
+  const int rows = min(R, n - t0);
+  const bf16* dob = dmerged + (size_t)bag * n * ld + head * DH;
+  const bf16* ob = merged + (size_t)bag * n * ld + head * DH;
+  const bf16* vb = v + (size_t)bh * n * DH;
+  // the two windows in one burst (rows past what the block's tiles read stay zero)
+  constexpr int PW = CB_WIN * 8 / 512;
+  bf16x8 ca[PW], cb[PW];
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    const int i = tid + 512 * j, w = i >> 3, d0 = (i & 7) * 8, t = t0 - HALF + w;
+    const bool ok = t >= 0 && t < n && w < rows + 2 * HALF;
+    const int tc = ok ? t : 0;
+    ca[j] = load8(dob + (size_t)tc * ld + d0);
+    cb[j] = load8(vb + (size_t)tc * DH + d0);
+    if (!ok) { ca[j] = (bf16x8){}; cb[j] = (bf16x8){}; }
+  }
+  if (tid < TAPS) ws[tid] = wconv[head * TAPS + tid];
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    const int i = tid + 512 * j, w = i >> 3, d0 = (i & 7) * 8;
+    *(bf16x8*)(dos + w * CB_ROW + d0) = ca[j];
+    *(bf16x8*)(vws + w * CB_ROW + d0) = cb[j];
+  }
+  __syncthreads();
+  // Toeplitz A fragments (the same for every tile): lane row r32, k = 16 s + 8 h + j
+  bf16x8 th[4], tl[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tau = r32 + 32 - (16 * st + 8 * h + j);
+      const float wv = (tau >= 0 && tau < TAPS) ? ws[tau] : 0.f;
+      const bf16 hi = (bf16)wv;
+      th[st][j] = hi;
+      tl[st][j] = (bf16)(wv - (float)hi);
+    }
+  }
+  float* stg = (float*)(smem + CbLay::ST_OFF) + wave * 32 * CB_ST;
+  constexpr int NTK = (TAPS + 1) / 2;  // taps per lane: tau = h + 2k (17)
+  float csl[NTK];
+#pragma unroll
+  for (int k = 0; k < NTK; ++k) csl[k] = 0.f;
+  const int ntile = (rows + 31) / 32;
+#pragma unroll 1
+  for (int i = wave; i < ntile; i += 8) {
+    // S = dO[tile] . v_win[32i .. 32i + 63]^T
+    f32x16 sa = (f32x16){}, sb = (f32x16){};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const bf16x8 a = *(const bf16x8*)(dos + (32 * i + HALF + r32) * CB_ROW + 16 * st + 8 * h);
+      const bf16x8 ba = *(const bf16x8*)(vws + (32 * i + r32) * CB_ROW + 16 * st + 8 * h);
+      const bf16x8 bb = *(const bf16x8*)(vws + (32 * i + 32 + r32) * CB_ROW + 16 * st + 8 * h);
+      mma16(sa, a, ba);
+      mma16(sb, a, bb);
+    }
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = acc_row(reg, h);
+      stg[row * CB_ST + r32] = sa[reg];
+      stg[row * CB_ST + 32 + r32] = sb[reg];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // band: lane (row r32, taps h + 2k); the row's dO . O over d 32h .. 32h + 31
+    const int lr = 32 * i + r32;
+    const bool rv = lr < rows;
+    float wc = 0.f, dd = 0.f;
+#pragma unroll
+    for (int k = 0; k < NTK; ++k) {
+      const int tau = h + 2 * k;
+      if (tau < TAPS) {
+        const float c = stg[r32 * CB_ST + r32 + tau];
+        if (rv) { csl[k] += c; wc = fmaf(ws[tau], c, wc); }
+      }
+    }
+    if (rv) {
+      const bf16* orow = ob + (size_t)(t0 + lr) * ld + 32 * h;
+      const bf16* grow = dos + (lr + HALF) * CB_ROW + 32 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bf16x8 o8 = load8(orow + 8 * q), g8 = *(const bf16x8*)(grow + 8 * q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dd = fmaf((float)g8[e], (float)o8[e], dd);
+      }
+    }
+    float tot = dd - wc;
+    tot += __shfl_xor(tot, 32, 64);
+    if (rv && h == 0) d1[(size_t)bh * n + t0 + lr] = tot;
+    // dv tile = Toep . dO_win[32i .. 32i + 63]
+    const bf16* dwin = dos + 32 * i * CB_ROW;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      f32x16 acc = (f32x16){};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const bf16x8 b = frag_tr_rows(dwin, CB_ROW, dt * 32, 16 * st, lane);
+        mma16(acc, th[st], b);
+        mma16(acc, tl[st], b);
+      }
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int l2 = 32 * i + acc_row(reg, h);
+        if (l2 < rows) dv[((size_t)bh * n + t0 + l2) * DH + dt * 32 + r32] = acc[reg];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();   // the stage is rewritten by the wave's next tile
+  }
+  // tap sums: over the 32 rows of each lane half, then over the waves in a fixed order
+#pragma unroll
+  for (int k = 0; k < NTK; ++k) {
+    float x = csl[k];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) x += __shfl_xor(x, o, 64);
+    const int tau = h + 2 * k;
+    if (r32 == 0 && tau < TAPS) csum[wave * 36 + tau] = x;
+  }
+  __syncthreads();
+  if (tid < TAPS) {
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) sum += csum[w * 36 + tid];
+    dw_part[((size_t)bag * nblk + blk) * (nh * TAPS) + head * TAPS + tid] = sum;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Flash-style backward shared by both attention products.  A workgroup owns a
 // block of 256 keys (4 waves x 64, key on the MFMA lane) and walks query chunks
 // of 32.  With P = exp(Q K^T - lse), dS = P (dO V^T - D):
@@ -1564,15 +1743,25 @@ extern "C" int tm_cast_f32(int dtype, const float* x, void* y, long long count, 
 }
 
 extern "C" long long tm_nys_conv_bwd_workspace(int nbags, int nh, int n) {
-  return (long long)nbags * ((n + 63) / 64) * nh * TAPS * (long long)sizeof(float);
+  const int r = conv_bwd_rows(nbags * nh, n);
+  const long long blocks = std::max((n + 63) / 64, (n + r - 1) / r);
+  return (long long)nbags * blocks * nh * TAPS * (long long)sizeof(float);
 }
 
 extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merged, const void* v, const float* wconv,
                                int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv,
                                void* stream) {
   TM_REQUIRE(nbh % nh == 0 && n > 0, "conv_bwd: bad shape");
-  const int ntb = (n + 63) / 64;
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == TM_BF16 && g_nys_variant != 7) {
+    const int r = conv_bwd_rows(nbh, n), nblk = (n + r - 1) / r;
+    tm_allow_smem(conv_bwd_mfma_kernel, CbLay::BYTES);
+    conv_bwd_mfma_kernel<<<dim3(nblk, nbh), 512, CbLay::BYTES, st>>>(
+        (const bf16*)dmerged, (const bf16*)merged, (const bf16*)v, wconv, n, nh, r, dv, d1, work);
+    TM_CHECK_LAUNCH();
+    return tm_splitk_reduce(work, dwconv, (nbh / nh) * nblk, (long long)nh * TAPS, 1.0f, 0, stream);
+  }
+  const int ntb = (n + 63) / 64;
   TM_DTYPE_DISPATCH(dtype, (conv_bwd_kernel<T><<<dim3(ntb, nbh), 256, 0, st>>>(
                                (const T*)dmerged, (const T*)merged, (const T*)v, wconv, n, nh, dv, d1, work)));
   TM_CHECK_LAUNCH();
