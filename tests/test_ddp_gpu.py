@@ -70,8 +70,10 @@ def test_rccl_allreduce_inside_captured_graph(overlap):
     replayed, against the same steps run eagerly without any collective."""
     import torch.distributed as dist
     from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
+    import gc
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                             device_id=torch.device("cuda", torch.cuda.current_device()))
+    graph = ar = None
     try:
         a, b = _model(3), _model(3)
         ta, tb = TransMILTask(a), TransMILTask(b)
@@ -114,4 +116,10 @@ def test_rccl_allreduce_inside_captured_graph(overlap):
         for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
             torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6, msg=n)
     finally:
+        # the captured graph holds the communicator's kernels and the hook's work handles:
+        # release both (and drain the device) before the communicator is destroyed
+        torch.cuda.synchronize()
+        graph = ar = None
+        gc.collect()
+        torch.cuda.synchronize()
         dist.destroy_process_group()

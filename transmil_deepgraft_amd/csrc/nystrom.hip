@@ -70,53 +70,58 @@ __global__ void landmarks_kernel(const T* __restrict__ q, const T* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// A2 = softmax_j(ql_i . kl_j), fp32 FMA.  grid (nbh, 16), block 256: 16 rows per block, thread = column j.
+// A2 = softmax_j(ql_i . kl_j), fp32 FMA.  grid (nbh, 256 / S2_ROWS), block 256: S2_ROWS rows per
+// block, thread = column j, which keeps row j of k~ (64 floats) in registers; the q~ rows are LDS
+// broadcasts.  (256 blocks: the 16-row version ran 128 blocks that each transposed all of k~
+// through LDS with scalar writes, 19-21 us.)
 // a2s (optional): the same values as bf16 hi / lo planes (hi = bf16(a), lo = bf16(a - hi); lo plane at
 // a2s + nbh * 256 * 256), the operand format of the split pseudo-inverse chain (pinv_split.hip).
+constexpr int S2_ROWS = 8;
 __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restrict__ ql, const float* __restrict__ kl,
                                                            float* __restrict__ a2, bf16* __restrict__ a2s) {
-  const int bh = blockIdx.x, i0 = blockIdx.y * 16, j = threadIdx.x, lane = j & 63, wave = j >> 6;
-  __shared__ float kt[DH][NL + 1];
-  __shared__ float qs[16][DH];
-  __shared__ float red[4][16];
-  const float* kb = kl + (size_t)bh * NL * DH;
-  // k~ of the head, transposed into LDS with 16-B loads (q~ rows through LDS as broadcasts: a
-  // scalar-path variant measured 24.7 vs 19.3 us)
-  for (int e4 = threadIdx.x; e4 < NL * DH / 4; e4 += 256) {
-    const f32x4 v = *(const f32x4*)(kb + 4 * e4);
-    const int jj = (4 * e4) / DH, d = (4 * e4) % DH;
-    kt[d][jj] = v[0]; kt[d + 1][jj] = v[1]; kt[d + 2][jj] = v[2]; kt[d + 3][jj] = v[3];
-  }
-  for (int e = threadIdx.x; e < 16 * DH; e += 256) qs[e / DH][e % DH] = ql[((size_t)bh * NL + i0) * DH + e];
+  const int bh = blockIdx.x, i0 = blockIdx.y * S2_ROWS, j = threadIdx.x, lane = j & 63, wave = j >> 6;
+  __shared__ float qs[S2_ROWS][DH];
+  __shared__ float red[4][S2_ROWS];
+  const float* krow = kl + ((size_t)bh * NL + j) * DH;
+  f32x4 kr[DH / 4];
+#pragma unroll
+  for (int c = 0; c < DH / 4; ++c) kr[c] = *(const f32x4*)(krow + 4 * c);
+  for (int e = threadIdx.x; e < S2_ROWS * DH; e += 256) qs[e / DH][e % DH] = ql[((size_t)bh * NL + i0) * DH + e];
   __syncthreads();
-  float s[16];
+  float s[S2_ROWS];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) s[r] = 0.f;
-  for (int d = 0; d < DH; ++d) {
-    const float kv = kt[d][j];
+  for (int r = 0; r < S2_ROWS; ++r) s[r] = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = fmaf(qs[r][d], kv, s[r]);
+  for (int c = 0; c < DH / 4; ++c) {
+#pragma unroll
+    for (int r = 0; r < S2_ROWS; ++r) {
+      const f32x4 q4 = *(const f32x4*)&qs[r][4 * c];
+      s[r] = fmaf(q4[0], kr[c][0], s[r]);
+      s[r] = fmaf(q4[1], kr[c][1], s[r]);
+      s[r] = fmaf(q4[2], kr[c][2], s[r]);
+      s[r] = fmaf(q4[3], kr[c][3], s[r]);
+    }
   }
   // row max
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < S2_ROWS; ++r) {
     const float m = wave_max(s[r]);
     if (lane == 0) red[wave][r] = m;
   }
   __syncthreads();
-  float mx[16];
+  float mx[S2_ROWS];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) mx[r] = fmaxf(fmaxf(red[0][r], red[1][r]), fmaxf(red[2][r], red[3][r]));
+  for (int r = 0; r < S2_ROWS; ++r) mx[r] = fmaxf(fmaxf(red[0][r], red[1][r]), fmaxf(red[2][r], red[3][r]));
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < S2_ROWS; ++r) {
     s[r] = __expf(s[r] - mx[r]);
     const float t = wave_sum(s[r]);
     if (lane == 0) red[wave][r] = t;
   }
   __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < S2_ROWS; ++r) {
     const float tot = (red[0][r] + red[1][r]) + (red[2][r] + red[3][r]);
     const size_t o = ((size_t)bh * NL + i0 + r) * NL + j;
     const float v = s[r] / tot;
@@ -1651,7 +1656,7 @@ extern "C" int tm_nys_landmarks(int dtype, const void* q, const void* k, int nbh
 }
 
 extern "C" int tm_nys_sim2_softmax(const float* ql, const float* kl, int nbh, float* a2, void* stream) {
-  sim2_softmax_kernel<<<dim3(nbh, NL / 16), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, nullptr);
+  sim2_softmax_kernel<<<dim3(nbh, NL / S2_ROWS), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, nullptr);
   TM_CHECK_LAUNCH();
   return 0;
 }
@@ -1659,7 +1664,7 @@ extern "C" int tm_nys_sim2_softmax(const float* ql, const float* kl, int nbh, fl
 extern "C" int tm_nys_sim2_softmax_split(const float* ql, const float* kl, int nbh, float* a2, void* a2s,
                                          void* stream) {
   TM_REQUIRE(a2s, "sim2_softmax_split: a2s is required");
-  sim2_softmax_kernel<<<dim3(nbh, NL / 16), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, (bf16*)a2s);
+  sim2_softmax_kernel<<<dim3(nbh, NL / S2_ROWS), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, (bf16*)a2s);
   TM_CHECK_LAUNCH();
   return 0;
 }
