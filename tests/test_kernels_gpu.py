@@ -483,3 +483,55 @@ def test_conv_bwd_bf16_mfma(nbags, n):
         assert _rel(dw.cpu().view(nh, 33), ref_dw) < 1e-5, variant
         outs.append(dv.cpu())
     assert _rel(outs[0], outs[1].double()) < 1e-5
+
+
+# ----------------------------------------------------------------------------- A3 attention backward
+def _a3_bwd_ref(ql, dw, k, v):
+    """fp64: A = softmax(ql k^T) over the keys; dS = A (dw v^T - rowsum(dw o A v));
+    dk = dS^T ql, dv = A^T dw, dql = dS k (the backward of W = A v, SURVEY App. A eq. 3/9)."""
+    ql, dw, k, v = (t.double() for t in (ql, dw, k, v))
+    s = ql @ k.transpose(1, 2)
+    lse = torch.logsumexp(s, -1)
+    a = torch.exp(s - lse[..., None])
+    w = a @ v
+    d = (dw * w).sum(-1)
+    ds = a * (dw @ v.transpose(1, 2) - d[..., None])
+    return lse, d, ds.transpose(1, 2) @ ql, a.transpose(1, 2) @ dw, ds @ k
+
+
+@pytest.mark.parametrize("nbh,n", [(8, 256), (2, 1280), (8, 1280), (8, 8448), (16, 8448)])
+def test_a3_bwd_bf16_even_split(nbh, n):
+    """The bf16 A3 backward (key units split evenly over the workgroups of a head: the 9-wave
+    form at 8 heads x 8448 keys, short workgroups elsewhere) and the legacy per-256-key-block
+    kernel (variant 3) against fp64."""
+    L = _lib()
+    from transmil_deepgraft_amd._lib import BF16
+    from transmil_deepgraft_amd.engine import _p, _stream
+    g = torch.Generator(device="cpu").manual_seed(n * 3 + nbh)
+    ql = (torch.randn(nbh, 256, 64, generator=g) * 0.3).to(torch.bfloat16)
+    dw = (torch.randn(nbh, 256, 64, generator=g) * 0.1).to(torch.bfloat16)
+    k = (torch.randn(nbh, n, 64, generator=g) * 0.3).to(torch.bfloat16)
+    v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16)
+    lse, d, ref_dk, ref_dv, ref_dql = _a3_bwd_ref(ql, dw, k, v)
+    outs = []
+    for variant in (0, 3):
+        L.lib().tm_debug_set_variant(1, variant)
+        try:
+            dk = torch.full((nbh, n, 64), float("nan"), device=DEV)
+            dv = torch.zeros(nbh, n, 64, device=DEV)           # accumulated into (+=)
+            dql = torch.full((nbh, 256, 64), float("nan"), device=DEV)
+            work = torch.empty(L.query("tm_nys_a3_bwd_workspace", nbh, n) // 4 + 16, device=DEV)
+            qd, wd, kd, vd = (t.to(DEV).contiguous() for t in (ql, dw, k, v))
+            lsed, dd = lse.float().to(DEV).contiguous(), d.float().to(DEV).contiguous()
+            L.call("tm_nys_a3_bwd", BF16, _p(qd), _p(wd), _p(kd), _p(vd), _p(lsed), _p(dd), nbh, 8, n,
+                   _p(dk), _p(dv), _p(work), _p(dql), 0, _stream())
+            torch.cuda.synchronize()
+        finally:
+            L.lib().tm_debug_set_variant(1, 0)
+        assert torch.isfinite(dk).all() and torch.isfinite(dv).all() and torch.isfinite(dql).all(), variant
+        assert _rel(dk.cpu(), ref_dk) < 2e-2, variant
+        assert _rel(dv.cpu(), ref_dv) < 2e-2, variant
+        assert _rel(dql.cpu(), ref_dql) < 2e-2, variant
+        outs.append((dk.cpu(), dv.cpu(), dql.cpu()))
+    for x, y in zip(*outs):
+        assert _rel(x, y.double()) < 2e-2

@@ -24,6 +24,7 @@
 //   attn_bwd<MODE>   shared flash-style backward for the A1 and A3 products
 //   assemble_dqkv    dq, dk, dv + landmark terms -> [B][n][3*h*64]
 #include <algorithm>
+#include <type_traits>
 #include "common.h"
 #include "../../include/transmil_hip.h"
 
@@ -1332,19 +1333,28 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
 // walk, so the walk itself issues no global loads (the per-chunk version paid two
 // dependent HBM round trips per 32-query chunk).  dV/dK operands come from the same
 // row-major images through transposing reads (acc_as_operand k order).
-struct BwdLay16 {
-  static constexpr int MAXQ = 288;  // query rows per workgroup (A1 even split: <= 9 chunks of 32)
-  static constexpr int KT_ROW = NL + 8, DS_ROW = NL + 8, QROW = DH + 8;
+// NW waves = NW 32-key units per workgroup; MQ = staged query rows.  <8, 288>: A1 (the 256
+// landmark keys, <= 9 query chunks) and the A3 key blocks of 256; <9, 256>: A3 with the n / 32 key
+// units of a head split evenly over 256 / nbh workgroups (8-9 units each: one chip round at
+// N = 8192 where 33 blocks of 256 keys per head were 264 workgroups on 256 CUs).
+template <int NW, int MQ>
+struct BwdLayT {
+  static constexpr int MAXQ = MQ;
+  static constexpr int NK = 32 * NW;  // key columns
+  static constexpr int KT_ROW = NK + 8, DS_ROW = NK + 8, QROW = DH + 8;
   static constexpr size_t KT_OFF = 0;
   static constexpr size_t DS_OFF = KT_OFF + DH * KT_ROW * 2;
   static constexpr size_t QS_OFF = DS_OFF + 32 * DS_ROW * 2;
   static constexpr size_t OS_OFF = QS_OFF + MAXQ * QROW * 2;
   static constexpr size_t XC_OFF = OS_OFF + MAXQ * QROW * 2;  // fp32 [3][2][1024]
   static constexpr size_t LS_OFF = XC_OFF + 6 * 1024 * 4;     // fp32 lse[MAXQ], D[MAXQ]
-  static constexpr size_t MAIN = LS_OFF + 2 * MAXQ * 4;       // 160512 B
-  static constexpr size_t EPI = (size_t)NL * 68 * 4;
+  static constexpr size_t MAIN = LS_OFF + 2 * MAXQ * 4;       // 160512 B (<8, 288>), 157184 B (<9, 256>)
+  static constexpr size_t EPI = (size_t)NK * 68 * 4;
   static constexpr size_t BYTES = MAIN > EPI ? MAIN : EPI;
 };
+using BwdLay16 = BwdLayT<8, 288>;
+using BwdLay9 = BwdLayT<9, 256>;
+static_assert(BwdLay9::BYTES <= 160 * 1024, "A3 even-split layout exceeds the CU's LDS");
 
 // A-operand fragment (rows m = mb + l32, 8 k in acc_as_operand order) of a row-major
 // [k][QROW] bf16 image: element j of lane half h <-> k = kb + 8 (j >> 2) + 4 h + (j & 3)
@@ -1359,10 +1369,14 @@ TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) {
   return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int MODE>
-__global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
-  using LY = BwdLay16;
+template <int MODE, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
+  using LY = std::conditional_t<NW == 9, BwdLay9, BwdLay16>;
+  static_assert(NW == 8 || (NW == 9 && MODE == MODE_A3), "9-wave form: A3 even split only");
+  constexpr int NT = 64 * NW;
   constexpr int KT_ROW = LY::KT_ROW, DS_ROW = LY::DS_ROW, QROW = LY::QROW;
+  // dQ roles: 2 d tiles x NKQ key groups of KQS 16-deep k-steps (8 waves: 4 x 64 keys; 9: 3 x 96)
+  constexpr int NKQ = NW == 9 ? 3 : 4, KQS = 2 * NW / NKQ;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* kt_s = (bf16*)(smem + LY::KT_OFF);
   bf16* ds_s = (bf16*)(smem + LY::DS_OFF);
@@ -1375,7 +1389,17 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, bh = blockIdx.y, nh = a.nh;
-  const int key0 = (MODE == MODE_A3) ? blk * NL : 0;
+  int key0 = (MODE == MODE_A3) ? blk * NL : 0;
+  int nunits = 8;  // 32-key units of this workgroup (wave w < nunits owns keys key0 + 32 w ..)
+  if (MODE == MODE_A3 && a.q_total > 0) {
+    // even split of the head's n / 32 key units over the gridDim.x workgroups (<= NW each, host-checked)
+    const int upk = a.n_key_rows / 32;
+    const int u0 = (int)((long long)blk * upk / gridDim.x), u1 = (int)((long long)(blk + 1) * upk / gridDim.x);
+    key0 = 32 * u0;
+    nunits = u1 - u0;
+  }
+  const int nk = 32 * nunits;
+  const bool active = wave < nunits;
   int q_begin = (MODE == MODE_A1) ? blk * a.n_queries_per_wg : 0;
   int q_count = a.n_queries_per_wg;  // <= 256, a multiple of 32 (host-checked)
   if (MODE == MODE_A1 && a.q_total > 0) {
@@ -1396,25 +1420,28 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
   const float* dd = a.dd + bh * a.dd_bh + q_begin;
 
   // ---- one burst of loads: K rows (for K^T), Q / dO rows, K / V fragments, lse / D ----
-  constexpr int QP = (LY::MAXQ * 8 + 511) / 512;  // 16-B query-row pieces per thread (5)
+  constexpr int QP = (LY::MAXQ * 8 + NT - 1) / NT;  // 16-B query-row pieces per thread (5 | 4)
   const int mykey = wave * 32;
   bf16x8 kr[4], qr[QP], orow[QP], kf[4], vf[4];
+  // key rows past nk (a short workgroup of the even split): clamped loads, finite, and their dS
+  // columns are written as zeros, so they add nothing to dQ
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = tid + 512 * j;  // 16-B piece: row c >> 3, d0 = (c & 7) * 8
-    kr[j] = load8(K + (size_t)(c >> 3) * DH + (c & 7) * 8);
+    const int c = tid + NT * j;  // 16-B piece: row c >> 3 (< 32 NW), d0 = (c & 7) * 8
+    kr[j] = load8(K + (size_t)min(c >> 3, nk - 1) * DH + (c & 7) * 8);
   }
 #pragma unroll
   for (int j = 0; j < QP; ++j) {
-    const int c = tid + 512 * j;
+    const int c = tid + NT * j;
     const int qq = min(c >> 3, q_count - 1);  // rows past q_count: clamped, never read back
     qr[j] = load8(Q + (size_t)qq * a.q_row + (c & 7) * 8);
     orow[j] = load8(dO + (size_t)qq * a.o_row + (c & 7) * 8);
   }
+  const int kfr = min(mykey + r, nk - 1);
 #pragma unroll
   for (int st = 0; st < 4; ++st) {
-    kf[st] = load8(K + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
-    vf[st] = load8(V + (size_t)(mykey + r) * DH + st * 16 + 8 * h);
+    kf[st] = load8(K + (size_t)kfr * DH + st * 16 + 8 * h);
+    vf[st] = load8(V + (size_t)kfr * DH + st * 16 + 8 * h);
   }
   float lsev = 0.f, ddv = 0.f;
   if (tid < LY::MAXQ) {
@@ -1425,13 +1452,13 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = tid + 512 * j, row = c >> 3, d0 = (c & 7) * 8;
+    const int c = tid + NT * j, row = c >> 3, d0 = (c & 7) * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) kt_s[(d0 + e) * KT_ROW + row] = kr[j][e];
   }
 #pragma unroll
   for (int j = 0; j < QP; ++j) {
-    const int c = tid + 512 * j, row = c >> 3, d0 = (c & 7) * 8;
+    const int c = tid + NT * j, row = c >> 3, d0 = (c & 7) * 8;
     if (row < LY::MAXQ) {
       *(bf16x8*)(qs + row * QROW + d0) = qr[j];
       *(bf16x8*)(os + row * QROW + d0) = orow[j];
@@ -1447,53 +1474,58 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) { dvt[i] = (f32x16){}; dkt[i] = (f32x16){}; }
 
-  const int dt_q = wave & 1, kq = wave >> 1;  // dQ role: d tile, key quarter
+  const int dt_q = wave & 1, kq = wave >> 1;  // dQ role: d tile, key group (waves < 2 NKQ)
+  const bool dq_role = wave < 2 * NKQ;
 #pragma unroll 1
   for (int c0 = 0; c0 < q_count; c0 += 32) {
     // S = Q K^T, dP = dO V^T: rows = queries (registers), cols = this wave's keys (lanes)
     f32x16 s = (f32x16){}, dp = (f32x16){};
+    if (active) {
 #pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const bf16x8 qa_f = *(const bf16x8*)(qs + (c0 + r) * QROW + st * 16 + 8 * h);
-      const bf16x8 oa_f = *(const bf16x8*)(os + (c0 + r) * QROW + st * 16 + 8 * h);
-      mma16(s, qa_f, kf[st]);
-      mma16(dp, oa_f, vf[st]);
-    }
+      for (int st = 0; st < 4; ++st) {
+        const bf16x8 qa_f = *(const bf16x8*)(qs + (c0 + r) * QROW + st * 16 + 8 * h);
+        const bf16x8 oa_f = *(const bf16x8*)(os + (c0 + r) * QROW + st * 16 + 8 * h);
+        mma16(s, qa_f, kf[st]);
+        mma16(dp, oa_f, vf[st]);
+      }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int qq = c0 + acc_row(i, h);
-      const float p = __expf(s[i] - lse_s[qq]);
-      s[i] = p;
-      dp[i] = p * (dp[i] - dd_s[qq]);
-    }
-    // dV^T += dO^T P ; dK^T += Q^T dS
+      for (int i = 0; i < 16; ++i) {
+        const int qq = c0 + acc_row(i, h);
+        const float p = __expf(s[i] - lse_s[qq]);
+        s[i] = p;
+        dp[i] = p * (dp[i] - dd_s[qq]);
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS
 #pragma unroll
-    for (int sp = 0; sp < 2; ++sp) {
-      const bf16x8 bp = acc_as_operand<bf16>(s, sp);
-      const bf16x8 bs = acc_as_operand<bf16>(dp, sp);
+      for (int sp = 0; sp < 2; ++sp) {
+        const bf16x8 bp = acc_as_operand<bf16>(s, sp);
+        const bf16x8 bs = acc_as_operand<bf16>(dp, sp);
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const bf16x8 ao = frag_tr_acc(os + c0 * QROW, dt * 32, 16 * sp, lane);
-        const bf16x8 aq = frag_tr_acc(qs + c0 * QROW, dt * 32, 16 * sp, lane);
-        mma16(dvt[dt], ao, bp);
-        mma16(dkt[dt], aq, bs);
+        for (int dt = 0; dt < 2; ++dt) {
+          const bf16x8 ao = frag_tr_acc(os + c0 * QROW, dt * 32, 16 * sp, lane);
+          const bf16x8 aq = frag_tr_acc(qs + c0 * QROW, dt * 32, 16 * sp, lane);
+          mma16(dvt[dt], ao, bp);
+          mma16(dkt[dt], aq, bs);
+        }
       }
     }
     __syncthreads();  // previous chunk's dQ reads of ds_s / xch are done
 #pragma unroll
-    for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + r] = from_f<bf16>(dp[i]);
+    for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + r] = from_f<bf16>(dp[i]);  // 0: idle wave
     __syncthreads();
-    // dQ chunk [32 q x 64 d] = dS [32 x 256] . K [256 x 64]: this wave: d tile dt_q, keys 64*kq..+63
+    // dQ chunk [32 q x 64 d] = dS [32 x NK] . K [NK x 64]: this wave: d tile dt_q, keys 16 KQS kq ..
     {
       f32x16 acc = (f32x16){};
+      if (dq_role) {
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int kk = kq * 64 + st * 16 + 8 * h;
-        mma16(acc, load8(ds_s + r * DS_ROW + kk), load8(kt_s + (dt_q * 32 + r) * KT_ROW + kk));
-      }
-      if (kq > 0) {
+        for (int st = 0; st < KQS; ++st) {
+          const int kk = kq * 16 * KQS + st * 16 + 8 * h;
+          mma16(acc, load8(ds_s + r * DS_ROW + kk), load8(kt_s + (dt_q * 32 + r) * KT_ROW + kk));
+        }
+        if (kq > 0) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) xch[((kq - 1) * 2 + dt_q) * 1024 + i * 64 + lane] = acc[i];
+          for (int i = 0; i < 16; ++i) xch[((kq - 1) * 2 + dt_q) * 1024 + i * 64 + lane] = acc[i];
+        }
       }
       __syncthreads();
       if (kq == 0) {
@@ -1503,8 +1535,9 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int qq = q_begin + c0 + acc_row(i, h);
-          const float v = ((acc[i] + xch[(0 * 2 + dt_q) * 1024 + i * 64 + lane]) +
-                           xch[(1 * 2 + dt_q) * 1024 + i * 64 + lane]) + xch[(2 * 2 + dt_q) * 1024 + i * 64 + lane];
+          float v = acc[i];
+#pragma unroll
+          for (int g = 0; g < NKQ - 1; ++g) v += xch[(g * 2 + dt_q) * 1024 + i * 64 + lane];
           dst[(size_t)qq * DH + dt_q * 32 + r] = v;
         }
       }
@@ -1529,7 +1562,7 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
       bf16* out = (bf16*)a.dqkv + ((size_t)bag * a.n_key_rows + key0) * 3 * inner + (which == 0 ? 2 : 1) * inner + hh * DH;
       const float* dvc = a.dv + bh * a.dv_bh + (size_t)key0 * DH;
       const float* dkl = a.dkl + (size_t)bh * NL * DH;
-      for (int i = tid; i < NL * DH / 4; i += 512) {
+      for (int i = tid; i < nk * DH / 4; i += NT) {
         const int key = i >> 4, d4 = (i & 15) * 4;
         f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
         if (which == 0) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
@@ -1548,7 +1581,7 @@ __global__ __launch_bounds__(512) void attn_bwd_bf16_kernel(BwdArgs a) {
     } else {
       dst = (which == 0 ? a.dv : a.dk) + (size_t)blk * a.slab_stride + bh * (which == 0 ? a.dv_bh : a.dk_bh);
     }
-    for (int i = tid; i < NL * DH / 4; i += 512) {
+    for (int i = tid; i < nk * DH / 4; i += NT) {
       const int key = i >> 4, d4 = (i & 15) * 4;
       f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
       float* p = dst + (size_t)key * DH + d4;
@@ -1826,8 +1859,37 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
 
 // A3 backward: keys = k rows, values = v rows, queries = ql_t (256 landmarks), dO = dw_t.
 // dk written (=), dv accumulated (+=), dql accumulated from partial slabs.
+namespace {
+// bf16 A3 backward grid: the head's n / 32 key units split evenly over 256 / nbh workgroups when
+// that is <= 9 units each (one chip round; the 9-wave form), else over ceil(units / 8) workgroups
+// of the 8-wave form.  Every workgroup writes one dq~ partial slab.
+struct A3Split { int wpg, nw; };
+A3Split a3_bwd_split(int nbh, int n) {
+  const int units = n / 32;
+  const int w = std::max(1, std::min(units, 256 / std::max(nbh, 1)));
+  const int per = (units + w - 1) / w;
+  if (per <= 8) return {w, 8};
+  if (per == 9) return {w, 9};
+  return {(units + 7) / 8, 8};
+}
+
+void launch_a3_bwd_bf16(BwdArgs& a, int nbh, int n, hipStream_t st, int& slabs) {
+  const A3Split sp = a3_bwd_split(nbh, n);
+  a.q_total = n;  // even split on
+  slabs = sp.wpg;
+  if (sp.nw == 9) {
+    tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9>, BwdLay9::BYTES);
+    attn_bwd_bf16_kernel<MODE_A3, 9><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
+  } else {
+    tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 8>, BwdLay16::BYTES);
+    attn_bwd_bf16_kernel<MODE_A3, 8><<<dim3(sp.wpg, nbh), 512, BwdLay16::BYTES, st>>>(a);
+  }
+}
+}  // namespace
+
 extern "C" long long tm_nys_a3_bwd_workspace(int nbh, int n) {
-  return (long long)(n / NL) * nbh * NL * DH * (long long)sizeof(float);
+  const long long slabs = std::max((long long)(n / NL), (long long)a3_bwd_split(nbh, n).wpg);
+  return slabs * nbh * NL * DH * (long long)sizeof(float);
 }
 
 extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
@@ -1847,15 +1909,15 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
   a.dv = dv; a.dv_bh = (long long)n * DH;
   a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
   hipStream_t st = (hipStream_t)stream;
+  int slabs = nkb;
   if (dtype == TM_BF16 && g_nys_variant != 3) {
-    tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3>, BwdLay16::BYTES);
-    attn_bwd_bf16_kernel<MODE_A3><<<dim3(nkb, nbh), 512, BwdLay16::BYTES, st>>>(a);
+    launch_a3_bwd_bf16(a, nbh, n, st, slabs);
   } else {
     TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A3>, bwd_smem_bytes<T>()),
                               attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
   }
   TM_CHECK_LAUNCH();
-  return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, accumulate, stream);
+  return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, accumulate, stream);
 }
 
 // bf16 A3 backward with the fused key-side epilogue: the final k / v parts of dqkv from dK, dV,
@@ -1879,10 +1941,10 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
   a.dqkv = dqkv; a.dkl = dkl; a.l = n / NL; a.inv_l = 1.0f / (float)(n / NL);
   hipStream_t st = (hipStream_t)stream;
-  tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3>, BwdLay16::BYTES);
-  attn_bwd_bf16_kernel<MODE_A3><<<dim3(nkb, nbh), 512, BwdLay16::BYTES, st>>>(a);
+  int slabs = nkb;
+  launch_a3_bwd_bf16(a, nbh, n, st, slabs);
   TM_CHECK_LAUNCH();
-  return tm_splitk_reduce(work, dql, nkb, (long long)nbh * NL * DH, 1.0f, 0, stream);
+  return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, 0, stream);
 }
 
 extern "C" int tm_nys_assemble_q(int dtype, const float* dq, const float* dql_a, const float* dql_b, int nbags,
