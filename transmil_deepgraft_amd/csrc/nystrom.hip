@@ -723,24 +723,46 @@ __global__ __launch_bounds__(256, 2) void a3_fwd_kernel(const float* __restrict_
   }
 }
 
-// combine the key-block partials: W[bh][q][d], lse3[bh][q]; grid (nbh, 64), block 256 (4 queries x 64 d)
-__global__ void a3_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_m,
-                                  const float* __restrict__ part_l, int nkb, int nbh, float* __restrict__ w,
-                                  float* __restrict__ lse3) {
-  const int bh = blockIdx.x, qi = blockIdx.y * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
+// combine the key-block partials: W[bh][q][d], lse3[bh][q]; grid (nbh, 16), block 256: thread =
+// (query blockIdx.y * 16 + tid / 16, 4 consecutive d).  The partials of U key blocks are requested
+// in one burst (clamped indices, masked adds), key blocks summed in index order.
+constexpr int A3C_U = 11;
+__global__ __launch_bounds__(256) void a3_combine_kernel(const float* __restrict__ part_o, const float* __restrict__ part_m,
+                                                         const float* __restrict__ part_l, int nkb, int nbh,
+                                                         float* __restrict__ w, float* __restrict__ lse3) {
+  const int bh = blockIdx.x, qi = blockIdx.y * 16 + (threadIdx.x >> 4), d4 = (threadIdx.x & 15) * 4;
+  const size_t q0 = (size_t)bh * NL + qi, kstride = (size_t)nbh * NL;
   float M = -INFINITY;
-#pragma unroll 8
-  for (int kb = 0; kb < nkb; ++kb) M = fmaxf(M, part_m[((size_t)kb * nbh + bh) * NL + qi]);
-  float L = 0.f, acc = 0.f;
-#pragma unroll 8
-  for (int kb = 0; kb < nkb; ++kb) {
-    const size_t pidx = ((size_t)kb * nbh + bh) * NL + qi;
-    const float sc = __expf(part_m[pidx] - M);
-    L += part_l[pidx] * sc;
-    acc += part_o[pidx * DH + d] * sc;
+  for (int kb0 = 0; kb0 < nkb; kb0 += A3C_U) {
+    float mv[A3C_U];
+#pragma unroll
+    for (int u = 0; u < A3C_U; ++u) mv[u] = part_m[(size_t)min(kb0 + u, nkb - 1) * kstride + q0];
+#pragma unroll
+    for (int u = 0; u < A3C_U; ++u) M = fmaxf(M, mv[u]);  // clamped repeats change nothing
   }
-  w[((size_t)bh * NL + qi) * DH + d] = acc / L;
-  if (d == 0) lse3[(size_t)bh * NL + qi] = M + __logf(L);
+  float L = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int kb0 = 0; kb0 < nkb; kb0 += A3C_U) {
+    float mv[A3C_U], lv[A3C_U];
+    f32x4 ov[A3C_U];
+#pragma unroll
+    for (int u = 0; u < A3C_U; ++u) {
+      const size_t pidx = (size_t)min(kb0 + u, nkb - 1) * kstride + q0;
+      mv[u] = part_m[pidx];
+      lv[u] = part_l[pidx];
+      ov[u] = *(const f32x4*)(part_o + pidx * DH + d4);
+    }
+#pragma unroll
+    for (int u = 0; u < A3C_U; ++u) {
+      if (kb0 + u < nkb) {
+        const float sc = __expf(mv[u] - M);
+        L += lv[u] * sc;
+        acc += ov[u] * sc;
+      }
+    }
+  }
+  *(f32x4*)(w + q0 * DH + d4) = acc / L;
+  if (d4 == 0) lse3[q0] = M + __logf(L);
 }
 
 // ---------------------------------------------------------------------------
@@ -1727,7 +1749,7 @@ extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const vo
     a3_fwd_kernel<T><<<dim3(nkb, nbh, 2), 256, sm, st>>>(ql, (const T*)k, (const T*)v, n, po, pm, pl);
   }));
   TM_CHECK_LAUNCH();
-  a3_combine_kernel<<<dim3(nbh, NL / 4), 256, 0, st>>>(po, pm, pl, nkb, nbh, w, lse3);
+  a3_combine_kernel<<<dim3(nbh, NL / 16), 256, 0, st>>>(po, pm, pl, nkb, nbh, w, lse3);
   TM_CHECK_LAUNCH();
   return 0;
 }
