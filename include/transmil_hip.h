@@ -136,12 +136,13 @@ int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const flo
                          const float* dv, int nbags, int nh, int n, float scale, void* dqkv, void* stream);
 /* bf16 mode, fused key side: the A3 backward writes the final bf16 k / v parts of dqkv
  * (k = dK + dk~[t/l]/l, v = dv_conv + dV) and dql (=) from its slabs; then tm_nys_assemble_q
- * writes the q part, scale * (dq + (dql_a + dql_b)[t/l]/l). */
+ * writes the q part, scale * (dq + (dql_a + dql_b)[t/l]/l).  dv_conv is read only for rows
+ * [dv_lo, dv_hi) (zero elsewhere; 0, n = dense); dq_row >= 0: dq is zero outside that row. */
 int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v, const float* lse3,
-                        const float* d3, int nbh, int nh, int n, const float* dv_conv, const float* dkl,
-                        float* work, float* dql, void* dqkv, void* stream);
-int tm_nys_assemble_q(int dtype, const float* dq, const float* dql_a, const float* dql_b, int nbags, int nh,
-                      int n, float scale, void* dqkv, void* stream);
+                        const float* d3, int nbh, int nh, int n, const float* dv_conv, int dv_lo, int dv_hi,
+                        const float* dkl, float* work, float* dql, void* dqkv, void* stream);
+int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a, const float* dql_b, int nbags,
+                      int nh, int n, float scale, void* dqkv, void* stream);
 
 /* ---- pseudo-inverse + small fp32 batched products (pinv.hip) -------------
  * moore_penrose_iter_pinv of nystrom_attention (App. A eq. 7).
@@ -192,7 +193,8 @@ int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int iters, const 
 /* fp32 -> split planes: y[i] = bf16(x[i]), y[count + i] = bf16(x[i] - y[i]); count % 8 == 0 */
 int tm_split_f32(const float* x, void* y, long long count, void* stream);
 
-/* ---- PPEG (ppeg.hip) -- code/models/TransMIL.py:60-75 -------------------- */
+/* ---- PPEG (ppeg.hip) -- code/models/TransMIL.py:60-75 -------------------- *
+ * wfold [49][D] tap-major (the three depthwise kernels + identity folded into one 7x7), bfold [D] */
 int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, const float* b5, const float* w3,
                  const float* b3, int D, float* wfold, float* bfold, void* stream);
 int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
@@ -243,6 +245,24 @@ int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, 
 /* dpre = dy * GELU'(pre) elementwise (fp32 dy / pre, dpre in dtype): the backward of the inner
  * Linear + GELU of the in_features = 2048 _fc1 branch (code/models/TransMIL.py:100-111) */
 int tm_gelu_bwd(int dtype, const float* dy, const float* pre, long long count, void* dpre, void* stream);
+
+/* ---- class-row specialisation of the last TransLayer (clsrow.hip) -- code/models/TransMIL.py:195-203 ----
+ * The logits read layer 2 only through the class token (norm(h)[:, 0]), which sits at row r = pad of
+ * the front-padded attention input.  Forward: merged[b][r] = A1 row + conv33 (lse1[bh][r] written),
+ * then H3[b*S] = H2[b*S] + dropout(merged[b][r] Wo^T + bo) (other H3 rows are not written).
+ * Backward (dL/dH3 zero outside the class rows): dWo, dbo (=), dmerged [B][D] (dtype) rows; then
+ * dq row r (the caller zero-fills dq), dk~ / dY (=) [nbh][256][64], the conv33 dv window rows
+ * r-16..r+16 (caller zero-fills dv) and dwconv (=) [nh][33]. */
+int tm_cls_a1_row_fwd(int dtype, const void* q, const void* v, const void* kl_t, const void* y_t, const float* wconv,
+                      int nbh, int nh, int n, int r, void* merged, float* lse1, void* stream);
+int tm_cls_out_fwd(int dtype, const void* merged, const void* wo, const float* bo, const float* H2, int B, int n, int r,
+                   int S, int D, float p, uint64_t seed, const uint64_t* seed_ptr, float* H3, void* stream);
+int tm_cls_out_bwd(int dtype, const float* dH, const void* merged, const void* wo, int B, int n, int r, int S, int D,
+                   float p, uint64_t seed, const uint64_t* seed_ptr, float* dwo, float* dbo, void* dmerged,
+                   void* stream);
+int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, const void* v, const void* kl_t, const void* y_t,
+                      const float* lse1, const float* wconv, int B, int nh, int n, int r, float* dq, float* dkl,
+                      float* dy, float* dv, float* dwconv, void* stream);
 
 /* fp32 -> dtype copies of up to 8 tensors (per-step bf16 GEMM weight operands) in one launch;
  * offset[] = prefix sums of the element counts, offset[0] = 0 */

@@ -456,3 +456,31 @@ def test_branch_models_bf16_close_to_reference(name):
     loss.backward()
     for n, p in ours.named_parameters():
         assert torch.isfinite(p.grad).all() and p.grad.abs().max() > 0, n
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 3e-2)])
+@pytest.mark.parametrize("train", [False, True])
+def test_last_layer_class_row_path_equals_dense(dtype, tol, train, monkeypatch):
+    """Layer 2 on the class rows only (clsrow.hip: A1 row + conv33, to_out, and their backward)
+    against the same engine running layer 2 dense: logits and every parameter gradient, B = 2,
+    eval and train mode (same dropout seed)."""
+    from transmil_deepgraft_amd import engine as E
+    _, ours = _pair(2, dtype=dtype)
+    if train:
+        ours.train()
+    x = torch.from_numpy(bag_input(1000, 512, 5, 2))
+    c0 = ours._dropout_counter.clone()
+    outs = []
+    for cls_only in (True, False):
+        monkeypatch.setattr(E.TransMILEngine.__init__, "__defaults__", (torch.bfloat16, None, "_fc", cls_only))
+        ours._dropout_counter.copy_(c0)
+        ours.zero_grad(set_to_none=True)
+        outs.append(_ours_forward_backward(ours, x, 1, 2))
+    (lc, gc), (ld, gd) = outs
+    assert ((lc - ld).abs().max() / ld.abs().max()).item() < tol
+    bad = []
+    for name, g in gd.items():
+        err = ((gc[name].double() - g.double()).abs().max() / g.double().abs().max().clamp_min(1e-12)).item()
+        if err > tol:
+            bad.append((name, err))
+    assert not bad, bad

@@ -90,8 +90,8 @@ _SIGS = {
     "tm_nys_a3_bwd_workspace": (L, [I, I]),
     "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, I, P]),
     "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
-    "tm_nys_a3_bwd_fused": (I, [P, P, P, P, P, P, I, I, I, P, P, P, P, P, P]),
-    "tm_nys_assemble_q": (I, [I, P, P, P, I, I, I, Fl, P, P]),
+    "tm_nys_a3_bwd_fused": (I, [P, P, P, P, P, P, I, I, I, P, I, I, P, P, P, P, P]),
+    "tm_nys_assemble_q": (I, [I, P, I, P, P, I, I, I, Fl, P, P]),
     "tm_nys_attn_row": (I, [I, P, P, P, P, P, P, I, I, I, P, P]),
     "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
     "tm_debug_set_variant": (None, [I, I]),
@@ -122,6 +122,10 @@ _SIGS = {
     "tm_ce_fwd": (I, [P, P, I, I, P, P, P, P, P]),
     "tm_ce_bwd": (I, [P, P, I, I, P, P, P]),
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
+    "tm_cls_a1_row_fwd": (I, [I, P, P, P, P, P, I, I, I, I, P, P, P]),
+    "tm_cls_out_fwd": (I, [I, P, P, P, P, I, I, I, I, I, Fl, U64, P, P, P]),
+    "tm_cls_out_bwd": (I, [I, P, P, P, I, I, I, I, I, Fl, U64, P, P, P, P, P]),
+    "tm_cls_a1_row_bwd": (I, [I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),
     "tm_gelu_bwd": (I, [I, P, P, L, P, P]),

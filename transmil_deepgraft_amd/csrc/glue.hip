@@ -56,7 +56,7 @@ __global__ void __launch_bounds__(256) step_prepare_kernel(tm_cast_table tab, lo
         if (dy >= 1 && dy <= 5 && dx >= 1 && dx <= 5) v += w5[(size_t)ch * 25 + (dy - 1) * 5 + (dx - 1)];
         if (dy >= 2 && dy <= 4 && dx >= 2 && dx <= 4) v += w3[(size_t)ch * 9 + (dy - 2) * 3 + (dx - 2)];
         if (dy == 3 && dx == 3) v += 1.0f;
-        wf[(size_t)ch * 49 + dy * 7 + dx] = v;
+        wf[(size_t)(dy * 7 + dx) * D + ch] = v;  // tap-major [49][D] (coalesced stencil reads)
       }
     bf[ch] = b7[ch] + b5[ch] + b3[ch];
     return;

@@ -1128,6 +1128,7 @@ struct BwdArgs {
   // bf16 A3 kernel, fused key side: non-null = write the FINAL k / v parts of dqkv (bf16,
   // [bag][n][3 nh 64]): k = dK + dk~[t / l] / l, v = dv (the conv backward's, read) + dV
   void* dqkv; const float* dkl; float inv_l; int l;
+  int dv_lo, dv_hi;   // fused: rows of the conv backward's dv that are read (zero outside)
 };
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
@@ -1321,7 +1322,9 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
       for (int i = tid; i < NL * DH / 4; i += 512) {
         const int key = i >> 4, d4 = (i & 15) * 4;
         f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
-        if (which == 0) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
+        if (which == 0) {
+          if (key0 + key >= a.dv_lo && key0 + key < a.dv_hi) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
+        }
         else val += *(const f32x4*)(dkl + (size_t)((key0 + key) / a.l) * DH + d4) * a.inv_l;
         *(bf16x4*)(out + (size_t)key * 3 * inner + d4) =
             (bf16x4){(bf16)val[0], (bf16)val[1], (bf16)val[2], (bf16)val[3]};
@@ -1587,7 +1590,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
       for (int i = tid; i < nk * DH / 4; i += NT) {
         const int key = i >> 4, d4 = (i & 15) * 4;
         f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
-        if (which == 0) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
+        if (which == 0) {
+          if (key0 + key >= a.dv_lo && key0 + key < a.dv_hi) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
+        }
         else val += *(const f32x4*)(dkl + (size_t)((key0 + key) / a.l) * DH + d4) * a.inv_l;
         *(bf16x4*)(out + (size_t)key * 3 * inner + d4) =
             (bf16x4){(bf16)val[0], (bf16)val[1], (bf16)val[2], (bf16)val[3]};
@@ -1661,7 +1666,7 @@ __global__ void assemble_dqkv_kernel(const float* __restrict__ dq, const float* 
 // q part of dqkv only (the k / v parts written by the fused A3 backward):
 // q = scale * (dq + (dql_a + dql_b)[t / l] / l); grid (ceil(n * nh * 8 / 256), nbags), block 256
 template <typename T>
-__global__ void assemble_q_kernel(const float* __restrict__ dq, const float* __restrict__ dql_a,
+__global__ void assemble_q_kernel(const float* __restrict__ dq, int dq_row, const float* __restrict__ dql_a,
                                   const float* __restrict__ dql_b, int n, int l, int nh, float scale,
                                   T* __restrict__ dqkv) {
   const int inner = nh * DH, per_row = inner / 8;
@@ -1674,7 +1679,8 @@ __global__ void assemble_q_kernel(const float* __restrict__ dq, const float* __r
   const size_t row = (bh * n + t) * DH + d;
   const size_t lrow = (bh * NL + t / l) * DH + d;
   const float inv_l = 1.0f / (float)l;
-  const f32x8 a = load8<float>(dq + row), b0 = load8<float>(dql_a + lrow), b1 = load8<float>(dql_b + lrow);
+  const f32x8 a = (dq_row < 0 || t == dq_row) ? load8<float>(dq + row) : (f32x8){};  // dq_row: the only non-zero row
+  const f32x8 b0 = load8<float>(dql_a + lrow), b1 = load8<float>(dql_b + lrow);
   vec8<T> out;
 #pragma unroll
   for (int e = 0; e < 8; ++e) out[e] = from_f<T>(scale * (a[e] + (b0[e] + b1[e]) * inv_l));
@@ -1947,7 +1953,8 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
 // backward); dql3 (=) from the per-key-block slabs.
 extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v,
                                    const float* lse3, const float* d3, int nbh, int nh, int n, const float* dv_conv,
-                                   const float* dkl, float* work, float* dql, void* dqkv, void* stream) {
+                                   int dv_lo, int dv_hi, const float* dkl, float* work, float* dql, void* dqkv,
+                                   void* stream) {
   TM_REQUIRE(n % NL == 0 && nbh % nh == 0, "a3_bwd_fused: n must be a multiple of 256");
   TM_REQUIRE(dv_conv && dkl && dqkv, "a3_bwd_fused: null operand");
   const int nkb = n / NL;
@@ -1962,6 +1969,7 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   a.dv = (float*)dv_conv; a.dv_bh = (long long)n * DH;
   a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
   a.dqkv = dqkv; a.dkl = dkl; a.l = n / NL; a.inv_l = 1.0f / (float)(n / NL);
+  a.dv_lo = dv_lo; a.dv_hi = dv_hi;
   hipStream_t st = (hipStream_t)stream;
   int slabs = nkb;
   launch_a3_bwd_bf16(a, nbh, n, st, slabs);
@@ -1969,13 +1977,13 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, 0, stream);
 }
 
-extern "C" int tm_nys_assemble_q(int dtype, const float* dq, const float* dql_a, const float* dql_b, int nbags,
-                                 int nh, int n, float scale, void* dqkv, void* stream) {
+extern "C" int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a, const float* dql_b,
+                                 int nbags, int nh, int n, float scale, void* dqkv, void* stream) {
   TM_REQUIRE(n % NL == 0, "assemble_q: n must be a multiple of 256");
   const long long items = (long long)n * nh * DH / 8;
   TM_DTYPE_DISPATCH(dtype, (assemble_q_kernel<T><<<dim3((unsigned)((items + 255) / 256), nbags), 256, 0,
-                                                    (hipStream_t)stream>>>(dq, dql_a, dql_b, n, n / NL, nh, scale,
-                                                                           (T*)dqkv)));
+                                                    (hipStream_t)stream>>>(dq, dq_row, dql_a, dql_b, n, n / NL, nh,
+                                                                           scale, (T*)dqkv)));
   TM_CHECK_LAUNCH();
   return 0;
 }

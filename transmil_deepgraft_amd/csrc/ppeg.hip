@@ -16,7 +16,7 @@ namespace {
 
 constexpr int KS = 7, R = 3, NT = 49;
 
-// w_fold[ch][49], b_fold[ch]
+// w_fold[49][ch] (tap-major: a wave's 64 channels of one tap are one 256-B load), b_fold[ch]
 __global__ void ppeg_fold_kernel(const float* __restrict__ w7, const float* __restrict__ b7,
                                  const float* __restrict__ w5, const float* __restrict__ b5,
                                  const float* __restrict__ w3, const float* __restrict__ b3, int D,
@@ -29,7 +29,7 @@ __global__ void ppeg_fold_kernel(const float* __restrict__ w7, const float* __re
       if (dy >= 1 && dy <= 5 && dx >= 1 && dx <= 5) v += w5[(size_t)ch * 25 + (dy - 1) * 5 + (dx - 1)];
       if (dy >= 2 && dy <= 4 && dx >= 2 && dx <= 4) v += w3[(size_t)ch * 9 + (dy - 2) * 3 + (dx - 2)];
       if (dy == R && dx == R) v += 1.0f;
-      wf[(size_t)ch * NT + dy * KS + dx] = v;
+      wf[(size_t)(dy * KS + dx) * D + ch] = v;
     }
   bf[ch] = b7[ch] + b5[ch] + b3[ch];
 }
@@ -39,6 +39,7 @@ __global__ void ppeg_fold_kernel(const float* __restrict__ w7, const float* __re
 // coalesced row segment across the wave's 64 channels) for 784 FMAs.
 // grid (ceil(nCB/4) * D/64, nRB, B), block 256: wave w -> column block 4*bx + w.
 constexpr int RB = 4;
+constexpr int WRB = 2;  // row blocks per weight-gradient workgroup
 
 template <bool BWD_DATA>
 __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ x, int S, int G, int D,
@@ -54,7 +55,7 @@ __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restri
   if (c0 >= G) return;
   float w[NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) w[t] = wf[(size_t)ch * NT + (BWD_DATA ? NT - 1 - t : t)];
+  for (int t = 0; t < NT; ++t) w[t] = wf[(size_t)(BWD_DATA ? NT - 1 - t : t) * D + ch];
   const float bias = BWD_DATA ? 0.f : bf[ch];
   float acc[RB][RB];
 #pragma unroll
@@ -91,8 +92,8 @@ __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restri
     }
 }
 
-// weight/bias gradient partials.  grid (ceil(nCB/4) * D/64, ceil(nRB/4), B), block 256:
-// a thread owns a channel and walks 4 row blocks of its column block; partial slab
+// weight/bias gradient partials.  grid (ceil(nCB/4) * D/64, ceil(nRB/WRB), B), block 256:
+// a thread owns a channel and walks WRB row blocks of its column block; partial slab
 // index = (b * gridDim.y + by) * gridDim.x/nchunk + bx/nchunk, layout [slab][ch][50].
 __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy_,
                                                          int S, int G, int D, float* __restrict__ part) {
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict
 #pragma unroll
   for (int t = 0; t <= NT; ++t) acc[t] = 0.f;
   if (c0 < G) {
-    for (int rb = blockIdx.y * 4; rb < blockIdx.y * 4 + 4; ++rb) {
+    for (int rb = blockIdx.y * WRB; rb < blockIdx.y * WRB + WRB; ++rb) {
       const int r0 = rb * RB;
       if (r0 >= G) break;
       float gv[RB][RB];
@@ -190,7 +191,7 @@ extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfo
 
 static int ppeg_wgrad_slabs(int B, int G) {
   const int ncb = (G + RB - 1) / RB;
-  return B * ((ncb + 3) / 4) * ((ncb + 3) / 4);
+  return B * ((ncb + 3) / 4) * ((ncb + WRB - 1) / WRB);
 }
 
 extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
@@ -207,7 +208,7 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
   const int ncb = (G + RB - 1) / RB;
   ppeg_stencil_kernel<true><<<dim3(((ncb + 3) / 4) * (D / 64), ncb, B), 256, 0, st>>>(dy, S, G, D, wfold, nullptr, dx);
   TM_CHECK_LAUNCH();
-  ppeg_wgrad_kernel<<<dim3(((ncb + 3) / 4) * (D / 64), (ncb + 3) / 4, B), 256, 0, st>>>(x, dy, S, G, D, work);
+  ppeg_wgrad_kernel<<<dim3(((ncb + 3) / 4) * (D / 64), (ncb + WRB - 1) / WRB, B), 256, 0, st>>>(x, dy, S, G, D, work);
   TM_CHECK_LAUNCH();
   if (int rc = tm_splitk_reduce(work, dwsum, ppeg_wgrad_slabs(B, G), (long long)D * 50, 1.0f, 0, stream)) return rc;
   ppeg_unfold_kernel<<<(D + 63) / 64, 64, 0, st>>>(dwsum, D, dw7, db7, dw5, db5, dw3, db3);

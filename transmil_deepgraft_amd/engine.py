@@ -238,8 +238,9 @@ def flush_reductions():
 
 
 # ----------------------------------------------------------------------------- NystromAttention core
-def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
-    """App. A eq. 4-9 on q, k, v [3, B*h, n, 64] -> merged [B, n, h*64] (T) + saved state."""
+def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool, cls_row=None):
+    """App. A eq. 4-9 on q, k, v [3, B*h, n, 64] -> merged [B, n, h*64] (T) + saved state.
+    ``cls_row``: only that row of merged (and of the A1 log-sum-exp) is computed (clsrow.hip)."""
     n, nbh, nh = geo.n, geo.nbh, geo.heads
     q, k, v = qkv[0], qkv[1], qkv[2]
     st = _stream()
@@ -280,42 +281,58 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool):
         y_t = y
     merged = pool(geo.B * n * nh * DH, tdtype).view(geo.B, n, nh * DH)
     lse1 = pool(nbh * n)
-    with probe("a1_fwd"):
-        _lib.call("tm_nys_a1_fwd", dt_code, _p(q), _p(v), _p(kl_t), _p(y_t), _p(wconv), nbh, nh, n, _p(merged),
-                  _p(lse1), st)
+    if cls_row is not None:
+        _lib.call("tm_cls_a1_row_fwd", dt_code, _p(q), _p(v), _p(kl_t), _p(y_t), _p(wconv), nbh, nh, n, cls_row,
+                  _p(merged), _p(lse1), st)
+    else:
+        with probe("a1_fwd"):
+            _lib.call("tm_nys_a1_fwd", dt_code, _p(q), _p(v), _p(kl_t), _p(y_t), _p(wconv), nbh, nh, n, _p(merged),
+                      _p(lse1), st)
     state = dict(ql=ql, kl=kl, ql_t=ql_t, kl_t=kl_t, a2=a2, a2s=a2s, pinv=saved, z=z, w=w, lse3=lse3, y=y,
                  y_t=y_t, lse1=lse1)
     return merged, state
 
 
 def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdtype, dt_code, pool,
-                          dwconv_out, scale):
-    """Backward of nystrom_core_forward: returns dqkv [B, n, 3*h*64] (T); writes dwconv_out."""
+                          dwconv_out, scale, cls_row=None):
+    """Backward of nystrom_core_forward: returns dqkv [B, n, 3*h*64] (T); writes dwconv_out.
+    ``cls_row``: dmerged is [B, h*64], the only non-zero row (``cls_row``) of the dense gradient."""
     n, nbh, nh = geo.n, geo.nbh, geo.heads
     q, k, v = qkv[0], qkv[1], qkv[2]
     st = _stream()
     mat = nbh * NL * NL
     prec = 1 if dt_code == BF16 else 0
-    # conv33 backward + D1
-    dq = pool(nbh * n * DH)
-    dk = pool(nbh * n * DH)
-    dv = pool(nbh * n * DH)
-    d1 = pool(nbh * n)
-    with defer_reductions(), probe("conv_bwd"):
-        work = pool(_lib.query("tm_nys_conv_bwd_workspace", geo.B, nh, n) // 4)
-        _lib.call("tm_nys_conv_bwd", dt_code, _p(dmerged), _p(merged), _p(v), _p(wconv), nbh, nh, n, _p(dv),
-                  _p(d1), _p(work), _p(dwconv_out), st)
-    # A1 product backward: dq (complete), dkl, dY
     y_t = state["y_t"]
-    qpw = 256 if n % 256 == 0 else 32
+    dk = pool(nbh * n * DH)
     dkl = pool(nbh * NL * DH).view(nbh, NL, DH)
     dy = pool(nbh * NL * DH).view(nbh, NL, DH)
-    work = pool(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, qpw) // 4)
-    with probe("a1_bwd"):
-        with defer_reductions():     # its dk~ and dY slab sums as one launch
-            _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t),
-                      _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, st)
-        flush_reductions()
+    fused = state["a2s"] is not None     # bf16 mode: the A3 backward writes the final k / v parts
+    if cls_row is not None:
+        # one non-zero query row: dq row, rank-1 dk~ / dY, the conv33 dv window (clsrow.hip); the
+        # bf16 consumers read only that row / window, the fp32 path reads dense zero-filled buffers
+        alloc = pool if fused else (lambda numel: torch.zeros(numel, dtype=torch.float32, device=q.device))
+        dq = alloc(nbh * n * DH)
+        dv = alloc(nbh * n * DH)
+        _lib.call("tm_cls_a1_row_bwd", dt_code, _p(dmerged), _p(q), _p(v), _p(state["kl_t"]), _p(y_t),
+                  _p(state["lse1"]), _p(wconv), geo.B, nh, n, cls_row, _p(dq), _p(dkl), _p(dy), _p(dv),
+                  _p(dwconv_out), st)
+    else:
+        # conv33 backward + D1
+        dq = pool(nbh * n * DH)
+        dv = pool(nbh * n * DH)
+        d1 = pool(nbh * n)
+        with defer_reductions(), probe("conv_bwd"):
+            work = pool(_lib.query("tm_nys_conv_bwd_workspace", geo.B, nh, n) // 4)
+            _lib.call("tm_nys_conv_bwd", dt_code, _p(dmerged), _p(merged), _p(v), _p(wconv), nbh, nh, n, _p(dv),
+                      _p(d1), _p(work), _p(dwconv_out), st)
+        # A1 product backward: dq (complete), dkl, dY
+        qpw = 256 if n % 256 == 0 else 32
+        work = pool(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, qpw) // 4)
+        with probe("a1_bwd"):
+            with defer_reductions():     # its dk~ and dY slab sums as one launch
+                _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t),
+                          _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, st)
+            flush_reductions()
     # Y = Z W
     dz = pool(mat).view(nbh, NL, NL)
     dw = pool(nbh * NL * DH).view(nbh, NL, DH)
@@ -332,7 +349,6 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     dql3 = pool(nbh * NL * DH).view(nbh, NL, DH)
     work3 = pool(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4)
     _lib.call("tm_nys_rowdot_cast", dt_code, _p(dw), _p(state["w"]), nbh * NL, _p(d3), _p(dw_t), st)
-    fused = state["a2s"] is not None     # bf16 mode: the A3 backward writes the final k / v parts
     if not fused:
         # A3 product backward: dk (=), dv (+=), dql3 (=)
         with probe("a3_bwd"):
@@ -359,10 +375,11 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL),
              bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
         with probe("a3_bwd"):
+            lo, hi = (0, n) if cls_row is None else (max(cls_row - 16, 0), min(cls_row + 17, n))
             _lib.call("tm_nys_a3_bwd_fused", _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]), _p(d3),
-                      nbh, nh, n, _p(dv), _p(dkl), _p(work3), _p(dql3), _p(dqkv), st)
-        _lib.call("tm_nys_assemble_q", dt_code, _p(dq), _p(dql), _p(dql3), geo.B, nh, n, C.c_float(scale),
-                  _p(dqkv), st)
+                      nbh, nh, n, _p(dv), lo, hi, _p(dkl), _p(work3), _p(dql3), _p(dqkv), st)
+        _lib.call("tm_nys_assemble_q", dt_code, _p(dq), -1 if cls_row is None else cls_row, _p(dql), _p(dql3),
+                  geo.B, nh, n, C.c_float(scale), _p(dqkv), st)
         return dqkv
     bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL, E1=dql3, e1=1.0),
          bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
@@ -372,8 +389,12 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
 
 
 # ----------------------------------------------------------------------------- TransLayer
-def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, seed, seed_dev=None):
-    """H [B*S, D] fp32 -> H + NystromAttention(LN(H)) (code/models/TransMIL.py:45-57)."""
+def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, seed, seed_dev=None, cls_only=False):
+    """H [B*S, D] fp32 -> H + NystromAttention(LN(H)) (code/models/TransMIL.py:45-57).
+
+    ``cls_only`` (the last layer, whose output the logits read only at the class token,
+    :201-203): the attention output, to_out and the residual add are computed for the class
+    rows b*S only; the other output rows are left unwritten."""
     B, S, n, D, pad = geo.B, geo.S, geo.n, geo.D, geo.pad
     st = _stream()
     xn = pool(B * n * D, tdtype).view(B, n, D)
@@ -385,12 +406,17 @@ def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, see
     with probe("qkv_gemm"):
         gemm(xn, prm["wqkv"], qkv, B * n, 3 * D, D, lda=D, ldb=D, ldc=0, dtype=dt_code,
              qkv=(B, geo.heads, DH, n, DH ** -0.5))
-    merged, state = nystrom_core_forward(qkv, geo, prm["wconv"], tdtype, dt_code, pool)
+    merged, state = nystrom_core_forward(qkv, geo, prm["wconv"], tdtype, dt_code, pool,
+                                         cls_row=pad if cls_only else None)
     Hout = pool(B * S * D).view(B * S, D)
-    gemm(merged, prm["wo"], Hout, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=dt_code, c_dtype=F32,
-         bias=prm["bo"], drop_p=drop_p, seed=seed, seed_ptr=seed_dev, resid=H, rowmap=(n, pad, S, 0, 0, 0))
+    if cls_only:
+        _lib.call("tm_cls_out_fwd", dt_code, _p(merged), _p(prm["wo"]), _p(prm["bo"]), _p(H), B, n, pad, S, D,
+                  C.c_float(drop_p), C.c_uint64(seed), _p(seed_dev), _p(Hout), st)
+    else:
+        gemm(merged, prm["wo"], Hout, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=dt_code, c_dtype=F32,
+             bias=prm["bo"], drop_p=drop_p, seed=seed, seed_ptr=seed_dev, resid=H, rowmap=(n, pad, S, 0, 0, 0))
     saved = dict(xn=xn, mean=mean, rstd=rstd, qkv=qkv, merged=merged, core=state, seed=seed, seed_dev=seed_dev,
-                 drop_p=drop_p)
+                 drop_p=drop_p, cls_only=cls_only)
     return Hout, saved
 
 
@@ -399,17 +425,26 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
     gradient of the layer input.  Parameter gradients go to ``grads``."""
     B, S, n, D, pad = geo.B, geo.S, geo.n, geo.D, geo.pad
     st = _stream()
-    dout = pool(B * n * D, tdtype).view(B, n, D)
-    _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
-              C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(dout), st)
-    # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
-    with defer_reductions():
-        weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code, work_pool=pool)
-        colsum(dout, B * n, D, D, dt_code, grads["bo"], pool)
-    dmerged = pool(B * n * D, tdtype).view(B, n, D)
-    gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
+    if saved["cls_only"]:
+        # dH is zero outside the class rows: dropout, dWo, dbo and dmerged on those rows only
+        dmerged = pool(B * D, tdtype).view(B, D)
+        _lib.call("tm_cls_out_bwd", dt_code, _p(dH), _p(saved["merged"]), _p(prm["wo"]), B, n, pad, S, D,
+                  C.c_float(saved["drop_p"]), C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(grads["wo"]),
+                  _p(grads["bo"]), _p(dmerged), st)
+    else:
+        dout = pool(B * n * D, tdtype).view(B, n, D)
+        _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
+                  C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(dout), st)
+        # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
+        with defer_reductions():
+            weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code,
+                        work_pool=pool)
+            colsum(dout, B * n, D, D, dt_code, grads["bo"], pool)
+        dmerged = pool(B * n * D, tdtype).view(B, n, D)
+        gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     dqkv = nystrom_core_backward(dmerged, saved["merged"], saved["qkv"], saved["core"], geo, prm["wconv"],
-                                 tdtype, dt_code, pool, grads["wconv"], DH ** -0.5)
+                                 tdtype, dt_code, pool, grads["wconv"], DH ** -0.5,
+                                 cls_row=pad if saved["cls_only"] else None)
     # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
     with defer_reductions():
         weight_grad(dqkv, saved["xn"], grads["wqkv"], 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
@@ -441,15 +476,18 @@ class TransMILEngine:
     ``fc1``: FC1_PLAIN (``in_features -> Linear+GELU``, code/models/TransMIL.py:128-133) or
     FC1_RCC2048 (``Linear(2048,1024)+GELU+LayerNorm(1024)+Linear(1024,512)+GELU``, :100-111).
     ``head``: parameter prefix of the class-token Linear (``_fc`` in TransMIL :155, ``_fc2`` in
-    code/models/MDMIL.py:73)."""
+    code/models/MDMIL.py:73).
+    ``cls_only``: layer 2's attention output / to_out forward and backward on the class rows only
+    (the logits read nothing else of it; clsrow.hip).  False runs them dense (same results)."""
 
-    def __init__(self, dtype: torch.dtype = torch.bfloat16, fc1=None, head="_fc"):
+    def __init__(self, dtype: torch.dtype = torch.bfloat16, fc1=None, head="_fc", cls_only=True):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("compute dtype must be torch.bfloat16 or torch.float32")
         self.tdtype = dtype
         self.dt_code = BF16 if dtype == torch.bfloat16 else F32
         self.fc1 = FC1_PLAIN if fc1 is None else fc1
         self.head = head
+        self.cls_only = cls_only
         _lib.lib()
 
     def _cast(self, w, pool):
@@ -589,7 +627,9 @@ class TransMILEngine:
         H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0], seed_dev)
         H2 = pool(B * geo.S * D).view(B * geo.S, D)
         _lib.call("tm_ppeg_fwd", _p(H1), B, geo.G, D, _p(prm["wfold"]), _p(prm["bfold"]), _p(H2), st)
-        H3, s2 = translayer_forward(H2, geo, prm[2], self.tdtype, self.dt_code, pool, drop_p, seeds[1], seed_dev)
+        # layer 2: the head reads its output only at the class rows (code/models/TransMIL.py:201-203)
+        H3, s2 = translayer_forward(H2, geo, prm[2], self.tdtype, self.dt_code, pool, drop_p, seeds[1], seed_dev,
+                                    cls_only=self.cls_only)
         Ccls = prm["fc_w"].shape[0]
         logits = torch.empty(B, Ccls, dtype=torch.float32, device=dev)
         xhat = pool(B * D)
