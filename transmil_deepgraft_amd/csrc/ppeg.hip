@@ -39,7 +39,7 @@ __global__ void ppeg_fold_kernel(const float* __restrict__ w7, const float* __re
 // coalesced row segment across the wave's 64 channels) for 784 FMAs.
 // grid (ceil(nCB/4) * D/64, nRB, B), block 256: wave w -> column block 4*bx + w.
 constexpr int RB = 4;
-constexpr int WRB = 2;  // row blocks per weight-gradient workgroup
+constexpr int WRB = 4;  // row blocks per weight-gradient workgroup
 
 template <bool BWD_DATA>
 __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ x, int S, int G, int D,
