@@ -7,8 +7,8 @@
 // ONE 7x7 depthwise stencil (w = w7 + pad(w5) + pad(w3) + delta, b = b7+b5+b3),
 // applied channel-last directly on the [B, S, D] fp32 residual stream: token
 // t = 1 + r*G + c (row-major, :71).  No transpose to NCHW, no padded copy.
-// Threads own (column group, channel): a wave covers 64 consecutive channels so
-// every tap load is one 256-B coalesced row segment.  HBM-bound.
+// Blocks own a tile of grid cells x 64 channels staged through LDS (one burst of coalesced
+// 256-B channel-row loads per window); HBM-bound.
 #include "common.h"
 #include "../../include/transmil_hip.h"
 
@@ -34,124 +34,143 @@ __global__ void ppeg_fold_kernel(const float* __restrict__ w7, const float* __re
   bf[ch] = b7[ch] + b5[ch] + b3[ch];
 }
 
-// Register-blocked stencil: a thread owns one channel and a 4x4 block of grid
-// cells; it streams the 10x10 input window once (100 loads, each a 256-B
-// coalesced row segment across the wave's 64 channels) for 784 FMAs.
-// grid (ceil(nCB/4) * D/64, nRB, B), block 256: wave w -> column block 4*bx + w.
-constexpr int RB = 4;
-constexpr int WRB = 4;  // row blocks per weight-gradient workgroup
+// LDS-tiled stencil: a 256-thread block owns a TR x TC tile of grid cells x 64 channels.  The
+// (TR + 6) x (TC + 6) input window (zero outside the grid) is requested in one burst of 16-B
+// loads (a wave covers 4 cells x 64 channels: four 256-B segments) into LDS [cell][64]; then
+// thread (channel, g) computes output rows 2g, 2g + 1 of the tile (16 cells x 49 taps) from LDS
+// (consecutive channels in consecutive banks) and stores 256-B channel rows.
+// grid (ceil(G / TC) * D / 64, ceil(G / TR), B), block 256.
+constexpr int TR = 8, TC = 8, WR = TR + KS - 1, WC = TC + KS - 1;  // 14 x 14 window
+constexpr int WIN = WR * WC;                                       // 196 cells
+constexpr int TILE_LDS = WIN * 64 * 4;                             // 50 KB
+
+// the block's input window into LDS (zero outside the G x G grid)
+TM_DEV void load_window(float* win, const float* __restrict__ xb, int G, int D, int r0, int c0) {
+  const int tid = threadIdx.x;
+  constexpr int PIECES = WIN * 16;              // 16-B pieces (4 channels each)
+  constexpr int PER = (PIECES + 255) / 256;     // 13: every load in flight before the first LDS write
+  f32x4 v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = u * 256 + tid, cell = i >> 4, c4 = (i & 15) * 4;
+    const int rr = r0 - R + cell / WC, cc = c0 - R + cell % WC;
+    v[u] = (i < PIECES && rr >= 0 && rr < G && cc >= 0 && cc < G)
+               ? *(const f32x4*)(xb + (size_t)(rr * G + cc) * D + c4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = u * 256 + tid;
+    if (i < PIECES) *(f32x4*)(win + (i >> 4) * 64 + (i & 15) * 4) = v[u];
+  }
+}
 
 template <bool BWD_DATA>
 __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ x, int S, int G, int D,
                                                            const float* __restrict__ wf, const float* __restrict__ bf,
                                                            float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float win[];
   const int nchunk = D / 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ch = (blockIdx.x % nchunk) * 64 + lane;
-  const int cb = (blockIdx.x / nchunk) * 4 + wave;
-  const int r0 = blockIdx.y * RB, c0 = cb * RB, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int chunk = blockIdx.x % nchunk, ch = chunk * 64 + lane;
+  const int r0 = blockIdx.y * TR, c0 = (blockIdx.x / nchunk) * TC, b = blockIdx.z;
   float* yb = y + (size_t)b * S * D;
-  if (blockIdx.x < (unsigned)nchunk && blockIdx.y == 0 && wave == 0) yb[ch] = x[(size_t)b * S * D + ch];  // class token
-  if (c0 >= G) return;
+  if (blockIdx.x < (unsigned)nchunk && blockIdx.y == 0 && g == 0) yb[ch] = x[(size_t)b * S * D + ch];  // class token
+  load_window(win, x + (size_t)b * S * D + D + chunk * 64, G, D, r0, c0);
   float w[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) w[t] = wf[(size_t)(BWD_DATA ? NT - 1 - t : t) * D + ch];
   const float bias = BWD_DATA ? 0.f : bf[ch];
-  float acc[RB][RB];
+  __syncthreads();
+  float acc[2][TC];
 #pragma unroll
-  for (int i = 0; i < RB; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < RB; ++j) acc[i][j] = bias;
-  const float* xb = x + (size_t)b * S * D + D + ch;  // grid token (0,0)
+    for (int j = 0; j < TC; ++j) acc[i][j] = bias;
 #pragma unroll
-  for (int ir = 0; ir < RB + KS - 1; ++ir) {
-    const int rr = r0 - R + ir;
-    if (rr < 0 || rr >= G) continue;
-    float xv[RB + KS - 1];
+  for (int ir = 0; ir < 2 + KS - 1; ++ir) {   // window rows 2g .. 2g + 7
+    float xv[WC];
 #pragma unroll
-    for (int ic = 0; ic < RB + KS - 1; ++ic) {
-      const int cc = c0 - R + ic;
-      xv[ic] = (cc >= 0 && cc < G) ? xb[((size_t)rr * G + cc) * D] : 0.f;
-    }
+    for (int ic = 0; ic < WC; ++ic) xv[ic] = win[((2 * g + ir) * WC + ic) * 64 + lane];
 #pragma unroll
-    for (int orow = 0; orow < RB; ++orow) {
+    for (int orow = 0; orow < 2; ++orow) {
       const int dy = ir - orow;
       if (dy < 0 || dy >= KS) continue;
 #pragma unroll
-      for (int oc = 0; oc < RB; ++oc)
+      for (int oc = 0; oc < TC; ++oc)
 #pragma unroll
         for (int dx = 0; dx < KS; ++dx) acc[orow][oc] = fmaf(w[dy * KS + dx], xv[oc + dx], acc[orow][oc]);
     }
   }
 #pragma unroll
-  for (int orow = 0; orow < RB; ++orow)
+  for (int orow = 0; orow < 2; ++orow)
 #pragma unroll
-    for (int oc = 0; oc < RB; ++oc) {
-      const int r = r0 + orow, c = c0 + oc;
+    for (int oc = 0; oc < TC; ++oc) {
+      const int r = r0 + 2 * g + orow, c = c0 + oc;
       if (r < G && c < G) yb[(size_t)(1 + r * G + c) * D + ch] = acc[orow][oc];
     }
 }
 
-// weight/bias gradient partials.  grid (ceil(nCB/4) * D/64, ceil(nRB/WRB), B), block 256:
-// a thread owns a channel and walks WRB row blocks of its column block; partial slab
-// index = (b * gridDim.y + by) * gridDim.x/nchunk + bx/nchunk, layout [slab][ch][50].
+// weight / bias gradient partials: dW[ch][tap] = sum_cells dy[cell][ch] x[cell + tap][ch],
+// db[ch] = sum_cells dy[cell][ch].  A block walks WT tiles along a row of tiles (x window and dy
+// tile through LDS, as the stencil), thread (channel, g) accumulating its 16 cells x 49 taps;
+// the 4 g partials are summed in order through LDS.  grid (ceil(nTC / WT) * D / 64, nTR, B),
+// partial slab index = (b * gridDim.y + by) * gridDim.x/nchunk + bx/nchunk, layout [slab][ch][50].
+constexpr int WT = 4;
+constexpr int DY_LDS = TR * TC * 64 * 4;   // 16 KB
 __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy_,
                                                          int S, int G, int D, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float win[];
+  float* dyt = win + WIN * 64;
   const int nchunk = D / 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int chunk = blockIdx.x % nchunk, ch = chunk * 64 + lane;
-  const int cb = (blockIdx.x / nchunk) * 4 + wave;
-  const int c0 = cb * RB, b = blockIdx.z;
-  const float* xb = x + (size_t)b * S * D + D + ch;
-  const float* gb = dy_ + (size_t)b * S * D + D + ch;
+  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+  const int chunk = blockIdx.x % nchunk;
+  const int r0 = blockIdx.y * TR, b = blockIdx.z;
+  const int ntc = (G + TC - 1) / TC;
+  const float* xb = x + (size_t)b * S * D + D + chunk * 64;
+  const float* gb = dy_ + (size_t)b * S * D + D + chunk * 64;
   float acc[NT + 1];
 #pragma unroll
   for (int t = 0; t <= NT; ++t) acc[t] = 0.f;
-  if (c0 < G) {
-    for (int rb = blockIdx.y * WRB; rb < blockIdx.y * WRB + WRB; ++rb) {
-      const int r0 = rb * RB;
-      if (r0 >= G) break;
-      float gv[RB][RB];
+  for (int tcol = (blockIdx.x / nchunk) * WT; tcol < min(ntc, (int)(blockIdx.x / nchunk) * WT + WT); ++tcol) {
+    const int c0 = tcol * TC;
+    __syncthreads();  // previous tile's LDS reads done
+    load_window(win, xb, G, D, r0, c0);
+    for (int i = tid; i < TR * TC * 16; i += 256) {
+      const int cell = i >> 4, c4 = (i & 15) * 4, rr = r0 + cell / TC, cc = c0 + cell % TC;
+      *(f32x4*)(dyt + cell * 64 + c4) = (rr < G && cc < G) ? *(const f32x4*)(gb + (size_t)(rr * G + cc) * D + c4)
+                                                            : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
 #pragma unroll
-      for (int orow = 0; orow < RB; ++orow)
+    for (int orow = 0; orow < 2; ++orow) {
+      const int tr = 2 * g + orow;
+      float gv[TC];
 #pragma unroll
-        for (int oc = 0; oc < RB; ++oc) {
-          const int r = r0 + orow, c = c0 + oc;
-          gv[orow][oc] = (r < G && c < G) ? gb[((size_t)r * G + c) * D] : 0.f;
-          acc[NT] += gv[orow][oc];
-        }
+      for (int oc = 0; oc < TC; ++oc) {
+        gv[oc] = dyt[(tr * TC + oc) * 64 + lane];
+        acc[NT] += gv[oc];
+      }
 #pragma unroll
-      for (int ir = 0; ir < RB + KS - 1; ++ir) {
-        const int rr = r0 - R + ir;
-        if (rr < 0 || rr >= G) continue;
-        float xv[RB + KS - 1];
+      for (int dy = 0; dy < KS; ++dy) {
+        float xv[WC];
 #pragma unroll
-        for (int ic = 0; ic < RB + KS - 1; ++ic) {
-          const int cc = c0 - R + ic;
-          xv[ic] = (cc >= 0 && cc < G) ? xb[((size_t)rr * G + cc) * D] : 0.f;
-        }
+        for (int ic = 0; ic < WC; ++ic) xv[ic] = win[((tr + dy) * WC + ic) * 64 + lane];
 #pragma unroll
-        for (int orow = 0; orow < RB; ++orow) {
-          const int dy = ir - orow;
-          if (dy < 0 || dy >= KS) continue;
+        for (int oc = 0; oc < TC; ++oc)
 #pragma unroll
-          for (int oc = 0; oc < RB; ++oc)
-#pragma unroll
-            for (int dx = 0; dx < KS; ++dx) acc[dy * KS + dx] = fmaf(gv[orow][oc], xv[oc + dx], acc[dy * KS + dx]);
-        }
+          for (int dx = 0; dx < KS; ++dx) acc[dy * KS + dx] = fmaf(gv[oc], xv[oc + dx], acc[dy * KS + dx]);
       }
     }
   }
-  __shared__ float red[4][64][NT + 1];
+  __syncthreads();
+  float* red = win;  // [4][64][NT + 1]
 #pragma unroll
-  for (int t = 0; t <= NT; ++t) red[wave][lane][t] = acc[t];
+  for (int t = 0; t <= NT; ++t) red[(g * 64 + lane) * (NT + 1) + t] = acc[t];
   __syncthreads();
   const int slab = (b * gridDim.y + blockIdx.y) * (gridDim.x / nchunk) + blockIdx.x / nchunk;
   float* dst = part + (size_t)slab * D * (NT + 1) + (size_t)chunk * 64 * (NT + 1);
-  for (int e = threadIdx.x; e < 64 * (NT + 1); e += 256) {
-    const int l = e / (NT + 1), t = e % (NT + 1);
-    dst[e] = (red[0][l][t] + red[1][l][t]) + (red[2][l][t] + red[3][l][t]);
-  }
+  for (int e = tid; e < 64 * (NT + 1); e += 256)
+    dst[e] = (red[e] + red[64 * (NT + 1) + e]) + (red[2 * 64 * (NT + 1) + e] + red[3 * 64 * (NT + 1) + e]);
 }
 
 // unfold folded gradients: dw7 = dwf, dw5 = centre 5x5, dw3 = centre 3x3, db* = db
@@ -182,16 +201,20 @@ extern "C" int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, c
 extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
                            void* stream) {
   TM_REQUIRE(x && y && x != y && D % 64 == 0 && G > 0, "ppeg_fwd: bad args");
-  const int ncb = (G + RB - 1) / RB;
-  const dim3 grid(((ncb + 3) / 4) * (D / 64), ncb, B);
-  ppeg_stencil_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(x, 1 + G * G, G, D, wfold, bfold, y);
+  const dim3 grid(((G + TC - 1) / TC) * (D / 64), (G + TR - 1) / TR, B);
+  ppeg_stencil_kernel<false><<<grid, 256, TILE_LDS, (hipStream_t)stream>>>(x, 1 + G * G, G, D, wfold, bfold, y);
   TM_CHECK_LAUNCH();
   return 0;
 }
 
+static dim3 wgrad_grid(int B, int G, int D) {
+  const int ntc = (G + TC - 1) / TC;
+  return dim3(((ntc + WT - 1) / WT) * (D / 64), (G + TR - 1) / TR, B);
+}
+
 static int ppeg_wgrad_slabs(int B, int G) {
-  const int ncb = (G + RB - 1) / RB;
-  return B * ((ncb + 3) / 4) * ((ncb + WRB - 1) / WRB);
+  const dim3 g = wgrad_grid(B, G, 64);
+  return (int)(g.x * g.y * g.z);
 }
 
 extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
@@ -205,10 +228,11 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
   TM_REQUIRE(x && dy && dx && dx != dy && D % 64 == 0, "ppeg_bwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   const int S = 1 + G * G;
-  const int ncb = (G + RB - 1) / RB;
-  ppeg_stencil_kernel<true><<<dim3(((ncb + 3) / 4) * (D / 64), ncb, B), 256, 0, st>>>(dy, S, G, D, wfold, nullptr, dx);
+  ppeg_stencil_kernel<true><<<dim3(((G + TC - 1) / TC) * (D / 64), (G + TR - 1) / TR, B), 256, TILE_LDS, st>>>(
+      dy, S, G, D, wfold, nullptr, dx);
   TM_CHECK_LAUNCH();
-  ppeg_wgrad_kernel<<<dim3(((ncb + 3) / 4) * (D / 64), (ncb + WRB - 1) / WRB, B), 256, 0, st>>>(x, dy, S, G, D, work);
+  tm_allow_smem(ppeg_wgrad_kernel, TILE_LDS + DY_LDS);
+  ppeg_wgrad_kernel<<<wgrad_grid(B, G, D), 256, TILE_LDS + DY_LDS, st>>>(x, dy, S, G, D, work);
   TM_CHECK_LAUNCH();
   if (int rc = tm_splitk_reduce(work, dwsum, ppeg_wgrad_slabs(B, G), (long long)D * 50, 1.0f, 0, stream)) return rc;
   ppeg_unfold_kernel<<<(D + 63) / 64, 64, 0, st>>>(dwsum, D, dw7, db7, dw5, db5, dw3, db3);
