@@ -1261,6 +1261,9 @@ struct ReduceEntry {
   int accumulate;
   float alpha;
   int vec;   // 1: 16-B units (count % 4 == 0, both pointers 16-B aligned)
+  int par;   // threads per output unit (power of 2 <= 64): each sums every par-th split, then a
+             // fixed xor-shuffle tree (entries with many splits and few outputs, e.g. LayerNorm
+             // weight partials of every 32-row block, would otherwise be one long serial loop)
 };
 struct ReduceTable {
   ReduceEntry e[DEFER_MAX];
@@ -1279,32 +1282,40 @@ __global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
   int e = 0;
   while ((int)blockIdx.x >= t.boff[e + 1]) ++e;
   const ReduceEntry r = t.e[e];
-  const long long u = (long long)(blockIdx.x - t.boff[e]) * 256 + threadIdx.x;
-  if (u >= t.off[e + 1] - t.off[e]) return;
+  const long long tt = (long long)(blockIdx.x - t.boff[e]) * 256 + threadIdx.x;
+  if (tt >= t.off[e + 1] - t.off[e]) return;  // whole groups of par lanes (par | 64) leave together
+  const int par = r.par, sub = (int)(tt & (par - 1));
+  const long long u = tt / par;
   constexpr int U = 12;
   if (r.vec) {
     const size_t j = (size_t)u * 4;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int z0 = 0; z0 < r.splits; z0 += U) {
+    for (int z0 = sub; z0 < r.splits; z0 += U * par) {
       f32x4 v[U];
 #pragma unroll
-      for (int k = 0; k < U; ++k) v[k] = *(const f32x4*)(r.slab + (size_t)min(z0 + k, r.splits - 1) * r.count + j);
+      for (int k = 0; k < U; ++k) v[k] = *(const f32x4*)(r.slab + (size_t)min(z0 + k * par, r.splits - 1) * r.count + j);
 #pragma unroll
-      for (int k = 0; k < U; ++k) s += (z0 + k < r.splits) ? v[k] : (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < U; ++k) s += (z0 + k * par < r.splits) ? v[k] : (f32x4){0.f, 0.f, 0.f, 0.f};
     }
+    for (int o = 1; o < par; o <<= 1)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], o, 64);
+    if (sub) return;
     s *= r.alpha;
     if (r.accumulate) s += *(const f32x4*)(r.out + j);
     *(f32x4*)(r.out + j) = s;
     return;
   }
   float s = 0.f;
-  for (int z0 = 0; z0 < r.splits; z0 += U) {
+  for (int z0 = sub; z0 < r.splits; z0 += U * par) {
     float v[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) v[k] = r.slab[(size_t)min(z0 + k, r.splits - 1) * r.count + u];
+    for (int k = 0; k < U; ++k) v[k] = r.slab[(size_t)min(z0 + k * par, r.splits - 1) * r.count + u];
 #pragma unroll
-    for (int k = 0; k < U; ++k) s += (z0 + k < r.splits) ? v[k] : 0.f;
+    for (int k = 0; k < U; ++k) s += (z0 + k * par < r.splits) ? v[k] : 0.f;
   }
+  for (int o = 1; o < par; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (sub) return;
   s *= r.alpha;
   if (r.accumulate) s += r.out[u];
   r.out[u] = s;
@@ -1335,9 +1346,14 @@ extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long 
     if (g_defer.n == DEFER_MAX)
       if (int rc = tm_reduce_flush(stream)) return rc;
     const int vec = count % 4 == 0 && ((uintptr_t)slab % 16) == 0 && ((uintptr_t)out % 16) == 0;
-    g_defer.e[g_defer.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha, vec};
-    // offsets count threads: one per 16-B unit when the entry allows it
-    g_defer.off[g_defer.n + 1] = g_defer.off[g_defer.n] + (vec ? count / 4 : count);
+    const long long units = vec ? count / 4 : count;
+    // threads per unit: enough that each sums <= 2 bursts of 12 splits, while the entry keeps
+    // to <= ~64 K threads
+    int par = 1;
+    while (par < 64 && (splits + par - 1) / par > 24 && units * par * 2 <= 65536) par <<= 1;
+    g_defer.e[g_defer.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha, vec, par};
+    // offsets count threads: par per 16-B unit (or element)
+    g_defer.off[g_defer.n + 1] = g_defer.off[g_defer.n] + units * par;
     ++g_defer.n;
     return 0;
   }
