@@ -197,7 +197,7 @@ def main():
 
     def body():
         loss = task.training_step((static_x, static_y, None))
-        loss.backward()
+        task.backward(loss)
         allreduce()
         opt.step()
 

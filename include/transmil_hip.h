@@ -87,9 +87,11 @@ int tm_layernorm_fwd(const float* x, const float* gamma, const float* beta, floa
                      int S, int n_pad, int pad, int dtype, void* y, float* mean, float* rstd, void* stream);
 long long tm_layernorm_bwd_workspace(int rows, int D, int rows_per_block);
 /* dx_accum[r] += LN'(dy) (dy read from the padded layout); dgamma/dbeta written */
+/* resid_cls_only != 0: dx_accum holds the residual gradient only at the class rows (row % S == 0);
+ * the other rows are written (=) without being read (the last layer's dL/dH, clsrow.hip) */
 int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const float* gamma, const float* mean,
                      const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
-                     float* dx_accum, float* work, float* dgamma, float* dbeta, void* stream);
+                     int resid_cls_only, float* dx_accum, float* work, float* dgamma, float* dbeta, void* stream);
 int tm_head_fwd(const float* h, int B, int S, int D, const float* gamma, const float* beta, float eps,
                 const float* W, const float* bias, int C, float* logits, float* xhat, float* rstd,
                 void* stream);

@@ -72,7 +72,7 @@ _SIGS = {
     "tm_colsum": (I, [P, I, I, I, I, I, P, P, I, P]),
     "tm_layernorm_fwd": (I, [P, P, P, Fl, I, I, I, I, I, I, P, P, P, P]),
     "tm_layernorm_bwd_workspace": (L, [I, I, I]),
-    "tm_layernorm_bwd": (I, [P, I, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P]),
+    "tm_layernorm_bwd": (I, [P, I, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P]),
     "tm_head_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P]),
     "tm_head_bwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "tm_nys_landmarks": (I, [I, P, P, I, I, P, P, P, P, P]),

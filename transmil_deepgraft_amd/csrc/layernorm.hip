@@ -86,7 +86,7 @@ template <typename T, int VPL>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, int rows, int S, int n_pad, int pad,
-                                                     int rows_per_block, float* __restrict__ dx_accum,
+                                                     int rows_per_block, int resid_cls_only, float* __restrict__ dx_accum,
                                                      float* __restrict__ part) {
   constexpr int D = VPL * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -101,7 +101,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     const int b = rr / S, t = rr % S;
     load_row_t<T, VPL>(g, dy + ((size_t)b * n_pad + pad + t) * D, lane);
     load_row<VPL>(xv, x + (size_t)rr * D, lane);
-    load_row<VPL>(acc, dx_accum + (size_t)rr * D, lane);
+    if (!resid_cls_only || t == 0) {
+      load_row<VPL>(acc, dx_accum + (size_t)rr * D, lane);
+    } else {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) acc[i] = 0.f;
+    }
     mu = mean[rr];
     rs = rstd[rr];
   };
@@ -280,17 +285,18 @@ extern "C" long long tm_layernorm_bwd_workspace(int rows, int D, int rows_per_bl
 
 extern "C" int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const float* gamma, const float* mean,
                                 const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
-                                float* dx_accum, float* work, float* dgamma, float* dbeta, void* stream) {
+                                int resid_cls_only, float* dx_accum, float* work, float* dgamma, float* dbeta,
+                                void* stream) {
   TM_REQUIRE(dy && x && gamma && mean && rstd && dx_accum && work && dgamma && dbeta, "layernorm_bwd: null arg");
   TM_REQUIRE(rows_per_block > 0 && S > 0, "layernorm_bwd: bad args");
   const int nb = (rows + rows_per_block - 1) / rows_per_block;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TM_BF16) {
     TM_VPL_DISPATCH(D, (ln_bwd_kernel<bf16, VPL><<<nb, 256, 0, st>>>((const bf16*)dy, x, gamma, mean, rstd, rows, S,
-                                                                     n_pad, pad, rows_per_block, dx_accum, work)));
+                                                                     n_pad, pad, rows_per_block, resid_cls_only, dx_accum, work)));
   } else {
     TM_VPL_DISPATCH(D, (ln_bwd_kernel<float, VPL><<<nb, 256, 0, st>>>((const float*)dy, x, gamma, mean, rstd, rows,
-                                                                      S, n_pad, pad, rows_per_block, dx_accum, work)));
+                                                                      S, n_pad, pad, rows_per_block, resid_cls_only, dx_accum, work)));
   }
   TM_CHECK_LAUNCH();
   int rc = tm_splitk_reduce(work, dgamma, nb, D, 1.0f, 0, stream);

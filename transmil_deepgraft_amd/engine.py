@@ -452,11 +452,12 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
     dxn = pool(B * n * D, tdtype).view(B, n, D)
     gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     # LayerNorm backward, accumulated into dH (residual branch already there)
-    rpb = 32
+    rpb = 8     # 2 rows per wave, both requested up front (the partials go through the deferred reduce)
     with defer_reductions():
         work = pool(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4)
         _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
-                  _p(saved["rstd"]), B * S, D, S, n, pad, rpb, _p(dH), _p(work), _p(grads["norm_w"]),
+                  _p(saved["rstd"]), B * S, D, S, n, pad, rpb, int(saved["cls_only"]), _p(dH), _p(work),
+                  _p(grads["norm_w"]),
                   _p(grads["norm_b"]), st)
 
 
@@ -655,7 +656,8 @@ class TransMILEngine:
         g = out if out is not None else {name: torch.empty_like(p, dtype=torch.float32)
                                          for name, p in params.items()}
         Ccls = prm["fc_w"].shape[0]
-        dH = torch.zeros(B * S, D, dtype=torch.float32, device=dev)
+        # layer 2 on the class rows reads dL/dH3 only there (its LayerNorm backward writes the rest)
+        dH = (torch.empty if self.cls_only else torch.zeros)(B * S, D, dtype=torch.float32, device=dev)
         _lib.call("tm_head_bwd", _p(dlogits.contiguous()), B, Ccls, S, D, _p(ctx["xhat"]), _p(ctx["hrstd"]),
                   _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g[self.head + ".weight"]),
                   _p(g[self.head + ".bias"]),
@@ -710,7 +712,7 @@ class TransMILEngine:
             rpb = 64
             work = pool(_lib.query("tm_layernorm_bwd_workspace", B * N, Fm, rpb) // 4)
             _lib.call("tm_layernorm_bwd", _p(dxln), F32, _p(inner["y0"]), _p(prm["ln0_w"]), _p(inner["mean0"]),
-                      _p(inner["rstd0"]), B * N, Fm, N, N, 0, rpb, _p(dy0), _p(work), _p(g[lnn + ".weight"]),
+                      _p(inner["rstd0"]), B * N, Fm, N, N, 0, rpb, 0, _p(dy0), _p(work), _p(g[lnn + ".weight"]),
                       _p(g[lnn + ".bias"]), st)
             dpre0 = pool(B * N * Fm, self.tdtype).view(B * N, Fm)
             _lib.call("tm_gelu_bwd", self.dt_code, _p(dy0), _p(inner["pre0"]), B * N * Fm, _p(dpre0), st)

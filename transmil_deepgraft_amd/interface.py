@@ -401,12 +401,15 @@ class _CrossEntropyOneHot(torch.autograd.Function):
         _lib.call("tm_ce_fwd", _p(lg), _p(lab), B, C, _p(loss), _p(prob), _p(yhat), _p(stats), _stream())
         ctx.save_for_backward(prob, lab)
         ctx.mark_non_differentiable(prob, yhat)
+        ctx.set_materialize_grads(False)    # no zero-filled gradients for prob / yhat (two launches)
         return loss, prob, yhat
 
     @staticmethod
     def backward(ctx, gloss, _gprob, _gyhat):
         from . import _lib
         from .engine import _p, _stream
+        if gloss is None:
+            return None, None, None
         prob, lab = ctx.saved_tensors
         B, C = prob.shape
         dl = torch.empty(B, C, device=prob.device)
@@ -460,6 +463,14 @@ class TransMILTask(nn.Module):
         self._last_loss = loss.detach()
         return loss
 
+    def backward(self, loss):
+        """``loss.backward()`` with the seed gradient taken from a persistent ones tensor (no
+        ``ones_like`` fill launch per step; Lightning's manual_backward equivalent)."""
+        one = getattr(self, "_one", None)
+        if one is None or one.device != loss.device or one.shape != loss.shape:
+            one = self._one = torch.ones_like(loss)
+        loss.backward(one)
+
     def optimization_step(self, batch, opt, allreduce=None):
         """One micro-batch of Lightning's automatic optimization with
         ``accumulate_grad_batches = K`` (code/train.py:199 uses K = 10 under DDP): the closure
@@ -472,7 +483,7 @@ class TransMILTask(nn.Module):
         if allreduce is not None:
             allreduce.sync = boundary
         loss = self.training_step(batch)
-        (loss / k if k > 1 else loss).backward()
+        self.backward(loss / k if k > 1 else loss)
         if boundary:
             if allreduce is not None:
                 allreduce()
