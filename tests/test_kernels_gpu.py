@@ -535,3 +535,27 @@ def test_a3_bwd_bf16_even_split(nbh, n):
         outs.append((dk.cpu(), dv.cpu(), dql.cpu()))
     for x, y in zip(*outs):
         assert _rel(x, y.double()) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("nbh,n", [(8, 256), (3, 1280), (8, 8448), (2, 33280)])
+def test_landmarks_segment_means(dtype, nbh, n):
+    """q~, k~ = means of l = n / 256 consecutive rows (App. A eq. 2) and their dtype copies."""
+    L = _lib()
+    from transmil_deepgraft_amd._lib import BF16, F32
+    from transmil_deepgraft_amd.engine import _p, _stream
+    g = torch.Generator(device="cpu").manual_seed(n + nbh)
+    q = torch.randn(nbh, n, 64, generator=g).to(dtype)
+    k = torch.randn(nbh, n, 64, generator=g).to(dtype)
+    l = n // 256
+    ref_q = q.double().view(nbh, 256, l, 64).mean(2)
+    ref_k = k.double().view(nbh, 256, l, 64).mean(2)
+    ql, kl = (torch.full((nbh, 256, 64), float("nan"), device=DEV) for _ in range(2))
+    qt, kt = (torch.empty(nbh, 256, 64, dtype=dtype, device=DEV) for _ in range(2))
+    qd, kd = q.to(DEV).contiguous(), k.to(DEV).contiguous()
+    L.call("tm_nys_landmarks", BF16 if dtype == torch.bfloat16 else F32, _p(qd), _p(kd), nbh, n, _p(ql), _p(kl),
+           _p(qt), _p(kt), _stream())
+    torch.cuda.synchronize()
+    assert (ql.cpu().double() - ref_q).abs().max().item() < 1e-5
+    assert (kl.cpu().double() - ref_k).abs().max().item() < 1e-5
+    assert torch.equal(qt.cpu(), ql.cpu().to(dtype)) and torch.equal(kt.cpu(), kl.cpu().to(dtype))

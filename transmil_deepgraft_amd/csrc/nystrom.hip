@@ -53,21 +53,54 @@ TM_DEV long long hoff(long long bh, int nh, long long bag_stride, long long head
 }
 
 // ---------------------------------------------------------------------------
-// landmarks: out[bh][j][d] = sum_{t<l} x[bh][j*l+t][d] / l ; grid (nbh, 64), block 256 (4 landmarks x 64 d)
+// landmarks: out[bh][j][d] = sum_{t<l} x[bh][j*l+t][d] / l ; grid (nbh, 32), block 256: thread
+// (landmark 8 blockIdx.y + tid / 32, d octet (tid / 4) % 8, row quarter tid % 4) sums its quarter of
+// the l rows with 8-wide loads (all of them in flight for l <= 36), then the 4 quarters meet by
+// xor shuffles in a fixed order.
 template <typename T>
-__global__ void landmarks_kernel(const T* __restrict__ q, const T* __restrict__ k, int n, int l,
-                                 float* __restrict__ ql, float* __restrict__ kl, T* __restrict__ ql_t,
-                                 T* __restrict__ kl_t) {
-  const int bh = blockIdx.x, j = blockIdx.y * 4 + (threadIdx.x >> 6), d = threadIdx.x & 63;
-  const T* qp = q + ((size_t)bh * n + (size_t)j * l) * DH + d;
-  const T* kp = k + ((size_t)bh * n + (size_t)j * l) * DH + d;
-  float sq = 0.f, sk = 0.f;
-  for (int t = 0; t < l; ++t) { sq += to_f(qp[(size_t)t * DH]); sk += to_f(kp[(size_t)t * DH]); }
+__global__ __launch_bounds__(256) void landmarks_kernel(const T* __restrict__ q, const T* __restrict__ k, int n,
+                                                        int l, float* __restrict__ ql, float* __restrict__ kl,
+                                                        T* __restrict__ ql_t, T* __restrict__ kl_t) {
+  const int bh = blockIdx.x, tid = threadIdx.x, tq = tid & 3, o = ((tid >> 2) & 7) * 8;
+  const int j = blockIdx.y * 8 + (tid >> 5);
+  const int per = (l + 3) / 4, t0 = tq * per, t1 = min(l, t0 + per);
+  const T* qp = q + ((size_t)bh * n + (size_t)j * l) * DH + o;
+  const T* kp = k + ((size_t)bh * n + (size_t)j * l) * DH + o;
+  float sq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sk[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int t = t0; t < t1; t += 9) {
+    vec8<T> a[9], b[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) {
+      const int tt = min(t + u, t1 - 1);
+      a[u] = load8(qp + (size_t)tt * DH);
+      b[u] = load8(kp + (size_t)tt * DH);
+    }
+#pragma unroll
+    for (int u = 0; u < 9; ++u)
+      if (t + u < t1)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { sq[e] += to_f(a[u][e]); sk[e] += to_f(b[u][e]); }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sq[e] += __shfl_xor(sq[e], 1, 64); sk[e] += __shfl_xor(sk[e], 1, 64);
+    sq[e] += __shfl_xor(sq[e], 2, 64); sk[e] += __shfl_xor(sk[e], 2, 64);
+  }
+  if (tq) return;
   const float inv_l = (float)l;
-  const size_t o = ((size_t)bh * NL + j) * DH + d;
-  const float vq = sq / inv_l, vk = sk / inv_l;
-  ql[o] = vq; kl[o] = vk;
-  ql_t[o] = from_f<T>(vq); kl_t[o] = from_f<T>(vk);
+  const size_t oo = ((size_t)bh * NL + j) * DH + o;
+  float vq[8], vk[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { vq[e] = sq[e] / inv_l; vk[e] = sk[e] / inv_l; }
+  *(f32x4*)(ql + oo) = (f32x4){vq[0], vq[1], vq[2], vq[3]};
+  *(f32x4*)(ql + oo + 4) = (f32x4){vq[4], vq[5], vq[6], vq[7]};
+  *(f32x4*)(kl + oo) = (f32x4){vk[0], vk[1], vk[2], vk[3]};
+  *(f32x4*)(kl + oo + 4) = (f32x4){vk[4], vk[5], vk[6], vk[7]};
+  vec8<T> tq8, tk8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { tq8[e] = from_f<T>(vq[e]); tk8[e] = from_f<T>(vk[e]); }
+  store8<T>(ql_t + oo, tq8);
+  store8<T>(kl_t + oo, tk8);
 }
 
 // ---------------------------------------------------------------------------
@@ -1710,7 +1743,7 @@ extern "C" int tm_nys_landmarks(int dtype, const void* q, const void* k, int nbh
                                 void* ql_t, void* kl_t, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0, "landmarks: n must be a positive multiple of 256");
   const int l = n / NL;
-  TM_DTYPE_DISPATCH(dtype, (landmarks_kernel<T><<<dim3(nbh, NL / 4), 256, 0, (hipStream_t)stream>>>(
+  TM_DTYPE_DISPATCH(dtype, (landmarks_kernel<T><<<dim3(nbh, NL / 8), 256, 0, (hipStream_t)stream>>>(
                                (const T*)q, (const T*)k, n, l, ql, kl, (T*)ql_t, (T*)kl_t)));
   TM_CHECK_LAUNCH();
   return 0;
