@@ -213,7 +213,8 @@ __global__ __launch_bounds__(256) void cls_out_bwd_kernel(const float* __restric
   }
 }
 
-// A1 row + conv33 backward: grid (nbh), block 256.  g = dmerged row (head slice), p = softmax
+// A1 row + conv33 backward: grid (nbh, 4), block 256; every block recomputes p, dp and dS (cheap,
+// L2-resident operands), then blockIdx.y picks one output: 0 dk~, 1 dY, 2 dq + dv window, 3 dwconv.  g = dmerged row (head slice), p = softmax
 // row (lse1), dp_j = g . Y_j, D1 = p . dp, dS_j = p_j (dp_j - D1):
 //   dq[bh][r] = sum_j dS_j k~_j  (the rest of dq is zero: the caller's buffer or dq_row consumers)
 //   dkl[bh][j] = dS_j q_r (=)      dy[bh][j] = p_j g (=)
@@ -250,21 +251,31 @@ __global__ __launch_bounds__(256) void a1_row_bwd_kernel(const T* __restrict__ d
   const float d1 = block_reduce_sum(pj * dp, red);
   const float ds = pj * (dp - d1);
   dss[tid] = ds;
-  // dk~ row j = dS_j q ; dY row j = p_j g
-  float* dklr = dkl + ((size_t)bh * NL + tid) * DH;
-  float* dyr = dy + ((size_t)bh * NL + tid) * DH;
+  const int role = blockIdx.y;
+  if (role == 0) {  // dk~ row j = dS_j q
+    float* dklr = dkl + ((size_t)bh * NL + tid) * DH;
 #pragma unroll
-  for (int c = 0; c < DH; c += 4) {
-    *(f32x4*)(dklr + c) = (f32x4){ds * qs[c], ds * qs[c + 1], ds * qs[c + 2], ds * qs[c + 3]};
-    *(f32x4*)(dyr + c) = (f32x4){pj * gs[c], pj * gs[c + 1], pj * gs[c + 2], pj * gs[c + 3]};
+    for (int c = 0; c < DH; c += 4)
+      *(f32x4*)(dklr + c) = (f32x4){ds * qs[c], ds * qs[c + 1], ds * qs[c + 2], ds * qs[c + 3]};
+    return;
   }
-  __syncthreads();
-  const float dqv = rows_dot(dss, kl_t + (size_t)bh * NL * DH, part);
-  if (tid < DH) dq[((size_t)bh * n + r) * DH + tid] = dqv;
-  // conv33 backward window
-  for (int i = tid; i < TAPS * DH; i += 256) {
-    const int tau = i / DH, dd = i % DH, t = r + tau - HALF;
-    if (t >= 0 && t < n) dv[((size_t)bh * n + t) * DH + dd] = wconv[h * TAPS + tau] * gs[dd];
+  if (role == 1) {  // dY row j = p_j g
+    float* dyr = dy + ((size_t)bh * NL + tid) * DH;
+#pragma unroll
+    for (int c = 0; c < DH; c += 4)
+      *(f32x4*)(dyr + c) = (f32x4){pj * gs[c], pj * gs[c + 1], pj * gs[c + 2], pj * gs[c + 3]};
+    return;
+  }
+  if (role == 2) {
+    __syncthreads();
+    const float dqv = rows_dot(dss, kl_t + (size_t)bh * NL * DH, part);
+    if (tid < DH) dq[((size_t)bh * n + r) * DH + tid] = dqv;
+    // conv33 backward window
+    for (int i = tid; i < TAPS * DH; i += 256) {
+      const int tau = i / DH, dd = i % DH, t = r + tau - HALF;
+      if (t >= 0 && t < n) dv[((size_t)bh * n + t) * DH + dd] = wconv[h * TAPS + tau] * gs[dd];
+    }
+    return;
   }
   if (b == 0) {
     // wave w: taps w, w + 4, ...; lanes = d; bags in index order
@@ -331,7 +342,7 @@ extern "C" int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, 
   TM_REQUIRE(dmerged && q && v && kl_t && y_t && lse1 && wconv && dq && dkl && dy && dv && dwconv && B > 0 && nh > 0,
              "cls_a1_row_bwd: bad args");
   TM_REQUIRE(n % NL == 0 && r >= 0 && r < n, "cls_a1_row_bwd: bad row / n");
-  TM_CLS_DISPATCH(dtype, (a1_row_bwd_kernel<T><<<B * nh, 256, 0, (hipStream_t)stream>>>(
+  TM_CLS_DISPATCH(dtype, (a1_row_bwd_kernel<T><<<dim3(B * nh, 4), 256, 0, (hipStream_t)stream>>>(
                              (const T*)dmerged, (const T*)q, (const T*)v, (const T*)kl_t, (const T*)y_t, lse1, wconv,
                              B, nh, n, r, dq, dkl, dy, dv, dwconv)));
   TM_CHECK_LAUNCH();
