@@ -247,6 +247,9 @@ int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, 
 /* dpre = dy * GELU'(pre) elementwise (fp32 dy / pre, dpre in dtype): the backward of the inner
  * Linear + GELU of the in_features = 2048 _fc1 branch (code/models/TransMIL.py:100-111) */
 int tm_gelu_bwd(int dtype, const float* dy, const float* pre, long long count, void* dpre, void* stream);
+/* y = max(a + b, 0) elementwise (the C5 encoder's residual add + ReLU, Bottleneck.forward,
+ * code/models/ResNet.py:97-124); 16-B aligned, y may alias a */
+int tm_add_relu(int dtype, const void* a, const void* b, void* y, long long count, void* stream);
 
 /* ---- class-row specialisation of the last TransLayer (clsrow.hip) -- code/models/TransMIL.py:195-203 ----
  * The logits read layer 2 only through the class token (norm(h)[:, 0]), which sits at row r = pad of

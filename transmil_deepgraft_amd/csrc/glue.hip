@@ -148,6 +148,23 @@ __global__ void cls_grad_kernel(const float* __restrict__ dH, int B, int S, int 
   }
 }
 
+// y = max(a + b, 0), elementwise over 8-element pieces (the C5 encoder's residual add + ReLU in
+// one pass instead of two; a and y may alias).  grid-stride, block 256.
+template <typename T>
+__global__ __launch_bounds__(256) void add_relu_kernel(const T* __restrict__ a, const T* __restrict__ b, T* y,
+                                                       long long count) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i + 8 <= count) {
+    const vec8<T> x = load8(a + i), z = load8(b + i);
+    vec8<T> o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f<T>(fmaxf(to_f(x[e]) + to_f(z[e]), 0.f));
+    store8<T>(y + i, o);
+  } else {
+    for (long long j = i; j < count; ++j) y[j] = from_f<T>(fmaxf(to_f(a[j]) + to_f(b[j]), 0.f));
+  }
+}
+
 }  // namespace
 
 // CrossEntropyLoss(logits, one_hot(label).float()) averaged over the B rows
@@ -304,6 +321,24 @@ extern "C" int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* str
   const long long threads = (off + 3) / 4;
   TM_DTYPE_DISPATCH(dtype, (cast_many_kernel<T><<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
                                *table)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_add_relu(int dtype, const void* a, const void* b, void* y, long long count, void* stream) {
+  TM_REQUIRE(a && b && y && count >= 0, "add_relu: bad args");
+  TM_REQUIRE(((uintptr_t)a % 16) == 0 && ((uintptr_t)b % 16) == 0 && ((uintptr_t)y % 16) == 0,
+             "add_relu: 16-B aligned buffers");
+  if (count == 0) return 0;
+  const unsigned blocks = (unsigned)((count + 2047) / 2048);
+  if (dtype == TM_BF16)
+    add_relu_kernel<bf16><<<blocks, 256, 0, (hipStream_t)stream>>>((const bf16*)a, (const bf16*)b, (bf16*)y, count);
+  else if (dtype == TM_F32)
+    add_relu_kernel<float><<<blocks, 256, 0, (hipStream_t)stream>>>((const float*)a, (const float*)b, (float*)y, count);
+  else {
+    tm_set_error("add_relu: dtype");
+    return 1;
+  }
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -60,6 +60,19 @@ def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, dtype, cl=True):
     return w.contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format), b
 
 
+def _add_relu_(y, idt):
+    """y = relu(y + idt) in place, one HIP pass (tm_add_relu) over two channels-last tensors."""
+    from . import _lib
+    from ._lib import BF16, F32
+    from .engine import _p, _stream
+    cl = torch.channels_last
+    if y.shape != idt.shape or y.dtype != idt.dtype or not (y.is_contiguous(memory_format=cl) and
+                                                            idt.is_contiguous(memory_format=cl)):
+        raise RuntimeError("add_relu: channels-last operands of one shape and dtype expected")
+    _lib.call("tm_add_relu", BF16 if y.dtype == torch.bfloat16 else F32, _p(y), _p(idt), _p(y), y.numel(), _stream())
+    return y
+
+
 class RetCCLResNet50(nn.Module):
     """``ResNet(Bottleneck, [3, 4, 6, 3])`` with ``fc = Identity``: tiles [n, 3, 224, 224] ->
     features [n, 2048] fp32."""
@@ -149,7 +162,7 @@ class RetCCLResNet50(nn.Module):
                 y = self._conv1x1(x, w1, b1, True)
                 y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
                 idt = x if d is None else self._conv1x1(x, d[0], d[1], False, d[2][0])
-                x = self._conv1x1(y, w3, b3, False).add_(idt).relu_()
+                x = _add_relu_(self._conv1x1(y, w3, b3, False), idt)
                 continue
             y = F.relu(F.conv2d(x, w1, b1))
             y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
