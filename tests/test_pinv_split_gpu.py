@@ -64,6 +64,8 @@ def test_sim2_softmax_split_matches_fp32():
     assert torch.equal(a2s[:nbh * 65536].view_as(a2), a2.to(torch.bfloat16))
     rec = a2s[:nbh * 65536].float() + a2s[nbh * 65536:].float()
     assert ((rec - a2.flatten()).abs() <= a2.flatten().abs() * 2.0 ** -16).all()
+    exact = torch.softmax(ql.double() @ kl.double().transpose(1, 2), -1)
+    assert ((a2.double() - exact).abs().max() / exact.abs().max()).item() < 1e-6
 
 
 @pytest.mark.parametrize("nbh", [8, 16, 24])

@@ -105,36 +105,40 @@ __global__ __launch_bounds__(256) void landmarks_kernel(const T* __restrict__ q,
 
 // ---------------------------------------------------------------------------
 // A2 = softmax_j(ql_i . kl_j), fp32 FMA.  grid (nbh, 256 / S2_ROWS), block 256: S2_ROWS rows per
-// block, thread = column j, which keeps row j of k~ (64 floats) in registers; the q~ rows are LDS
-// broadcasts.  (256 blocks: the 16-row version ran 128 blocks that each transposed all of k~
-// through LDS with scalar writes, 19-21 us.)
+// block, thread = column j.  k~ of the head arrives by coalesced 16-B loads (every load in flight
+// at once) and is transposed into LDS ([64][260] fp32: thread j reads column j, conflict-free);
+// the q~ rows are LDS broadcasts.
 // a2s (optional): the same values as bf16 hi / lo planes (hi = bf16(a), lo = bf16(a - hi); lo plane at
 // a2s + nbh * 256 * 256), the operand format of the split pseudo-inverse chain (pinv_split.hip).
-constexpr int S2_ROWS = 8;
+constexpr int S2_ROWS = 8, S2_KT = NL + 4;
 __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restrict__ ql, const float* __restrict__ kl,
                                                            float* __restrict__ a2, bf16* __restrict__ a2s) {
   const int bh = blockIdx.x, i0 = blockIdx.y * S2_ROWS, j = threadIdx.x, lane = j & 63, wave = j >> 6;
+  __shared__ float kt[DH * S2_KT];   // k~^T
   __shared__ float qs[S2_ROWS][DH];
   __shared__ float red[4][S2_ROWS];
-  const float* krow = kl + ((size_t)bh * NL + j) * DH;
-  f32x4 kr[DH / 4];
+  {
+    const float* kb = kl + (size_t)bh * NL * DH;
+    f32x4 v[16];
 #pragma unroll
-  for (int c = 0; c < DH / 4; ++c) kr[c] = *(const f32x4*)(krow + 4 * c);
+    for (int u = 0; u < 16; ++u) v[u] = *(const f32x4*)(kb + (size_t)(u * 256 + j) * 4);  // piece p: row p/16, d 4 (p%16)
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int p = u * 256 + j, row = p >> 4, d0 = (p & 15) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kt[(d0 + e) * S2_KT + row] = v[u][e];
+    }
+  }
   for (int e = threadIdx.x; e < S2_ROWS * DH; e += 256) qs[e / DH][e % DH] = ql[((size_t)bh * NL + i0) * DH + e];
   __syncthreads();
   float s[S2_ROWS];
 #pragma unroll
   for (int r = 0; r < S2_ROWS; ++r) s[r] = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < DH; ++c) {
+    const float kv = kt[c * S2_KT + j];
 #pragma unroll
-  for (int c = 0; c < DH / 4; ++c) {
-#pragma unroll
-    for (int r = 0; r < S2_ROWS; ++r) {
-      const f32x4 q4 = *(const f32x4*)&qs[r][4 * c];
-      s[r] = fmaf(q4[0], kr[c][0], s[r]);
-      s[r] = fmaf(q4[1], kr[c][1], s[r]);
-      s[r] = fmaf(q4[2], kr[c][2], s[r]);
-      s[r] = fmaf(q4[3], kr[c][3], s[r]);
-    }
+    for (int r = 0; r < S2_ROWS; ++r) s[r] = fmaf(qs[r][c], kv, s[r]);
   }
   // row max
 #pragma unroll
