@@ -202,9 +202,12 @@ int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, const float*
 int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
                 void* stream);
 long long tm_ppeg_bwd_workspace(int B, int G, int D);
+/* dout (nullable): also writes the padded to_out-dropout gradient of the TransLayer below from dx
+ * (as tm_dropout_bwd_pad with the same dtype / n_pad / pad / p / seed / seed_ptr) */
 int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const float* wfold, float* dx,
                 float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
-                float* db3, void* stream);
+                float* db3, int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
+                const uint64_t* seed_ptr, void* stream);
 
 /* ---- AttMIL gated attention pooling (attmil.hip) -- code/models/AttMIL.py:88-110 ----
  * Z [N, 2D] = H [Wv;Wu]^T + [bv;bu] (caller's GEMM), H [N, L], w [D] / b [1] = attention_weights,

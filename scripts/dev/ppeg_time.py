@@ -1,6 +1,7 @@
 """Time the PPEG stencil forward / backward (+ weight gradient) at the bench shape (G = 91, D = 512)."""
 import sys, os, time
 sys.path.insert(0, os.getcwd())
+import ctypes as C
 import torch
 from transmil_deepgraft_amd import _lib
 from transmil_deepgraft_amd.engine import _p, _stream
@@ -34,7 +35,8 @@ g7, g5, g3 = (torch.empty(D, k * k, device=dev) for k in (7, 5, 3))
 gb7, gb5, gb3 = (torch.empty(D, device=dev) for _ in range(3))
 f = lambda: _lib.call("tm_ppeg_fwd", _p(x), B, G, D, _p(wf), _p(bf), _p(y), _stream())
 bwd = lambda: _lib.call("tm_ppeg_bwd", _p(x), _p(dy), B, G, D, _p(wf), _p(dx), _p(work), _p(dws), _p(g7), _p(gb7),
-                        _p(g5), _p(gb5), _p(g3), _p(gb3), _stream())
+                        _p(g5), _p(gb5), _p(g3), _p(gb3), 0, None, 0, 0, C.c_float(0.0), C.c_uint64(0), None,
+                        _stream())
 mb = S * D * 4 * 2 / 1e6
 tf, tb = timeit(f), timeit(bwd)
 print(f"ppeg fwd {tf:6.2f} us ({mb / tf:5.2f} TB/s on {mb:.1f} MB)   bwd (data + weights) {tb:6.2f} us", flush=True)

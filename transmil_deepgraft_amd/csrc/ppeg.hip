@@ -64,17 +64,49 @@ TM_DEV void load_window(float* win, const float* __restrict__ xb, int G, int D, 
   }
 }
 
+// Backward only, optional: the next layer-backward's first step fused into the stencil's stores --
+// dout[b][pad + t][c] = T(keep(b*S + t, c) * scale * dx[b*S + t][c]) and zero pad rows, the
+// padded to_out-dropout gradient of the TransLayer below (as tm_dropout_bwd_pad).
+struct DropPad {
+  void* out;        // null: off
+  int dtype, n_pad, pad;
+  float p, scale;
+  uint64_t seed0;
+  const uint64_t* seed_ptr;
+};
+
+TM_DEV void droppad_store(const DropPad& dp, uint64_t seed, int b, int S, int D, int t, int ch, float v) {
+  if (dp.p > 0.f) v = dropout_u01(seed, (uint32_t)(b * S + t), (uint32_t)ch) >= dp.p ? v * dp.scale : 0.f;
+  const size_t o = ((size_t)b * dp.n_pad + dp.pad + t) * D + ch;
+  if (dp.dtype == TM_BF16) ((bf16*)dp.out)[o] = (bf16)v;
+  else ((float*)dp.out)[o] = v;
+}
+
 template <bool BWD_DATA>
 __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ x, int S, int G, int D,
                                                            const float* __restrict__ wf, const float* __restrict__ bf,
-                                                           float* __restrict__ y) {
+                                                           float* __restrict__ y, DropPad dp) {
   extern __shared__ __attribute__((aligned(16))) float win[];
   const int nchunk = D / 64;
   const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
   const int chunk = blockIdx.x % nchunk, ch = chunk * 64 + lane;
   const int r0 = blockIdx.y * TR, c0 = (blockIdx.x / nchunk) * TC, b = blockIdx.z;
   float* yb = y + (size_t)b * S * D;
-  if (blockIdx.x < (unsigned)nchunk && blockIdx.y == 0 && g == 0) yb[ch] = x[(size_t)b * S * D + ch];  // class token
+  const bool fuse = BWD_DATA && dp.out != nullptr;
+  const uint64_t seed = fuse && dp.p > 0.f ? effective_seed(dp.seed0, dp.seed_ptr) : 0;
+  if (blockIdx.x < (unsigned)nchunk && blockIdx.y == 0) {
+    if (g == 0) {  // class token passes through
+      const float v = x[(size_t)b * S * D + ch];
+      yb[ch] = v;
+      if (fuse) droppad_store(dp, seed, b, S, D, 0, ch, v);
+    }
+    if (fuse)  // the front pad rows of dout are zero
+      for (int t = g; t < dp.pad; t += 4) {
+        const size_t o = ((size_t)b * dp.n_pad + t) * D + ch;
+        if (dp.dtype == TM_BF16) ((bf16*)dp.out)[o] = (bf16)0.f;
+        else ((float*)dp.out)[o] = 0.f;
+      }
+  }
   load_window(win, x + (size_t)b * S * D + D + chunk * 64, G, D, r0, c0);
   float w[NT];
 #pragma unroll
@@ -106,7 +138,10 @@ __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restri
 #pragma unroll
     for (int oc = 0; oc < TC; ++oc) {
       const int r = r0 + 2 * g + orow, c = c0 + oc;
-      if (r < G && c < G) yb[(size_t)(1 + r * G + c) * D + ch] = acc[orow][oc];
+      if (r < G && c < G) {
+        yb[(size_t)(1 + r * G + c) * D + ch] = acc[orow][oc];
+        if (fuse) droppad_store(dp, seed, b, S, D, 1 + r * G + c, ch, acc[orow][oc]);
+      }
     }
 }
 
@@ -202,7 +237,8 @@ extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfo
                            void* stream) {
   TM_REQUIRE(x && y && x != y && D % 64 == 0 && G > 0, "ppeg_fwd: bad args");
   const dim3 grid(((G + TC - 1) / TC) * (D / 64), (G + TR - 1) / TR, B);
-  ppeg_stencil_kernel<false><<<grid, 256, TILE_LDS, (hipStream_t)stream>>>(x, 1 + G * G, G, D, wfold, bfold, y);
+  ppeg_stencil_kernel<false><<<grid, 256, TILE_LDS, (hipStream_t)stream>>>(x, 1 + G * G, G, D, wfold, bfold, y,
+                                                                          DropPad{});
   TM_CHECK_LAUNCH();
   return 0;
 }
@@ -224,12 +260,16 @@ extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
 // dy: [B,S,D] upstream gradient; x: PPEG input.  dx written (=); weight grads written.
 extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const float* wfold, float* dx,
                            float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
-                           float* db3, void* stream) {
+                           float* db3, int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
+                           const uint64_t* seed_ptr, void* stream) {
   TM_REQUIRE(x && dy && dx && dx != dy && D % 64 == 0, "ppeg_bwd: bad args");
+  TM_REQUIRE(!dout || ((dtype == TM_BF16 || dtype == TM_F32) && n_pad >= pad + 1 + G * G && pad >= 0),
+             "ppeg_bwd: bad dropout-pad output");
   hipStream_t st = (hipStream_t)stream;
   const int S = 1 + G * G;
+  const DropPad dp{dout, dtype, n_pad, pad, p, p > 0.f ? 1.f / (1.f - p) : 1.f, seed, seed_ptr};
   ppeg_stencil_kernel<true><<<dim3(((G + TC - 1) / TC) * (D / 64), (G + TR - 1) / TR, B), 256, TILE_LDS, st>>>(
-      dy, S, G, D, wfold, nullptr, dx);
+      dy, S, G, D, wfold, nullptr, dx, dp);
   TM_CHECK_LAUNCH();
   tm_allow_smem(ppeg_wgrad_kernel, TILE_LDS + DY_LDS);
   ppeg_wgrad_kernel<<<wgrad_grid(B, G, D), 256, TILE_LDS + DY_LDS, st>>>(x, dy, S, G, D, work);

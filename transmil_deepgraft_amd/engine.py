@@ -420,9 +420,10 @@ def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, see
     return Hout, saved
 
 
-def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_code, pool):
+def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_code, pool, dout=None):
     """dH [B*S, D] fp32 (gradient of the layer output) is turned IN PLACE into the
-    gradient of the layer input.  Parameter gradients go to ``grads``."""
+    gradient of the layer input.  Parameter gradients go to ``grads``.  ``dout``: the padded
+    to_out-dropout gradient, already written by the producer of dH (tm_ppeg_bwd)."""
     B, S, n, D, pad = geo.B, geo.S, geo.n, geo.D, geo.pad
     st = _stream()
     if saved["cls_only"]:
@@ -432,9 +433,10 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
                   C.c_float(saved["drop_p"]), C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(grads["wo"]),
                   _p(grads["bo"]), _p(dmerged), st)
     else:
-        dout = pool(B * n * D, tdtype).view(B, n, D)
-        _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
-                  C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(dout), st)
+        if dout is None:
+            dout = pool(B * n * D, tdtype).view(B, n, D)
+            _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
+                      C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(dout), st)
         # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
         with defer_reductions():
             weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code,
@@ -662,20 +664,25 @@ class TransMILEngine:
                   _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g[self.head + ".weight"]),
                   _p(g[self.head + ".bias"]),
                   _p(g["norm.weight"]), _p(g["norm.bias"]), _p(dH), st)
+        dout1 = None
         for li, Hin, saved in ((2, ctx["H2"], ctx["s2"]), (1, ctx["H0"], ctx["s1"])):
             pre = f"layer{li}."
             gl = {"wo": g[pre + "attn.to_out.0.weight"], "bo": g[pre + "attn.to_out.0.bias"],
                   "wqkv": g[pre + "attn.to_qkv.weight"], "wconv": g[pre + "attn.res_conv.weight"],
                   "norm_w": g[pre + "norm.weight"], "norm_b": g[pre + "norm.bias"]}
-            translayer_backward(dH, Hin, saved, geo, prm[li], gl, self.tdtype, self.dt_code, pool)
+            translayer_backward(dH, Hin, saved, geo, prm[li], gl, self.tdtype, self.dt_code, pool, dout=dout1)
             if li == 2:
                 dH1 = pool(B * S * D).view(B * S, D)
                 work = pool(_lib.query("tm_ppeg_bwd_workspace", B, geo.G, D) // 4)
                 dwsum = pool(D * 50)
+                # the stencil also writes layer 1's padded to_out-dropout gradient (its first step)
+                s1 = ctx["s1"]
+                dout1 = pool(B * geo.n * D, self.tdtype).view(B, geo.n, D)
                 _lib.call("tm_ppeg_bwd", _p(ctx["H1"]), _p(dH), B, geo.G, D, _p(prm["wfold"]), _p(dH1), _p(work),
                           _p(dwsum), _p(g["pos_layer.proj.weight"]), _p(g["pos_layer.proj.bias"]),
                           _p(g["pos_layer.proj1.weight"]), _p(g["pos_layer.proj1.bias"]),
-                          _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), st)
+                          _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), self.dt_code, _p(dout1),
+                          geo.n, geo.pad, C.c_float(s1["drop_p"]), C.c_uint64(s1["seed"]), _p(s1["seed_dev"]), st)
                 dH = dH1
                 flush_reductions()     # head, norm, layer2 and PPEG parameter gradients final
                 if ready is not None:
