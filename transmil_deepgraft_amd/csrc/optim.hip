@@ -58,7 +58,31 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
                                                                       int* __restrict__ counters, float beta1,
                                                                       float beta2, float eps, int la_k,
                                                                       float la_alpha) {
-  __shared__ int s_ti;
+  // the element loads go out first: nothing they address depends on the step counters, so the
+  // counter load and the bias-correction math overlap them (no LDS hand-off or barrier)
+  const long long total = tab.offset[tab.count];
+  const long long blk0 = (long long)blockIdx.x * OPT_PER_BLOCK;
+  const long long i0 = blk0 + 4LL * threadIdx.x;
+  if (i0 >= total) return;
+  int ti = 0;
+  while (ti < tab.count - 1 && blk0 >= tab.offset[ti + 1]) ++ti;  // block-uniform
+  while (i0 >= tab.offset[ti + 1]) ++ti;
+  const tm_optim_tensor& T = tab.t[ti];
+  const long long j0 = i0 - tab.offset[ti];
+  const int n = (int)min(4LL, T.numel - j0);   // the tensor's padding tail: n < 4 (or <= 0)
+  if (n <= 0) return;
+  const bool vec = n == 4 && ((uintptr_t)(T.param + j0) % 16) == 0 && ((uintptr_t)(T.grad + j0) % 16) == 0;
+  f32x4 m4 = *(const f32x4*)(exp_avg + i0), v4 = *(const f32x4*)(exp_avg_sq + i0);
+  f32x4 p4, g4, s4 = {0.f, 0.f, 0.f, 0.f};
+  if (vec) {
+    p4 = *(const f32x4*)(T.param + j0);
+    g4 = *(const f32x4*)(T.grad + j0);
+  } else {
+    for (int e = 0; e < 4; ++e) {
+      p4[e] = e < n ? T.param[j0 + e] : 0.f;
+      g4[e] = e < n ? T.grad[j0 + e] : 0.f;
+    }
+  }
   const float step = (float)counters[0];
   const int la_step = counters[1];
   RAdamScal r;
@@ -72,56 +96,26 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
                         : 0.0f;
   r.sync = la_k > 0 && la_step % la_k == 0;
   r.first_sync = la_step <= la_k;
-  const long long total = tab.offset[tab.count];
-  const long long blk0 = (long long)blockIdx.x * OPT_PER_BLOCK;
-  if (threadIdx.x == 0) {
-    int t = 0;
-    while (t < tab.count - 1 && blk0 >= tab.offset[t + 1]) ++t;
-    s_ti = t;
-  }
-  __syncthreads();
-  const long long i0 = blk0 + 4LL * threadIdx.x;
-  if (i0 < total) {
-    int ti = s_ti;
-    while (i0 >= tab.offset[ti + 1]) ++ti;
-    const tm_optim_tensor& T = tab.t[ti];
-    const long long j0 = i0 - tab.offset[ti];
-    const int n = (int)min(4LL, T.numel - j0);   // the tensor's padding tail: n < 4 (or <= 0)
-    if (n > 0) {
-      const bool vec = n == 4 && ((uintptr_t)(T.param + j0) % 16) == 0 && ((uintptr_t)(T.grad + j0) % 16) == 0;
-      f32x4 m4 = *(const f32x4*)(exp_avg + i0), v4 = *(const f32x4*)(exp_avg_sq + i0);
-      f32x4 p4, g4, s4 = {0.f, 0.f, 0.f, 0.f};
-      if (vec) {
-        p4 = *(const f32x4*)(T.param + j0);
-        g4 = *(const f32x4*)(T.grad + j0);
-      } else {
-        for (int e = 0; e < 4; ++e) {
-          p4[e] = e < n ? T.param[j0 + e] : 0.f;
-          g4[e] = e < n ? T.grad[j0 + e] : 0.f;
-        }
-      }
-      if (r.sync && !r.first_sync) s4 = *(const f32x4*)(slow + i0);
+  if (r.sync && !r.first_sync) s4 = *(const f32x4*)(slow + i0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float m = m4[e], v = v4[e];
-        float p = radam_elem(p4[e], g4[e], m, v, r, T.lr, T.weight_decay, beta1, beta2, eps);
-        if (r.sync) {
-          p = r.first_sync ? p : s4[e] + la_alpha * (p - s4[e]);
-          s4[e] = p;
-        }
-        m4[e] = m;
-        v4[e] = v;
-        p4[e] = p;
-      }
-      *(f32x4*)(exp_avg + i0) = m4;
-      *(f32x4*)(exp_avg_sq + i0) = v4;
-      if (r.sync) *(f32x4*)(slow + i0) = s4;
-      if (vec) {
-        *(f32x4*)(T.param + j0) = p4;
-      } else {
-        for (int e = 0; e < n; ++e) T.param[j0 + e] = p4[e];
-      }
+  for (int e = 0; e < 4; ++e) {
+    float m = m4[e], v = v4[e];
+    float p = radam_elem(p4[e], g4[e], m, v, r, T.lr, T.weight_decay, beta1, beta2, eps);
+    if (r.sync) {
+      p = r.first_sync ? p : s4[e] + la_alpha * (p - s4[e]);
+      s4[e] = p;
     }
+    m4[e] = m;
+    v4[e] = v;
+    p4[e] = p;
+  }
+  *(f32x4*)(exp_avg + i0) = m4;
+  *(f32x4*)(exp_avg_sq + i0) = v4;
+  if (r.sync) *(f32x4*)(slow + i0) = s4;
+  if (vec) {
+    *(f32x4*)(T.param + j0) = p4;
+  } else {
+    for (int e = 0; e < n; ++e) T.param[j0 + e] = p4[e];
   }
 }
 

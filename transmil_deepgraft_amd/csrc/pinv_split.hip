@@ -480,16 +480,25 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
                                                              long long plane, const float* __restrict__ part, int nbh,
                                                              const float* __restrict__ dXc, int softmax,
                                                              float* __restrict__ out) {
-  __shared__ float tile[NL][17];
   __shared__ float red[4][16];
   __shared__ float bc[4];
   const int bh = blockIdx.x, i0 = blockIdx.y * 16, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const size_t hb = (size_t)bh * MAT;
-  // G0[j][i0 + ii] -> tile[j][ii]
-  for (int e = t; e < NL * 16; e += 256) {
-    const int j = e >> 4, ii = e & 15;
-    const size_t o = hb + (size_t)j * NL + i0 + ii;
-    tile[j][ii] = (float)G0[o] + (float)G0[o + plane];
+  // every load is issued up front (one memory round trip): G0[t][i0..i0+15] (the transpose term of
+  // column t, 32 contiguous bytes per plane), X and dXc rows i0..i0+15 at column t, the sums
+  float g0[16], xv[16], dx[16];
+  {
+    const size_t o = hb + (size_t)t * NL + i0;
+    const bf16x8 h0 = *(const bf16x8*)(G0 + o), h1 = *(const bf16x8*)(G0 + o + 8);
+    const bf16x8 l0 = *(const bf16x8*)(G0 + plane + o), l1 = *(const bf16x8*)(G0 + plane + o + 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { g0[e] = (float)h0[e] + (float)l0[e]; g0[8 + e] = (float)h1[e] + (float)l1[e]; }
+  }
+#pragma unroll
+  for (int ii = 0; ii < 16; ++ii) {
+    const size_t off = hb + (size_t)(i0 + ii) * NL + t;
+    xv[ii] = X[off];
+    dx[ii] = dXc[off];
   }
   // maxima, tie counts and the fixed-order sum of the partial dots
   float mc = -INFINITY, mr = -INFINITY;
@@ -497,6 +506,12 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
   float nc = 0.f, nr = 0.f, ps = 0.f;
   for (int e = t; e < nbh * NL; e += 256) { nc += sums[e] == mc; nr += sums[nbh * NL + e] == mr; }
   for (int e = t; e < nbh * 16; e += 256) ps += part[e];
+  const float* rs = sums + (size_t)bh * NL;
+  const float* cs = sums + (size_t)(nbh + bh) * NL;
+  const float csv = cs[t];
+  float rsv[16];
+#pragma unroll
+  for (int ii = 0; ii < 16; ++ii) rsv[ii] = rs[i0 + ii];
   nc = wave_sum(nc); nr = wave_sum(nr); ps = wave_sum(ps);
   if (lane == 0) { red[wave][0] = nc; red[wave][1] = nr; red[wave][2] = ps; }
   __syncthreads();
@@ -509,18 +524,12 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
   const float c = mc * mr, ic = 1.f / c;
   const float dc = -bc[2] * ic * ic;
   const float dMc = dc * mr / bc[0], dMr = dc * mc / bc[1];
-  const float* rs = sums + (size_t)bh * NL;
-  const float* cs = sums + (size_t)(nbh + bh) * NL;
-  const float tie_r = cs[t] == mr ? dMr : 0.f;
-  float dx[16], xv[16];
+  const float tie_r = csv == mr ? dMr : 0.f;
 #pragma unroll
   for (int ii = 0; ii < 16; ++ii) {
-    const int i = i0 + ii;
-    const size_t off = hb + (size_t)i * NL + t;
-    xv[ii] = X[off];
     const float sg = xv[ii] > 0.f ? 1.f : (xv[ii] < 0.f ? -1.f : 0.f);
-    const float tie_c = rs[i] == mc ? dMc : 0.f;
-    dx[ii] = dXc[off] + tile[t][ii] * ic + sg * (tie_c + tie_r);
+    const float tie_c = rsv[ii] == mc ? dMc : 0.f;
+    dx[ii] = dx[ii] + g0[ii] * ic + sg * (tie_c + tie_r);
   }
   if (!softmax) {
 #pragma unroll
