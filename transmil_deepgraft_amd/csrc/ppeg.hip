@@ -83,7 +83,7 @@ TM_DEV void droppad_store(const DropPad& dp, uint64_t seed, int b, int S, int D,
 }
 
 template <bool BWD_DATA>
-__global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ x, int S, int G, int D,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void ppeg_stencil_kernel(const float* __restrict__ x, int S, int G, int D,
                                                            const float* __restrict__ wf, const float* __restrict__ bf,
                                                            float* __restrict__ y, DropPad dp) {
   extern __shared__ __attribute__((aligned(16))) float win[];
