@@ -25,7 +25,7 @@
 
 namespace {
 
-constexpr int OPT_THREADS = 256, OPT_PER_BLOCK = OPT_THREADS * 4;
+constexpr int OPT_THREADS = 256, OPT_PIECES = 2, OPT_PER_BLOCK = OPT_THREADS * 4 * OPT_PIECES;
 
 __global__ void optim_tick_kernel(int* counters) {
   counters[0] += 1;
@@ -58,29 +58,51 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
                                                                       int* __restrict__ counters, float beta1,
                                                                       float beta2, float eps, int la_k,
                                                                       float la_alpha) {
-  // the element loads go out first: nothing they address depends on the step counters, so the
-  // counter load and the bias-correction math overlap them (no LDS hand-off or barrier)
+  // each thread updates OPT_PIECES 4-element pieces (a block's pieces OPT_THREADS*4 apart, so
+  // every load is coalesced).  The tensor of a piece is found wave-uniformly (scalar loads of the
+  // table; a per-lane search indexes the kernarg table with vector loads, a dependent round trip
+  // per level ahead of the element loads); a wave that straddles a tensor boundary walks the few
+  // tensors it touches.  Every element load goes out before the counters are read and before any store (a
+  // param store of one piece could alias another piece's loads).
   const long long total = tab.offset[tab.count];
   const long long blk0 = (long long)blockIdx.x * OPT_PER_BLOCK;
-  const long long i0 = blk0 + 4LL * threadIdx.x;
-  if (i0 >= total) return;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int ti = 0;
-  while (ti < tab.count - 1 && blk0 >= tab.offset[ti + 1]) ++ti;  // block-uniform
-  while (i0 >= tab.offset[ti + 1]) ++ti;
-  const tm_optim_tensor& T = tab.t[ti];
-  const long long j0 = i0 - tab.offset[ti];
-  const int n = (int)min(4LL, T.numel - j0);   // the tensor's padding tail: n < 4 (or <= 0)
-  if (n <= 0) return;
-  const bool vec = n == 4 && ((uintptr_t)(T.param + j0) % 16) == 0 && ((uintptr_t)(T.grad + j0) % 16) == 0;
-  f32x4 m4 = *(const f32x4*)(exp_avg + i0), v4 = *(const f32x4*)(exp_avg_sq + i0);
-  f32x4 p4, g4, s4 = {0.f, 0.f, 0.f, 0.f};
-  if (vec) {
-    p4 = *(const f32x4*)(T.param + j0);
-    g4 = *(const f32x4*)(T.grad + j0);
-  } else {
-    for (int e = 0; e < 4; ++e) {
-      p4[e] = e < n ? T.param[j0 + e] : 0.f;
-      g4[e] = e < n ? T.grad[j0 + e] : 0.f;
+  struct Piece { float* param; long long j0; float lr, wd; int n; bool vec; };
+  long long i0[OPT_PIECES];
+  Piece pc[OPT_PIECES];
+  f32x4 m4[OPT_PIECES], v4[OPT_PIECES], p4[OPT_PIECES], g4[OPT_PIECES], s4[OPT_PIECES];
+#pragma unroll
+  for (int u = 0; u < OPT_PIECES; ++u) {
+    const long long wbase = blk0 + (long long)u * OPT_THREADS * 4 + wave * 256;  // wave-uniform
+    i0[u] = wbase + 4 * (threadIdx.x & 63);
+    pc[u].n = 0;
+    s4[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (wbase >= total) continue;
+    while (ti < tab.count - 1 && wbase >= tab.offset[ti + 1]) ++ti;
+    const float* grad = nullptr;
+    for (int t = ti; t < tab.count && tab.offset[t] < wbase + 256; ++t) {  // wave-uniform t
+      if (i0[u] >= tab.offset[t] && i0[u] < tab.offset[t + 1]) {
+        const tm_optim_tensor& T = tab.t[t];
+        pc[u].param = T.param; grad = T.grad; pc[u].lr = T.lr; pc[u].wd = T.weight_decay;
+        pc[u].j0 = i0[u] - tab.offset[t];
+        pc[u].n = (int)min(4LL, T.numel - pc[u].j0);   // the tensor's padding tail: n < 4 (or <= 0)
+      }
+    }
+    const int n = pc[u].n;
+    if (n <= 0) continue;
+    const long long j0 = pc[u].j0;
+    pc[u].vec = n == 4 && ((uintptr_t)(pc[u].param + j0) % 16) == 0 && ((uintptr_t)(grad + j0) % 16) == 0;
+    m4[u] = *(const f32x4*)(exp_avg + i0[u]);
+    v4[u] = *(const f32x4*)(exp_avg_sq + i0[u]);
+    if (pc[u].vec) {
+      p4[u] = *(const f32x4*)(pc[u].param + j0);
+      g4[u] = *(const f32x4*)(grad + j0);
+    } else {
+      for (int e = 0; e < 4; ++e) {
+        p4[u][e] = e < n ? pc[u].param[j0 + e] : 0.f;
+        g4[u][e] = e < n ? grad[j0 + e] : 0.f;
+      }
     }
   }
   const float step = (float)counters[0];
@@ -96,26 +118,35 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
                         : 0.0f;
   r.sync = la_k > 0 && la_step % la_k == 0;
   r.first_sync = la_step <= la_k;
-  if (r.sync && !r.first_sync) s4 = *(const f32x4*)(slow + i0);
+  if (r.sync && !r.first_sync) {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float m = m4[e], v = v4[e];
-    float p = radam_elem(p4[e], g4[e], m, v, r, T.lr, T.weight_decay, beta1, beta2, eps);
-    if (r.sync) {
-      p = r.first_sync ? p : s4[e] + la_alpha * (p - s4[e]);
-      s4[e] = p;
-    }
-    m4[e] = m;
-    v4[e] = v;
-    p4[e] = p;
+    for (int u = 0; u < OPT_PIECES; ++u)
+      if (pc[u].n > 0) s4[u] = *(const f32x4*)(slow + i0[u]);
   }
-  *(f32x4*)(exp_avg + i0) = m4;
-  *(f32x4*)(exp_avg_sq + i0) = v4;
-  if (r.sync) *(f32x4*)(slow + i0) = s4;
-  if (vec) {
-    *(f32x4*)(T.param + j0) = p4;
-  } else {
-    for (int e = 0; e < n; ++e) T.param[j0 + e] = p4[e];
+#pragma unroll
+  for (int u = 0; u < OPT_PIECES; ++u) {
+    const int n = pc[u].n;
+    if (n <= 0) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float m = m4[u][e], v = v4[u][e];
+      float p = radam_elem(p4[u][e], g4[u][e], m, v, r, pc[u].lr, pc[u].wd, beta1, beta2, eps);
+      if (r.sync) {
+        p = r.first_sync ? p : s4[u][e] + la_alpha * (p - s4[u][e]);
+        s4[u][e] = p;
+      }
+      m4[u][e] = m;
+      v4[u][e] = v;
+      p4[u][e] = p;
+    }
+    *(f32x4*)(exp_avg + i0[u]) = m4[u];
+    *(f32x4*)(exp_avg_sq + i0[u]) = v4[u];
+    if (r.sync) *(f32x4*)(slow + i0[u]) = s4[u];
+    if (pc[u].vec) {
+      *(f32x4*)(pc[u].param + pc[u].j0) = p4[u];
+    } else {
+      for (int e = 0; e < n; ++e) pc[u].param[pc[u].j0 + e] = p4[u][e];
+    }
   }
 }
 
