@@ -21,7 +21,7 @@ __global__ void cast_many_kernel(tm_cast_table tab) {
 }
 
 // The per-step preparation of the fused forward as ONE launch: blocks [0, cast_blocks) convert
-// the cast table (GEMM weights + the bag to T), the next ceil(D/256) blocks fold PPEG's
+// the cast table (GEMM weights + the bag to T), the next ceil(49 D/256) blocks fold PPEG's
 // 7x7 + 5x5 + 3x3 + identity into one 7x7 kernel (code/models/TransMIL.py:72), and the last
 // block advances the dropout counter and writes this forward's seed snapshot.
 template <typename T>
@@ -35,30 +35,45 @@ __global__ void __launch_bounds__(256) step_prepare_kernel(tm_cast_table tab, lo
                                                            const float* __restrict__ cls, float* __restrict__ H,
                                                            int B, int S) {
   if (blockIdx.x < cast_blocks) {
-    const long long i4 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (i4 >= tab.offset[tab.count]) return;
-    int t = 0;
-    while (i4 >= tab.offset[t + 1]) ++t;
-    const long long j = i4 - tab.offset[t], n = tab.offset[t + 1] - tab.offset[t];
-    const float* src = tab.src[t];
-    T* dst = (T*)tab.dst[t];
-    for (int e = 0; e < 4 && j + e < n; ++e) dst[j + e] = from_f<T>(src[j + e]);
+    // 4 elements per thread (offsets are multiples of 4, so a piece never straddles tensors); the
+    // tensor is found wave-uniformly -- scalar loads of the table, a wave on a tensor boundary
+    // walks the few tensors it touches -- and the piece moves as one 16-B load / one 4-T store
+    const long long total = tab.offset[tab.count];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long wbase = ((long long)blockIdx.x * blockDim.x + wave * 64) * 4;
+    if (wbase >= total) return;
+    const long long i4 = wbase + 4 * (threadIdx.x & 63);
+    int t0 = 0;
+    while (t0 < tab.count - 1 && wbase >= tab.offset[t0 + 1]) ++t0;
+    for (int t = t0; t < tab.count && tab.offset[t] < wbase + 256; ++t) {  // wave-uniform t
+      if (i4 < tab.offset[t] || i4 >= tab.offset[t + 1]) continue;
+      const long long j = i4 - tab.offset[t];
+      const float* src = tab.src[t] + j;
+      T* dst = (T*)tab.dst[t] + j;
+      if (((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % (4 * sizeof(T))) == 0) {
+        const f32x4 v = *(const f32x4*)src;
+        vec4<T> o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = from_f<T>(v[e]);
+        *(vec4<T>*)dst = o;
+      } else {
+        for (int e = 0; e < 4; ++e) dst[e] = from_f<T>(src[e]);
+      }
+    }
     return;
   }
   const long long fb = blockIdx.x - cast_blocks;
-  const int nfold = w7 ? (D + 255) / 256 : 0;
-  if (fb < nfold) {
-    const int ch = (int)fb * 256 + threadIdx.x;
-    if (ch >= D) return;
-    for (int dy = 0; dy < 7; ++dy)
-      for (int dx = 0; dx < 7; ++dx) {
-        float v = w7[(size_t)ch * 49 + dy * 7 + dx];
-        if (dy >= 1 && dy <= 5 && dx >= 1 && dx <= 5) v += w5[(size_t)ch * 25 + (dy - 1) * 5 + (dx - 1)];
-        if (dy >= 2 && dy <= 4 && dx >= 2 && dx <= 4) v += w3[(size_t)ch * 9 + (dy - 2) * 3 + (dx - 2)];
-        if (dy == 3 && dx == 3) v += 1.0f;
-        wf[(size_t)(dy * 7 + dx) * D + ch] = v;  // tap-major [49][D] (coalesced stencil reads)
-      }
-    bf[ch] = b7[ch] + b5[ch] + b3[ch];
+  const int nfold = w7 ? (49 * D + 255) / 256 : 0;
+  if (fb < nfold) {  // one thread per (tap, channel), channels fastest
+    const int i = (int)fb * 256 + threadIdx.x;
+    if (i >= 49 * D) return;
+    const int tap = i / D, ch = i - tap * D, dy = tap / 7, dx = tap - dy * 7;
+    float v = w7[(size_t)ch * 49 + tap];
+    if (dy >= 1 && dy <= 5 && dx >= 1 && dx <= 5) v += w5[(size_t)ch * 25 + (dy - 1) * 5 + (dx - 1)];
+    if (dy >= 2 && dy <= 4 && dx >= 2 && dx <= 4) v += w3[(size_t)ch * 9 + (dy - 2) * 3 + (dx - 2)];
+    if (dy == 3 && dx == 3) v += 1.0f;
+    wf[(size_t)tap * D + ch] = v;  // tap-major [49][D] (coalesced stencil reads)
+    if (tap == 0) bf[ch] = b7[ch] + b5[ch] + b3[ch];
     return;
   }
   if (threadIdx.x == 0 && counter) {
@@ -298,7 +313,7 @@ extern "C" int tm_step_prepare(int dtype, const tm_cast_table* table, const floa
     off = table->offset[i + 1];
   }
   const long long cast_blocks = ((off + 3) / 4 + 255) / 256;
-  const long long blocks = cast_blocks + (w7 ? (D + 255) / 256 : 0) + 1;
+  const long long blocks = cast_blocks + (w7 ? (49LL * D + 255) / 256 : 0) + 1;
   TM_DTYPE_DISPATCH(dtype, (step_prepare_kernel<T><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
                                *table, cast_blocks, w7, b7, w5, b5, w3, b3, D, wfold, bfold, counter, seed_out,
                                cls, H, B, S)));
