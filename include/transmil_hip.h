@@ -203,7 +203,9 @@ int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const f
                 void* stream);
 long long tm_ppeg_bwd_workspace(int B, int G, int D);
 /* dout (nullable): also writes the padded to_out-dropout gradient of the TransLayer below from dx
- * (as tm_dropout_bwd_pad with the same dtype / n_pad / pad / p / seed / seed_ptr) */
+ * (as tm_dropout_bwd_pad with the same dtype / n_pad / pad / p / seed / seed_ptr).  The weight
+ * gradients are summed from the workspace straight into dw7..db3 (=); dwsum is not written (kept in
+ * the signature for ABI stability, may be null) */
 int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const float* wfold, float* dx,
                 float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
                 float* db3, int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,

@@ -209,18 +209,31 @@ __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict
 }
 
 // unfold folded gradients: dw7 = dwf, dw5 = centre 5x5, dw3 = centre 3x3, db* = db
-__global__ void ppeg_unfold_kernel(const float* __restrict__ g, int D, float* __restrict__ dw7,
-                                   float* __restrict__ db7, float* __restrict__ dw5, float* __restrict__ db5,
-                                   float* __restrict__ dw3, float* __restrict__ db3) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= D) return;
-  const float* s = g + (size_t)ch * (NT + 1);
-  for (int t = 0; t < NT; ++t) dw7[(size_t)ch * NT + t] = s[t];
-  for (int dy = 0; dy < 5; ++dy)
-    for (int dx = 0; dx < 5; ++dx) dw5[(size_t)ch * 25 + dy * 5 + dx] = s[(dy + 1) * KS + dx + 1];
-  for (int dy = 0; dy < 3; ++dy)
-    for (int dx = 0; dx < 3; ++dx) dw3[(size_t)ch * 9 + dy * 3 + dx] = s[(dy + 2) * KS + dx + 2];
-  db7[ch] = s[NT]; db5[ch] = s[NT]; db3[ch] = s[NT];
+// the weight-gradient partial slabs summed (in slab order, as tm_splitk_reduce) straight into the
+// unfolded gradients: thread i = (ch, t) of the [D][50] partial layout, t < 49 a tap of the folded
+// 7x7 kernel (its 5x5 / 3x3 centre taps also feed dw5 / dw3: the fold is a sum), t = 49 the bias
+__global__ __launch_bounds__(256) void ppeg_wgrad_reduce_kernel(const float* __restrict__ part, int slabs, int D,
+                                                                float* __restrict__ dw7, float* __restrict__ db7,
+                                                                float* __restrict__ dw5, float* __restrict__ db5,
+                                                                float* __restrict__ dw3, float* __restrict__ db3) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t count = (size_t)D * (NT + 1);
+  if (i >= (int)count) return;
+  constexpr int U = 12;
+  float s = 0.f;
+  for (int z0 = 0; z0 < slabs; z0 += U) {
+    float v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) v[k] = part[(size_t)min(z0 + k, slabs - 1) * count + i];
+#pragma unroll
+    for (int k = 0; k < U; ++k) s += z0 + k < slabs ? v[k] : 0.f;
+  }
+  const int ch = i / (NT + 1), t = i - ch * (NT + 1);
+  if (t == NT) { db7[ch] = s; db5[ch] = s; db3[ch] = s; return; }
+  dw7[(size_t)ch * NT + t] = s;
+  const int dy = t / KS, dx = t - dy * KS;
+  if (dy >= 1 && dy <= 5 && dx >= 1 && dx <= 5) dw5[(size_t)ch * 25 + (dy - 1) * 5 + dx - 1] = s;
+  if (dy >= 2 && dy <= 4 && dx >= 2 && dx <= 4) dw3[(size_t)ch * 9 + (dy - 2) * 3 + dx - 2] = s;
 }
 
 }  // namespace
@@ -274,8 +287,9 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
   tm_allow_smem(ppeg_wgrad_kernel, TILE_LDS + DY_LDS);
   ppeg_wgrad_kernel<<<wgrad_grid(B, G, D), 256, TILE_LDS + DY_LDS, st>>>(x, dy, S, G, D, work);
   TM_CHECK_LAUNCH();
-  if (int rc = tm_splitk_reduce(work, dwsum, ppeg_wgrad_slabs(B, G), (long long)D * 50, 1.0f, 0, stream)) return rc;
-  ppeg_unfold_kernel<<<(D + 63) / 64, 64, 0, st>>>(dwsum, D, dw7, db7, dw5, db5, dw3, db3);
+  (void)dwsum;
+  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, ppeg_wgrad_slabs(B, G), D, dw7, db7, dw5,
+                                                                     db5, dw3, db3);
   TM_CHECK_LAUNCH();
   return 0;
 }
