@@ -118,10 +118,18 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
   __shared__ float qs[S2_ROWS][DH];
   __shared__ float red[4][S2_ROWS];
   {
+    // the q~ rows go out with the k~ loads (one memory round trip before the LDS writes)
+    static_assert(S2_ROWS * DH % 256 == 0, "sim2: q~ rows per thread");
+    constexpr int QE = S2_ROWS * DH / 256;
+    float qv[QE];
+#pragma unroll
+    for (int u = 0; u < QE; ++u) qv[u] = ql[((size_t)bh * NL + i0) * DH + u * 256 + j];
     const float* kb = kl + (size_t)bh * NL * DH;
     f32x4 v[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = *(const f32x4*)(kb + (size_t)(u * 256 + j) * 4);  // piece p: row p/16, d 4 (p%16)
+#pragma unroll
+    for (int u = 0; u < QE; ++u) qs[(u * 256 + j) / DH][(u * 256 + j) % DH] = qv[u];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int p = u * 256 + j, row = p >> 4, d0 = (p & 15) * 4;
@@ -129,7 +137,6 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
       for (int e = 0; e < 4; ++e) kt[(d0 + e) * S2_KT + row] = v[u][e];
     }
   }
-  for (int e = threadIdx.x; e < S2_ROWS * DH; e += 256) qs[e / DH][e % DH] = ql[((size_t)bh * NL + i0) * DH + e];
   __syncthreads();
   float s[S2_ROWS];
 #pragma unroll
