@@ -386,6 +386,20 @@ TM_DEV void tile_of_block(int& m0, int& n0) {
   n0 = (id % ntx) * BN;
 }
 
+// the same renumbering over the whole (x, y, split) grid, splits slowest: an XCD's run of
+// workgroups covers one or two splits' K-slices of A and B (split-K launches read each slice's
+// panels into one or two L2s instead of all eight).  Bijective for any grid size.
+TM_DEV void tile_split_of_block(int& m0, int& n0, int& z) {
+  const int ntx = gridDim.x, per = gridDim.x * gridDim.y, nwg = per * gridDim.z;
+  const int orig = (blockIdx.z * gridDim.y + blockIdx.y) * ntx + blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  z = id / per;
+  const int rr = id - z * per;
+  m0 = (rr / ntx) * BM;
+  n0 = (rr % ntx) * BN;
+}
+
 // NBUF = 2: double-buffered LDS (one barrier per k-tile); NBUF = 1: one LDS buffer, two
 // barriers per k-tile, half the LDS -> twice the resident workgroups per CU.
 template <typename T, typename OutT, bool A_T, bool B_KN, int NBUF = 2>
@@ -629,9 +643,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;  // 4 (M) x 2 (N) waves of 32 x 64
-  int m0, n0;
-  tile_of_block(m0, n0);
-  const int kbeg = blockIdx.z * g.k_per_split;
+  int m0, n0, zs;
+  tile_split_of_block(m0, n0, zs);
+  const int kbeg = zs * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   const int nk = kend > kbeg ? (kend - kbeg) / 64 : 0;  // host guarantees 64 | (kend - kbeg)
 
@@ -701,7 +715,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
       }
     }
   } else
-  gemm_epilogue_rows<OutT, BN, BM, 512, KIND>(smem, C, g, m0, n0);
+  gemm_epilogue_rows<OutT, BN, BM, 512, KIND>(smem, C, g, m0, n0, zs);
   if constexpr (STAMP) {
     ring_stamp<STAMP>(ts, 5);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
