@@ -206,6 +206,44 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, int B, int C,
                                 float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dh) {
   constexpr int D = VPL * 64;
   const int lane = threadIdx.x;
+  if (B == 1 && C <= 4) {
+    // one bag (the reference's batch size), few classes: every load first, one memory round trip
+    float dl[4], gm[VPL], bt[VPL], xh[VPL], w[4][VPL];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dl[k] = k < C ? dlogits[k] : 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane * VPL + i;
+      gm[i] = gamma[c]; bt[i] = beta[c]; xh[i] = xhat[c];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k][i] = k < C ? W[(size_t)k * D + c] : 0.f;
+    }
+    float g[VPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane * VPL + i;
+      float dy = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < C) {
+          dW[(size_t)k * D + c] = 0.f + dl[k] * (xh[i] * gm[i] + bt[i]);
+          dy += dl[k] * w[k][i];
+        }
+      dgamma[c] = 0.f + dy * xh[i];
+      dbeta[c] = 0.f + dy;
+      g[i] = dy * gm[i];
+      s1 += g[i];
+      s2 += g[i] * xh[i];
+    }
+    if (lane == 0)
+      for (int k = 0; k < C; ++k) dbias[k] = 0.f + dl[k];
+    s1 = wave_sum(s1) * (1.0f / D);
+    s2 = wave_sum(s2) * (1.0f / D);
+    const float rs = rstd[0];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) dh[lane * VPL + i] = rs * (g[i] - s1 - xh[i] * s2);
+    return;
+  }
   float dgm[VPL], dbt[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) { dgm[i] = 0.f; dbt[i] = 0.f; }
