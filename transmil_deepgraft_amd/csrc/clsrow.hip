@@ -108,6 +108,20 @@ __global__ __launch_bounds__(256) void a1_row_fwd_kernel(const T* __restrict__ q
   __shared__ float ps[NL];
   __shared__ float part[32][DH];
   const int bh = blockIdx.x, b = bh / nh, h = bh % nh, tid = threadIdx.x;
+  // the Y rows and the conv window are loaded up front, with the score operands (one memory round
+  // trip instead of three: nothing below the first barrier issues a global load)
+  const int g = tid >> 3, o = (tid & 7) * 8, tg = tid >> 6, d = tid & 63;
+  vec8<T> ym[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ym[i] = load8(y_t + (size_t)bh * NL * DH + (size_t)(8 * g + i) * DH + o);
+  float xc[9], wc[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int tau = tg + 4 * i, t = r + tau - HALF;
+    const bool in = tau < TAPS && t >= 0 && t < n;
+    xc[i] = in ? to_f(v[((size_t)bh * n + t) * DH + d]) : 0.f;
+    wc[i] = tau < TAPS ? wconv[h * TAPS + tau] : 0.f;
+  }
   const T* qr = q + ((size_t)bh * n + r) * DH;
   const float s = row_score(qr, kl_t + ((size_t)bh * NL + tid) * DH);
   const float m = block_reduce_max(s, red);
@@ -116,8 +130,29 @@ __global__ __launch_bounds__(256) void a1_row_fwd_kernel(const T* __restrict__ q
   ps[tid] = e / l;
   if (tid == 0) lse1[(size_t)bh * n + r] = m + __logf(l);
   __syncthreads();
-  const float py = rows_dot(ps, y_t + (size_t)bh * NL * DH, part);
-  const float cv = conv_row(v + (size_t)bh * n * DH, wconv + h * TAPS, r, n, part);
+  // sum_j p_j Y[j][d]: thread (g, o) its 8 rows x 8 columns, then the 32 row groups in order
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float wj = ps[8 * g + i];
+#pragma unroll
+    for (int e2 = 0; e2 < 8; ++e2) acc[e2] = fmaf(wj, to_f(ym[i][e2]), acc[e2]);
+  }
+#pragma unroll
+  for (int e2 = 0; e2 < 8; ++e2) part[g][o + e2] = acc[e2];
+  __syncthreads();
+  float py = 0.f;
+  if (tid < DH)
+    for (int gg = 0; gg < 32; ++gg) py += part[gg][tid];
+  __syncthreads();
+  // conv33: thread (tg, d) its taps tg, tg + 4, ..., then the 4 tap groups in order
+  float ca = 0.f;
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+    if (tg + 4 * i < TAPS) ca = fmaf(wc[i], xc[i], ca);
+  part[tg][d] = ca;
+  __syncthreads();
+  const float cv = tid < DH ? (part[0][tid] + part[1][tid]) + (part[2][tid] + part[3][tid]) : 0.f;
   if (tid < DH) merged[((size_t)b * n + r) * nh * DH + h * DH + tid] = from_f<T>(py + cv);
 }
 
