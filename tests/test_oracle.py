@@ -99,6 +99,61 @@ def test_pinv_matches_hf_iterative_inv():
     torch.testing.assert_close(ours, theirs, rtol=1e-9, atol=1e-9)
 
 
+@pytest.mark.parametrize("n,B", [(300, 2), (1025, 1), (8282, 1)])
+def test_nystrom_eq2_to_9_match_hf_nystromformer(n, B):
+    """Independent pin of SURVEY.md App. A eq. 2-9 (the arithmetic of the third-party
+    ``nystrom_attention`` the reference calls at code/models/TransMIL.py:26-34,47) against
+    transformers' ``NystromformerSelfAttention.forward``, which implements the same algorithm:
+    segment-mean landmarks over the padded sequence (eq. 4), the three softmaxes (eq. 5-6),
+    ``iterative_inv`` (eq. 7, init 'original'), ``(A1 Z)(A3 V)`` (eq. 8) and a depthwise (33, 1)
+    conv on V (eq. 9).  HF scales q and k by dh^-1/4 each; the oracle scales q by dh^-1/2: the
+    same products.  HF's Z0 divides by max(colsum) only; the oracle also by max(rowsum), which is
+    1 up to rounding for a softmax.
+
+    Mapping: the oracle's ``to_qkv`` row blocks become HF's query / key / value weights (zero
+    biases), ``res_conv.weight`` becomes ``conv.weight``; HF is fed the already front-padded
+    input (eq. 1, n' = n rounded up to 256) and its context layer is compared with the oracle's
+    pre-``to_out`` activation (captured by a pre-hook on ``to_out[0]``), fp64, to 1e-9 relative.
+    n' = 512 (B = 2: the global max couples the bags), 1280 (config C1) and 8448 (config C2)."""
+    from transformers import NystromformerConfig
+    from transformers.models.nystromformer.modeling_nystromformer import NystromformerSelfAttention
+    from oracle.nystrom_ref import NystromAttention
+    m = 256
+    npad = (n + m - 1) // m * m
+    g = torch.Generator().manual_seed(11 + n)
+    ours = NystromAttention(dim=512, dim_head=64, heads=8, num_landmarks=m, pinv_iterations=6,
+                            residual=True, dropout=0.7).double().eval()
+    with torch.no_grad():
+        for p in ours.parameters():
+            p.copy_(torch.randn(p.shape, generator=g, dtype=torch.float64) * 0.05)
+    cfg = NystromformerConfig(hidden_size=512, num_attention_heads=8, num_landmarks=m,
+                              segment_means_seq_len=npad, conv_kernel_size=33,
+                              inv_coeff_init_option=False, attention_probs_dropout_prob=0.0)
+    hf = NystromformerSelfAttention(cfg).double().eval()
+    assert hf.init_option == "original"
+    w = ours.to_qkv.weight.detach()
+    with torch.no_grad():
+        for i, lin in enumerate((hf.query, hf.key, hf.value)):
+            lin.weight.copy_(w[i * 512:(i + 1) * 512])
+            lin.bias.zero_()
+        hf.conv.weight.copy_(ours.res_conv.weight)
+    x = torch.randn(B, n, 512, generator=g, dtype=torch.float64)
+    got = {}
+    handle = ours.to_out[0].register_forward_pre_hook(lambda _m, inp: got.__setitem__("ctx", inp[0]))
+    try:
+        with torch.no_grad():
+            ours(x)
+    finally:
+        handle.remove()
+    xpad = torch.cat([torch.zeros(B, npad - n, 512, dtype=torch.float64), x], dim=1)
+    with torch.no_grad():
+        theirs = hf(xpad)[0]
+    ctx = got["ctx"]
+    assert ctx.shape == theirs.shape == (B, npad, 512)
+    rel = ((ctx - theirs).abs().max() / theirs.abs().max()).item()
+    assert rel < 1e-9, rel
+
+
 def test_pinv_global_max_couples_bags():
     """The Z0 scale uses maxima over the WHOLE [B,h,m,m] tensor (App. A eq. 7)."""
     from oracle.nystrom_ref import moore_penrose_iter_pinv
