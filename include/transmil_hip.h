@@ -167,10 +167,6 @@ typedef struct tm_bmm_job {
 } tm_bmm_job;
 /* prec 0: exact fp32 MFMA; prec 1: bf16x3 (hi/lo split, ~16-bit operands, fp32 accumulate) */
 int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream);
-/* microbenchmark ablation switch (which = 0: bmm kernel variant); not for production use */
-void tm_debug_set_variant(int which, int value);
-/* XCD id (HW_REG_XCC_ID) of every block of an nblocks x threads launch -> out[nblocks] (int32) */
-int tm_debug_xcc_map(int* out, int nblocks, int threads, void* stream);
 long long tm_pinv_saved_floats(int nbh, int iters);
 int tm_pinv_fwd(const float* X, int nbh, int iters, int prec, float* saved, void* stream);
 long long tm_pinv_bwd_workspace_floats(int nbh);

@@ -3,7 +3,9 @@
     python scripts/microbench.py [--n 8192] [--reps 50]
 
 Each case is run `reps` times between two events on the current stream; the
-median of 5 rounds is printed.  Used to A/B kernel variants on the GPU box.
+median of 5 rounds is printed.  Used to A/B kernel variants on the GPU box: it runs on the
+diagnostic build (`make -C transmil_deepgraft_amd/csrc diag`), whose tm_debug_* switches select
+the variants; the product library has none.
 """
 import argparse
 import ctypes as C
@@ -16,6 +18,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("TRANSMIL_HIP_LIB", os.path.join(ROOT, "transmil_deepgraft_amd", "libtransmil_hip_diag.so"))
 
 from transmil_deepgraft_amd import _lib  # noqa: E402
 from transmil_deepgraft_amd import engine as E  # noqa: E402

@@ -1,0 +1,67 @@
+"""One rank of the two-rank gradient-averaging test (tests/test_ddp_gpu.py).
+
+Launched twice by the test with RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the
+environment; both ranks share the one leased GPU, so the process group is gloo (RCCL refuses
+two ranks on one device; gloo all-reduces CUDA tensors through host staging).  Each rank runs
+the fused HIP TransMIL step (bf16 mode, train mode) on its own bags through
+``TransMILTask.optimization_step`` with ``GradAllReduce(model=..., overlap=True)``: the part-0
+all_reduce is issued by the fused backward's mid-backward ``ready(0)`` hook, and with
+``accumulate_grad_batches = K`` only every K-th micro-batch reduces (Lightning's DDP no-sync,
+code/train.py:178-201).  The final parameters go to ``argv[1]``.
+
+Not collected by pytest (no ``test_`` prefix); imports nothing from ``oracle/``.
+"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+N_PATCHES = 700
+
+
+def build_model():
+    from transmil_deepgraft_amd.models import TransMIL
+    torch.manual_seed(0)
+    return TransMIL(2, 512, 512).cuda().train().set_compute_dtype(torch.bfloat16)
+
+
+def bag(rank, micro):
+    g = torch.Generator(device="cuda").manual_seed(1000 * rank + micro)
+    x = torch.rand(1, N_PATCHES, 512, device="cuda", generator=g)
+    return x, torch.tensor([(rank + micro) % 2], device="cuda"), None   # (bags, labels, names)
+
+
+def main(out_path, k, steps):
+    import torch.distributed as dist
+    from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    rank = dist.get_rank()
+    model = build_model()
+    ar = GradAllReduce(model.parameters(), model=model, overlap=True)
+    issued = []      # parts whose all_reduce the backward's ready() hook issued (mid-backward)
+
+    def spy(i, inner=ar._on_ready):
+        before = set(ar._works)
+        inner(i)
+        if i in ar._works and i not in before:
+            issued.append(i)
+    ar.bucket.hooks = [spy]
+    task = TransMILTask(model, accumulate_grad_batches=k)
+    opt = task.configure_optimizers()[0][0]
+    for micro in range(steps * k):
+        task.optimization_step(bag(rank, micro), opt, allreduce=ar)
+    torch.cuda.synchronize()
+    owned = all(ar.bucket.owns(p) for p in model.parameters()) or all(p.grad is None for p in model.parameters())
+    torch.save({"params": {n: p.detach().cpu() for n, p in model.named_parameters()},
+                "issued": issued, "owned": owned, "rank": rank}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]))

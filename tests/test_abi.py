@@ -77,3 +77,17 @@ def test_error_path_without_gpu():
 def test_build_info():
     from transmil_deepgraft_amd import _lib
     assert b"gfx950" in _lib.lib().tm_build_info()
+
+
+def test_product_library_has_no_diagnostic_switches():
+    """Kernel-variant switches and timing stamps live only in the TM_DIAG build
+    (libtransmil_hip_diag.so, scripts/microbench.py): the product library exports no tm_debug_*
+    entry point, so no process-global state can change another stream's kernels."""
+    import subprocess
+    from transmil_deepgraft_amd import _lib
+    lib = _lib.lib()
+    for name in _lib.DIAG_SIGS:
+        assert not hasattr(lib, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True)
+    if nm.returncode == 0:
+        assert "tm_debug" not in nm.stdout

@@ -123,3 +123,67 @@ def test_rccl_allreduce_inside_captured_graph(overlap):
         gc.collect()
         torch.cuda.synchronize()
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_two_ranks_average_through_the_hip_engine(k, tmp_path):
+    """Two processes on the one leased GPU (gloo: RCCL refuses two ranks on one device), each
+    running the fused HIP TransMIL step (bf16 mode, train mode) on its own bags with
+    ``GradAllReduce(model=..., overlap=True)`` and ``accumulate_grad_batches = k``
+    (tests/ddp_two_rank_worker.py; reference: Lightning DDP, code/train.py:178-201, K = 10 at
+    :199).  After 2 optimizer steps both ranks hold the same parameters, equal (rtol 1e-5) to one
+    process that accumulates both ranks' bags with loss / (2k) -- the gradient average DDP
+    computes -- through the same kernels and optimizer, with the dropout stream replayed.  The
+    part-0 all_reduce is issued by the fused backward's ready() hook."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import ddp_two_rank_worker as W
+    from transmil_deepgraft_amd.interface import TransMILTask
+    steps, world = 2, 2
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(here, "ddp_two_rank_worker.py"),
+                                       str(tmp_path / f"rank{r}.pt"), str(k), str(steps)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=100)[0].decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-3000:]}"
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    for r in range(world):
+        assert res[r]["issued"] == [0, 1] * steps, res[r]["issued"]
+    for n in res[0]["params"]:
+        torch.testing.assert_close(res[0]["params"][n], res[1]["params"][n], rtol=0, atol=0, msg=n)
+
+    # one process, both ranks' bags, the DDP mean taken by the loss scale
+    model = W.build_model()
+    c0 = model._dropout_counter.clone()
+    task = TransMILTask(model)
+    opt = task.configure_optimizers()[0][0]
+    start = {n: p.detach().clone() for n, p in model.named_parameters()}
+    for s in range(steps):
+        for micro in range(s * k, (s + 1) * k):
+            for r in range(world):
+                model._dropout_counter.copy_(c0 + micro)     # each rank's stream at this micro-batch
+                task.backward(task.training_step(W.bag(r, micro)) / (world * k))
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
+    moved = 0.0
+    for n, p in model.named_parameters():
+        got = res[0]["params"][n]
+        torch.testing.assert_close(got, p.detach().cpu(), rtol=1e-5, atol=1e-7, msg=n)
+        moved = max(moved, (p.detach() - start[n]).abs().max().item())
+    assert moved > 1e-5      # the steps changed the parameters (the comparison is not vacuous)

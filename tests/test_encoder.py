@@ -71,3 +71,34 @@ def test_image_path_end_to_end():
     lo.sum().backward()
     assert all(p.grad is None for p in enc.parameters())
     assert all(p.grad is not None for p in mil.parameters())
+
+
+@pytest.mark.gpu
+def test_folded_weights_follow_parent_loads_and_inplace_edits():
+    """The eval-mode folded conv+BN weights are re-derived after a checkpoint loaded through a
+    parent module (ImageBagModel.load_state_dict goes through _load_from_state_dict, not the
+    encoder's own load_state_dict) and after an in-place BatchNorm statistics edit."""
+    from transmil_deepgraft_amd.encoder import ImageBagModel
+    from transmil_deepgraft_amd.models import TransMIL
+    torch.backends.cudnn.allow_tf32 = False
+    enc = _encoder(torch.float32).cuda()
+    x = torch.from_numpy(encoder_tiles(2, seed=9)).cuda()
+    with torch.no_grad():
+        first = enc(x)
+    other = _encoder(torch.float32)
+    with torch.no_grad():
+        other.bn1.running_mean.add_(0.5)
+        other.layer1[0].conv1.weight.mul_(1.5)
+    parent = ImageBagModel(enc, TransMIL(2, 2048).cuda())
+    sd = {"model_ft." + k: v for k, v in other.state_dict().items()}
+    sd.update({"model." + k: v for k, v in parent.model.state_dict().items()})
+    parent.load_state_dict(sd)
+    with torch.no_grad():
+        after_load = enc(x)
+        expect = other.cuda()(x)
+    torch.testing.assert_close(after_load, expect, rtol=1e-5, atol=1e-5)
+    assert not torch.allclose(after_load, first)
+    with torch.no_grad():
+        enc.bn1.running_mean.sub_(0.5)          # in place: back to the first statistics for bn1
+        other.bn1.running_mean.sub_(0.5)
+        torch.testing.assert_close(enc(x), other(x), rtol=1e-5, atol=1e-5)

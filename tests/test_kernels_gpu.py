@@ -22,20 +22,10 @@ def _rel(a, b):
 
 
 # ----------------------------------------------------------------------------- GEMM
-@pytest.fixture(params=[0, 1, 2, 3, 4, 6, 7], ids=["ring2", "2buf", "ring4", "1buf", "persist", "ring3", "big"])
-def gemm_variant(request):
-    """Every GEMM main loop (default 2-stage global_load_lds ring, register-staged 2 / 1 LDS
-    buffers, 4- and 3-stage rings, persistent ring, 256-row big tiles)."""
-    from transmil_deepgraft_amd import _lib
-    _lib.lib().tm_debug_set_variant(2, request.param)
-    yield request.param
-    _lib.lib().tm_debug_set_variant(2, 0)
-
-
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("a_trans,b_kn", [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize("K", [168, 320])
-def test_gemm_layouts(dtype, a_trans, b_kn, K, gemm_variant):
+def test_gemm_layouts(dtype, a_trans, b_kn, K):
     """K = 168: register-staged loop; K = 320 (bf16): the global_load_lds ring."""
     from transmil_deepgraft_amd.engine import gemm
     from transmil_deepgraft_amd._lib import BF16, F32
@@ -55,14 +45,11 @@ def test_gemm_layouts(dtype, a_trans, b_kn, K, gemm_variant):
 
 
 @pytest.mark.parametrize("a_trans,b_kn", [(0, 0), (0, 1), (1, 1)])
-@pytest.mark.parametrize("variant", [0, 4])
-def test_gemm_persistent_many_tiles(a_trans, b_kn, variant):
+def test_gemm_persistent_many_tiles(a_trans, b_kn):
     """More tiles than workgroups (every workgroup walks several tiles, the DMA ring runs across
     tile boundaries) in the QKV / dX layouts and the split-K weight gradient (6 splits x 48 tiles)."""
     from transmil_deepgraft_amd.engine import gemm, weight_grad, Pool
     from transmil_deepgraft_amd._lib import BF16, F32
-    from transmil_deepgraft_amd import _lib
-    _lib.lib().tm_debug_set_variant(2, variant)
     g = torch.Generator(device="cpu").manual_seed(3)
     if a_trans:     # dW[M, N] = sum_k dY[k, m] X[k, n]
         M, N, K = 1536, 512, 4224
@@ -80,12 +67,11 @@ def test_gemm_persistent_many_tiles(a_trans, b_kn, variant):
         out = torch.empty(M, N, dtype=torch.float32, device=DEV)
         gemm(A.to(DEV), Bs, out, M, N, K, lda=K, ldb=N if b_kn else K, ldc=N, b_kn=b_kn, dtype=BF16, c_dtype=F32)
     torch.cuda.synchronize()
-    _lib.lib().tm_debug_set_variant(2, 0)
     assert _rel(out.cpu(), ref) < 1e-5
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_epilogue_bias_gelu_rowmap_dup(dtype, gemm_variant):
+def test_gemm_epilogue_bias_gelu_rowmap_dup(dtype):
     from transmil_deepgraft_amd.engine import gemm
     from transmil_deepgraft_amd._lib import BF16, F32
     code = BF16 if dtype == torch.bfloat16 else F32
@@ -138,7 +124,7 @@ def test_gemm_dropout_residual_and_splitk():
     assert _rel(res.cpu(), dY.double().t() @ X.double()) < 1e-5
 
 
-def test_gemm_ring_splitk_weight_grad_bf16(gemm_variant):
+def test_gemm_ring_splitk_weight_grad_bf16():
     """bf16 split-K weight gradient through the global_load_lds ring (K = 33 x 256)."""
     from transmil_deepgraft_amd.engine import weight_grad, Pool
     from transmil_deepgraft_amd._lib import BF16
@@ -153,7 +139,7 @@ def test_gemm_ring_splitk_weight_grad_bf16(gemm_variant):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_gemm_qkv_scatter(dtype, gemm_variant):
+def test_gemm_qkv_scatter(dtype):
     from transmil_deepgraft_amd.engine import gemm
     from transmil_deepgraft_amd._lib import BF16, F32
     code = BF16 if dtype == torch.bfloat16 else F32
@@ -394,8 +380,7 @@ def _a1_ref(q, v, kl, y, wconv, nh):
 
 @pytest.mark.parametrize("nbh,n", [(8, 256), (8, 1280), (32, 512), (8, 8448), (8, 33280)])
 def test_a1_fwd_bf16_kernels(nbh, n):
-    """The per-CU chunk-walking bf16 A1 kernel (MFMA conv, LDS-DMA windows) and the legacy
-    128-query kernel (variant 4) against fp64; and against each other."""
+    """The per-CU chunk-walking bf16 A1 kernel (MFMA conv, LDS-DMA windows) against fp64."""
     L = _lib()
     from transmil_deepgraft_amd._lib import BF16
     from transmil_deepgraft_amd.engine import _p, _stream
@@ -407,23 +392,15 @@ def test_a1_fwd_bf16_kernels(nbh, n):
     y = torch.randn(nbh, 256, 64, generator=g).to(torch.bfloat16)
     wconv = torch.randn(nh, 33, generator=g) * 0.1
     ref_m, ref_l = _a1_ref(q, v, kl, y, wconv, nh)
-    outs = []
-    for variant in (0, 14):
-        L.lib().tm_debug_set_variant(1, variant)
-        try:
-            merged = torch.full((nbh // nh, n, nh * 64), float("nan"), dtype=torch.bfloat16, device=DEV)
-            lse = torch.full((nbh, n), float("nan"), device=DEV)
-            qd, vd, kd, yd, wd = (t.to(DEV).contiguous() for t in (q, v, kl, y, wconv))
-            L.call("tm_nys_a1_fwd", BF16, _p(qd), _p(vd), _p(kd), _p(yd), _p(wd), nbh, nh, n, _p(merged), _p(lse),
-                   _stream())
-            torch.cuda.synchronize()
-        finally:
-            L.lib().tm_debug_set_variant(1, 0)
-        assert torch.isfinite(merged.float()).all() and torch.isfinite(lse).all()
-        assert _rel(merged.cpu(), ref_m) < 2e-2, variant
-        assert (lse.cpu().double() - ref_l).abs().max().item() < 1e-4, variant
-        outs.append(merged.cpu().float())
-    assert _rel(outs[0], outs[1].double()) < 2e-2
+    merged = torch.full((nbh // nh, n, nh * 64), float("nan"), dtype=torch.bfloat16, device=DEV)
+    lse = torch.full((nbh, n), float("nan"), device=DEV)
+    qd, vd, kd, yd, wd = (t.to(DEV).contiguous() for t in (q, v, kl, y, wconv))
+    L.call("tm_nys_a1_fwd", BF16, _p(qd), _p(vd), _p(kd), _p(yd), _p(wd), nbh, nh, n, _p(merged), _p(lse),
+           _stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(merged.float()).all() and torch.isfinite(lse).all()
+    assert _rel(merged.cpu(), ref_m) < 2e-2
+    assert (lse.cpu().double() - ref_l).abs().max().item() < 1e-4
 
 
 # ----------------------------------------------------------------------------- conv33 backward
@@ -451,7 +428,7 @@ def _conv_bwd_ref(dO, O, v, wconv, nh):
 @pytest.mark.gpu
 @pytest.mark.parametrize("nbags,n", [(1, 100), (1, 8448), (2, 1000), (4, 300)])
 def test_conv_bwd_bf16_mfma(nbags, n):
-    """The MFMA conv33 backward (bf16 mode) and the fp32-LDS kernel (variant 7) against fp64."""
+    """The MFMA conv33 backward (bf16 mode) against fp64."""
     L = _lib()
     from transmil_deepgraft_amd._lib import BF16
     from transmil_deepgraft_amd.engine import _p, _stream
@@ -463,26 +440,18 @@ def test_conv_bwd_bf16_mfma(nbags, n):
     v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16)
     wconv = torch.randn(nh, 33, generator=g) * 0.1
     ref_dv, ref_d1, ref_dw = _conv_bwd_ref(dO, O, v, wconv, nh)
-    outs = []
-    for variant in (0, 7):
-        L.lib().tm_debug_set_variant(1, variant)
-        try:
-            dv = torch.full((nbh, n, 64), float("nan"), device=DEV)
-            d1 = torch.full((nbh, n), float("nan"), device=DEV)
-            dw = torch.full((nh * 33,), float("nan"), device=DEV)
-            work = torch.empty(L.query("tm_nys_conv_bwd_workspace", nbags, nh, n) // 4 + 16, device=DEV)
-            dOd, Od, vd, wd = (t.to(DEV).contiguous() for t in (dO, O, v, wconv))
-            L.call("tm_nys_conv_bwd", BF16, _p(dOd), _p(Od), _p(vd), _p(wd), nbh, nh, n, _p(dv), _p(d1), _p(work),
-                   _p(dw), _stream())
-            torch.cuda.synchronize()
-        finally:
-            L.lib().tm_debug_set_variant(1, 0)
-        assert torch.isfinite(dv).all() and torch.isfinite(d1).all() and torch.isfinite(dw).all(), variant
-        assert _rel(dv.cpu(), ref_dv) < 1e-5, variant
-        assert (d1.cpu().double() - ref_d1).abs().max().item() < 1e-3 * ref_d1.abs().max().item(), variant
-        assert _rel(dw.cpu().view(nh, 33), ref_dw) < 1e-5, variant
-        outs.append(dv.cpu())
-    assert _rel(outs[0], outs[1].double()) < 1e-5
+    dv = torch.full((nbh, n, 64), float("nan"), device=DEV)
+    d1 = torch.full((nbh, n), float("nan"), device=DEV)
+    dw = torch.full((nh * 33,), float("nan"), device=DEV)
+    work = torch.empty(L.query("tm_nys_conv_bwd_workspace", nbags, nh, n) // 4 + 16, device=DEV)
+    dOd, Od, vd, wd = (t.to(DEV).contiguous() for t in (dO, O, v, wconv))
+    L.call("tm_nys_conv_bwd", BF16, _p(dOd), _p(Od), _p(vd), _p(wd), nbh, nh, n, _p(dv), _p(d1), _p(work),
+           _p(dw), _stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(dv).all() and torch.isfinite(d1).all() and torch.isfinite(dw).all()
+    assert _rel(dv.cpu(), ref_dv) < 1e-5
+    assert (d1.cpu().double() - ref_d1).abs().max().item() < 1e-3 * ref_d1.abs().max().item()
+    assert _rel(dw.cpu().view(nh, 33), ref_dw) < 1e-5
 
 
 # ----------------------------------------------------------------------------- A3 attention backward
@@ -502,8 +471,7 @@ def _a3_bwd_ref(ql, dw, k, v):
 @pytest.mark.parametrize("nbh,n", [(8, 256), (2, 1280), (8, 1280), (8, 8448), (16, 8448)])
 def test_a3_bwd_bf16_even_split(nbh, n):
     """The bf16 A3 backward (key units split evenly over the workgroups of a head: the 9-wave
-    form at 8 heads x 8448 keys, short workgroups elsewhere) and the legacy per-256-key-block
-    kernel (variant 3) against fp64."""
+    form at 8 heads x 8448 keys, short workgroups elsewhere) against fp64."""
     L = _lib()
     from transmil_deepgraft_amd._lib import BF16
     from transmil_deepgraft_amd.engine import _p, _stream
@@ -513,28 +481,19 @@ def test_a3_bwd_bf16_even_split(nbh, n):
     k = (torch.randn(nbh, n, 64, generator=g) * 0.3).to(torch.bfloat16)
     v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16)
     lse, d, ref_dk, ref_dv, ref_dql = _a3_bwd_ref(ql, dw, k, v)
-    outs = []
-    for variant in (0, 3):
-        L.lib().tm_debug_set_variant(1, variant)
-        try:
-            dk = torch.full((nbh, n, 64), float("nan"), device=DEV)
-            dv = torch.zeros(nbh, n, 64, device=DEV)           # accumulated into (+=)
-            dql = torch.full((nbh, 256, 64), float("nan"), device=DEV)
-            work = torch.empty(L.query("tm_nys_a3_bwd_workspace", nbh, n) // 4 + 16, device=DEV)
-            qd, wd, kd, vd = (t.to(DEV).contiguous() for t in (ql, dw, k, v))
-            lsed, dd = lse.float().to(DEV).contiguous(), d.float().to(DEV).contiguous()
-            L.call("tm_nys_a3_bwd", BF16, _p(qd), _p(wd), _p(kd), _p(vd), _p(lsed), _p(dd), nbh, 8, n,
-                   _p(dk), _p(dv), _p(work), _p(dql), 0, _stream())
-            torch.cuda.synchronize()
-        finally:
-            L.lib().tm_debug_set_variant(1, 0)
-        assert torch.isfinite(dk).all() and torch.isfinite(dv).all() and torch.isfinite(dql).all(), variant
-        assert _rel(dk.cpu(), ref_dk) < 2e-2, variant
-        assert _rel(dv.cpu(), ref_dv) < 2e-2, variant
-        assert _rel(dql.cpu(), ref_dql) < 2e-2, variant
-        outs.append((dk.cpu(), dv.cpu(), dql.cpu()))
-    for x, y in zip(*outs):
-        assert _rel(x, y.double()) < 2e-2
+    dk = torch.full((nbh, n, 64), float("nan"), device=DEV)
+    dv = torch.zeros(nbh, n, 64, device=DEV)           # accumulated into (+=)
+    dql = torch.full((nbh, 256, 64), float("nan"), device=DEV)
+    work = torch.empty(L.query("tm_nys_a3_bwd_workspace", nbh, n) // 4 + 16, device=DEV)
+    qd, wd, kd, vd = (t.to(DEV).contiguous() for t in (ql, dw, k, v))
+    lsed, dd = lse.float().to(DEV).contiguous(), d.float().to(DEV).contiguous()
+    L.call("tm_nys_a3_bwd", BF16, _p(qd), _p(wd), _p(kd), _p(vd), _p(lsed), _p(dd), nbh, 8, n,
+           _p(dk), _p(dv), _p(work), _p(dql), 0, _stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(dk).all() and torch.isfinite(dv).all() and torch.isfinite(dql).all()
+    assert _rel(dk.cpu(), ref_dk) < 2e-2
+    assert _rel(dv.cpu(), ref_dv) < 2e-2
+    assert _rel(dql.cpu(), ref_dql) < 2e-2
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

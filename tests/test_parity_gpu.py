@@ -27,13 +27,18 @@ def _pair(ncls, feat=512, seed=2021, dtype=torch.float32):
 
 
 def _ref64(ref, x, **kw):
-    """Run the oracle in fp64 (its `x.float()` at :174 is bypassed)."""
+    """Run the oracle in fp64 (its `x.float()` at :174 is bypassed).  Without ``return_attn``
+    the unused [B,h,n',n'] product of TransLayer (:47) is skipped: it reaches neither the logits
+    nor any gradient, and at N = 32768 it would need 71 GB."""
+    from oracle.transmil_ref import TransLayer
     orig = torch.Tensor.float
     torch.Tensor.float = lambda self, *a, **k: self
+    TransLayer.compute_attn = bool(kw.get("return_attn", False))
     try:
         return ref(x.double(), **kw)
     finally:
         torch.Tensor.float = orig
+        TransLayer.compute_attn = True
 
 
 def _ref_forward_backward(ref, x, label, ncls):
@@ -54,7 +59,7 @@ def _ours_forward_backward(ours, x, label, ncls):
 
 
 @pytest.mark.parametrize("N,B,ncls", [(1, 1, 2), (2, 1, 2), (3, 1, 2), (100, 1, 2), (1000, 1, 2),
-                                      (257, 1, 3), (300, 2, 2), (4000, 1, 3)])
+                                      (257, 1, 3), (300, 2, 2), (4000, 1, 3), (8192, 1, 2)])
 def test_transmil_fp32_logits_and_grads(N, B, ncls):
     ref, ours = _pair(ncls)
     x = torch.from_numpy(bag_input(N, 512, 77 + N, B))
@@ -86,8 +91,8 @@ def test_golden_d512_logits(name, N):
 def test_golden_long_sequence_c3(dtype, atol):
     """Config C3 (SURVEY.md section 8 d): 3-class, N = 32768 (n' = 33280, l = 130) against
     the oracle-generated fixture (tests/golden/make_golden_long.py); fp32 within 1e-4, bf16
-    within 5e-2, argmax equal.  Then one bf16 train-mode backward at that size: every
-    gradient finite and nonzero."""
+    within 5e-2, argmax equal.  The train-mode backward at this size is checked against the
+    fp64 oracle in test_train_mode_dropout_matches_oracle_with_same_mask."""
     fx = load("d512c3_n32768")
     _, ours = _pair(3, dtype=dtype)
     N = 32768
@@ -96,16 +101,6 @@ def test_golden_long_sequence_c3(dtype, atol):
         lo = ours(x).cpu().numpy()
     np.testing.assert_allclose(lo, fx["logits.f64"], rtol=0, atol=atol)
     assert (lo.argmax(1) == fx["logits"].argmax(1)).all()
-    if dtype == torch.bfloat16:
-        ours.train()
-        logits = ours(x)
-        loss = torch.nn.CrossEntropyLoss()(logits, torch.nn.functional.one_hot(
-            torch.tensor([2], device=DEV), 3).float())
-        loss.backward()
-        torch.cuda.synchronize()
-        for name, p in ours.named_parameters():
-            assert torch.isfinite(p.grad).all(), name
-            assert p.grad.abs().max() > 0, name
 
 
 @pytest.mark.parametrize("name", ["d512_b4_n300", "d512_peaky_n1024", "d512c3_ref_n32768"])
@@ -170,29 +165,6 @@ def test_bf16_mode_grads_close_to_oracle(N):
         if err > 6e-2:
             bad.append((name, err))
     assert not bad, bad
-
-
-def test_bf16_staged_attention_backward_matches_the_per_chunk_one():
-    """The once-staged bf16 attention backward (default: the A1 queries split evenly over one
-    workgroup per CU) and the per-chunk-staged one (variant 3: 256-query blocks) compute the
-    same products; only the partition of the landmark-gradient partial sums differs (32 vs 12
-    slabs at N = 3000, n' = 3072); the fp32 partial sums differ in rounding, which can flip a
-    bf16 rounding downstream, so the gradients agree within 2e-3 (the bf16 gate is 6e-2)."""
-    from transmil_deepgraft_amd import _lib
-    ref, ours = _pair(2, dtype=torch.bfloat16)
-    x = torch.from_numpy(bag_input(3000, 512, 7))
-    grads = []
-    for variant in (0, 3):
-        _lib.lib().tm_debug_set_variant(1, variant)
-        try:
-            ours.zero_grad(set_to_none=True)
-            _, g = _ours_forward_backward(ours, x, 0, 2)
-        finally:
-            _lib.lib().tm_debug_set_variant(1, 0)
-        grads.append(g)
-    for name in grads[0]:
-        a, b = grads[0][name].double(), grads[1][name].double()
-        assert ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item() < 2e-3, name
 
 
 def test_return_attn_contract():
@@ -335,23 +307,34 @@ def dropout_keep(seed_dev_value, layer_seed, rows, cols, p):
     return u >= p
 
 
-def test_train_mode_dropout_matches_oracle_with_same_mask():
-    """Train mode (dropout 0.7 on to_out): the forward mask and the mask the
-    backward re-derives equal the host restatement of the kernel hash; logits and
-    every gradient match the oracle with that mask applied (fp32 parity mode)."""
+@pytest.mark.parametrize("N,ncls,dtype,ltol,gtol", [
+    (300, 2, torch.float32, 1e-4, 2e-3),
+    (8192, 2, torch.float32, 1e-4, 2e-3),      # config C2's shape in the fp32 parity mode
+    (8192, 2, torch.bfloat16, 5e-2, 6e-2),     # config C2 exactly as bench.py times it
+    (32768, 3, torch.bfloat16, 5e-2, 6e-2),    # config C3
+])
+def test_train_mode_dropout_matches_oracle_with_same_mask(N, ncls, dtype, ltol, gtol):
+    """Train mode (dropout 0.7 on to_out), the step the reference trains with
+    (code/models/model_interface.py:333-349 -> code/models/TransMIL.py:167-211): the mask the
+    kernels draw is replayed into the fp64 oracle through the host restatement of the kernel
+    hash, then logits and EVERY parameter gradient are compared (relative to each tensor's
+    largest entry).  fp32 parity mode: logits 1e-4, gradients 2e-3.  bf16 bench mode (the
+    configuration bench.py times, N = 8192; and config C3, N = 32768, 3-class): logits 5e-2,
+    gradients 6e-2 (bf16 operands carry ~3 significant digits)."""
     import math
     from transmil_deepgraft_amd.engine import TransMILEngine
-    ref, ours = _pair(2)
+    ref, ours = _pair(ncls, dtype=dtype)
     ours.train()
-    N, B = 300, 1
+    B = 1
     G = math.ceil(math.sqrt(N))
     S = G * G + 1
     npad = (S + 255) // 256 * 256
     pad = npad - S
     seed_val = int(ours._dropout_counter.item()) + 1
     layer_seeds = TransMILEngine.forward.__defaults__[1]
-    x = torch.from_numpy(bag_input(N, 512, 21, B))
-    lo, go = _ours_forward_backward(ours, x, 1, 2)
+    x = torch.from_numpy(bag_input(N, 512, 21 + N, B))
+    label = ncls - 1
+    lo, go = _ours_forward_backward(ours, x, label, ncls)
     hooks = []
     for li, layer in ((0, ref.layer1), (1, ref.layer2)):
         keep = dropout_keep(seed_val, layer_seeds[li], B * S, 512, 0.7).reshape(B, S, 512)
@@ -363,15 +346,15 @@ def test_train_mode_dropout_matches_oracle_with_same_mask():
             return out
         hooks.append(layer.attn.to_out[0].register_forward_hook(hook))
     try:
-        lr, gr = _ref_forward_backward(ref, x, 1, 2)
+        lr, gr = _ref_forward_backward(ref, x, label, ncls)
     finally:
         for h in hooks:
             h.remove()
-    np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=1e-4)
+    np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=ltol)
     bad = []
     for name, g in gr.items():
         err = ((go[name].double() - g).abs().max() / g.abs().max().clamp_min(1e-12)).item()
-        if err > 2e-3:
+        if err > gtol:
             bad.append((name, err))
     assert not bad, bad
 

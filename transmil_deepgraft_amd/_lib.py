@@ -94,8 +94,6 @@ _SIGS = {
     "tm_nys_assemble_q": (I, [I, P, I, P, P, I, I, I, Fl, P, P]),
     "tm_nys_attn_row": (I, [I, P, P, P, P, P, P, I, I, I, P, P]),
     "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
-    "tm_debug_set_variant": (None, [I, I]),
-    "tm_debug_xcc_map": (I, [P, I, I, P]),
     "tm_pinv_saved_floats": (L, [I, I]),
     "tm_pinv_fwd": (I, [P, I, I, I, P, P]),
     "tm_pinv_bwd_workspace_floats": (L, [I]),
@@ -136,6 +134,18 @@ _SIGS = {
 
 EXPORTED = tuple(_SIGS)
 
+# Entry points of the diagnostic build only (`make -C transmil_deepgraft_amd/csrc diag` ->
+# libtransmil_hip_diag.so, selected with TRANSMIL_HIP_LIB; scripts/microbench.py): kernel-variant
+# switches and timing stamps.  Not part of the ABI; the product library does not export them.
+DIAG_SIGS = {
+    "tm_debug_set_variant": (None, [I, I]),
+    "tm_debug_xcc_map": (I, [P, I, I, P]),
+    "tm_debug_set_split_variant": (None, [I]),
+    "tm_debug_set_split_stamps": (None, [P]),
+    "tm_debug_a1_stamps": (I, [P, I]),
+    "tm_debug_gemm_stamps": (I, [P, I]),
+}
+
 _lib = None
 
 
@@ -152,6 +162,11 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in DIAG_SIGS.items():
+            if hasattr(handle, name):
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
         _lib = handle
     return _lib
 

@@ -27,6 +27,16 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 
 #define TM_DEV __device__ __forceinline__
 
+// Ablation / diagnostic switches exist only in the TM_DIAG build (`make diag` ->
+// libtransmil_hip_diag.so, loaded by scripts/microbench.py through TRANSMIL_HIP_LIB).  The product
+// library has no process-global mutable state: every selector is the constant 0 (the default
+// kernel), the alternative kernels are not compiled and no tm_debug_* symbol is exported.
+#ifdef TM_DIAG
+#define TM_DIAG_VAR(v) (v)
+#else
+#define TM_DIAG_VAR(v) 0
+#endif
+
 template <typename T> struct V8;
 template <> struct V8<bf16> { typedef bf16x8 type; };
 template <> struct V8<float> { typedef f32x8 type; };

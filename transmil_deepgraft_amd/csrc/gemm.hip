@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ A, cons
 //     -> fragment = two ds_read_b64_tr_b16 (4 k-rows x 2 chunks per 16-lane group all distinct)
 constexpr int NSTAGE = 4;
 constexpr int STAGE_BYTES = 2 * 128 * 64 * 2;  // A + B images
-constexpr int RING_BYTES = NSTAGE * STAGE_BYTES;
+[[maybe_unused]] constexpr int RING_BYTES = NSTAGE * STAGE_BYTES;
 
 // One operand image of one stage: 16 wave-instructions of 1 KB, 2 per wave (8 waves).
 template <bool KSTRIDED>
@@ -739,7 +739,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
 // image 64 rows x EP_ROW fp32 (two halves per tile).  Same fragment reads and epilogue as the
 // ring kernel above; the split-K index rides in the tile id.
 constexpr int PSTAGE = 3;
-constexpr int PERSIST_LDS = PSTAGE * STAGE_BYTES + 64 * EP_ROW * 4;
+[[maybe_unused]] constexpr int PERSIST_LDS = PSTAGE * STAGE_BYTES + 64 * EP_ROW * 4;
 
 struct PTile {
   int i, t, m0, n0, split, kbeg, nk, kt;
@@ -1039,7 +1039,10 @@ constexpr size_t gemm_smem() {
 // on a CU shares its operand intake instead of waiting for a second round (QKV 32.2 vs 36.5 us
 // big-tile; to_out 17.9 vs 21.0 register-staged; dxn 31.1 vs 36.4; fc1 18.3 vs 25.3; weight
 // grads 19.3 / 35.6 / 29.1 vs 21.5 / 39.1 / 38.1; scripts/dev/gemm_shapes.py)
+#ifdef TM_DIAG
 int g_gemm_variant = 0;
+#endif
+#define GEMM_VARIANT TM_DIAG_VAR(g_gemm_variant)
 
 // the specialised epilogue a launch can use (EK_ANY keeps the runtime-mode one)
 inline int epilogue_kind(const tm_gemm_args& g) {
@@ -1051,7 +1054,7 @@ inline int epilogue_kind(const tm_gemm_args& g) {
 
 template <typename OutT>
 bool ring_ok(const tm_gemm_args& g) {
-  if (g_gemm_variant != 0 && g_gemm_variant != 8 && (g_gemm_variant < 2 || g_gemm_variant > 6 || g_gemm_variant == 3)) return false;
+  if (GEMM_VARIANT != 0 && GEMM_VARIANT != 8 && (GEMM_VARIANT < 2 || GEMM_VARIANT > 6 || GEMM_VARIANT == 3)) return false;
   // whole 64-deep k-tiles in every split; k-strided operands need >= 8 rows/cols (clamped 16-B pieces)
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if ((g.a_trans && g.M < 8) || (g.b_kn && g.N < 8)) return false;
@@ -1062,7 +1065,7 @@ bool ring_ok(const tm_gemm_args& g) {
 
 template <typename OutT>
 bool big_ok(const tm_gemm_args& g) {
-  if (g_gemm_variant != 7) return false;
+  if (GEMM_VARIANT != 7) return false;
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if (g.a_trans && (g.M % 8 != 0 || g.M < 8)) return false;
   if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
@@ -1073,6 +1076,7 @@ template <typename T, typename OutT>
 int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.splits);
   if constexpr (sizeof(T) == 2) {
+#ifdef TM_DIAG
     if (big_ok<OutT>(g)) {
 #define TM_BIG_CASE(AT, BKN, TBN)                                                                  \
       if (g.a_trans == AT && g.b_kn == BKN) {                                                      \
@@ -1090,7 +1094,7 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
       }
 #undef TM_BIG_CASE
     }
-    if (ring_ok<OutT>(g) && g_gemm_variant == 4) {
+    if (ring_ok<OutT>(g) && GEMM_VARIANT == 4) {
       const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
       const int ntiles = tiles_m * tiles_n * g.splits;
       const int nwg = ntiles < 256 ? ntiles : 256;
@@ -1105,11 +1109,30 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
       TM_PERSIST_CASE(0, 0) TM_PERSIST_CASE(0, 1) TM_PERSIST_CASE(1, 0) TM_PERSIST_CASE(1, 1)
 #undef TM_PERSIST_CASE
     }
+#endif
     if (ring_ok<OutT>(g)) {
       constexpr size_t epi = (size_t)BM * EP_ROW * sizeof(float);
+#ifdef TM_DIAG
+#define TM_RING_DIAG(AT, BKN)                                                                   \
+        else if (GEMM_VARIANT == 8) {                                                       \
+          constexpr size_t sm = 2 * STAGE_BYTES > epi ? 2 * STAGE_BYTES : epi;                  \
+          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2, true>, sm);                          \
+          gemm_ring_kernel<OutT, AT, BKN, 2, true><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        } else if (GEMM_VARIANT == 6) {                                                       \
+          constexpr size_t sm = 3 * STAGE_BYTES > epi ? 3 * STAGE_BYTES : epi;                  \
+          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 3>, sm);                                \
+          gemm_ring_kernel<OutT, AT, BKN, 3><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        } else {                                                                                \
+          constexpr size_t sm = RING_BYTES > epi ? RING_BYTES : epi;                            \
+          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN>, sm);                                   \
+          gemm_ring_kernel<OutT, AT, BKN><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+        }
+#else
+#define TM_RING_DIAG(AT, BKN)
+#endif
 #define TM_RING_CASE(AT, BKN)                                                                   \
       if (g.a_trans == AT && g.b_kn == BKN) {                                                   \
-        if (g_gemm_variant == 0 || g_gemm_variant == 5) {                                       \
+        if (GEMM_VARIANT == 0 || GEMM_VARIANT == 5) {                                       \
           constexpr size_t sm = 2 * STAGE_BYTES > epi ? 2 * STAGE_BYTES : epi;                  \
           const int kind = epilogue_kind(g);                                                    \
           if (kind == EK_PLAIN) {                                                               \
@@ -1125,45 +1148,43 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
             tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2>, sm);                              \
             gemm_ring_kernel<OutT, AT, BKN, 2><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
           }                                                                                     \
-        } else if (g_gemm_variant == 8) {                                                       \
-          constexpr size_t sm = 2 * STAGE_BYTES > epi ? 2 * STAGE_BYTES : epi;                  \
-          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 2, true>, sm);                          \
-          gemm_ring_kernel<OutT, AT, BKN, 2, true><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
-        } else if (g_gemm_variant == 6) {                                                       \
-          constexpr size_t sm = 3 * STAGE_BYTES > epi ? 3 * STAGE_BYTES : epi;                  \
-          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN, 3>, sm);                                \
-          gemm_ring_kernel<OutT, AT, BKN, 3><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
-        } else {                                                                                \
-          constexpr size_t sm = RING_BYTES > epi ? RING_BYTES : epi;                            \
-          tm_allow_smem(gemm_ring_kernel<OutT, AT, BKN>, sm);                                   \
-          gemm_ring_kernel<OutT, AT, BKN><<<grid, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
         }                                                                                       \
+        TM_RING_DIAG(AT, BKN)                                                                   \
         TM_CHECK_LAUNCH();                                                                      \
         return 0;                                                                               \
       }
       TM_RING_CASE(0, 0) TM_RING_CASE(0, 1) TM_RING_CASE(1, 0) TM_RING_CASE(1, 1)
 #undef TM_RING_CASE
+#undef TM_RING_DIAG
     }
   }
   const T* a = (const T*)A;
   const T* b = (const T*)B;
   OutT* c = (OutT*)C;
-#define TM_GEMM_CASE(AT, BKN)                                                       \
-  if (g.a_trans == AT && g.b_kn == BKN) {                                           \
-    if (g_gemm_variant != 1) {                                                      \
-      constexpr size_t sm = gemm_smem<T, AT, BKN, 1>();                             \
-      tm_allow_smem(gemm_kernel<T, OutT, AT, BKN, 1>, sm);                          \
-      gemm_kernel<T, OutT, AT, BKN, 1><<<grid, 256, sm, st>>>(a, b, c, g);          \
-    } else {                                                                        \
+#ifdef TM_DIAG
+#define TM_GEMM_2BUF(AT, BKN)                                                       \
+    if (GEMM_VARIANT == 1) {                                                        \
       constexpr size_t sm = gemm_smem<T, AT, BKN>();                                \
       tm_allow_smem(gemm_kernel<T, OutT, AT, BKN>, sm);                             \
       gemm_kernel<T, OutT, AT, BKN><<<grid, 256, sm, st>>>(a, b, c, g);             \
-    }                                                                               \
+      TM_CHECK_LAUNCH();                                                            \
+      return 0;                                                                     \
+    }
+#else
+#define TM_GEMM_2BUF(AT, BKN)
+#endif
+#define TM_GEMM_CASE(AT, BKN)                                                       \
+  if (g.a_trans == AT && g.b_kn == BKN) {                                           \
+    TM_GEMM_2BUF(AT, BKN)                                                           \
+    constexpr size_t sm = gemm_smem<T, AT, BKN, 1>();                               \
+    tm_allow_smem(gemm_kernel<T, OutT, AT, BKN, 1>, sm);                            \
+    gemm_kernel<T, OutT, AT, BKN, 1><<<grid, 256, sm, st>>>(a, b, c, g);            \
     TM_CHECK_LAUNCH();                                                              \
     return 0;                                                                       \
   }
   TM_GEMM_CASE(0, 0) TM_GEMM_CASE(0, 1) TM_GEMM_CASE(1, 0) TM_GEMM_CASE(1, 1)
 #undef TM_GEMM_CASE
+#undef TM_GEMM_2BUF
   tm_set_error("gemm: bad transpose flags");
   return 1;
 }
@@ -1250,6 +1271,7 @@ extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args
   return launch_t<float, float>(A, B, C, *g, st);
 }
 
+#ifdef TM_DIAG
 extern "C" void tm_debug_set_gemm_variant(int value) { g_gemm_variant = value; }
 
 // copy the variant-8 ring stamps ([block][8] u64) to a host buffer (diagnostics only)
@@ -1261,6 +1283,7 @@ extern "C" int tm_debug_gemm_stamps(unsigned long long* host, int count) {
   }
   return 0;
 }
+#endif
 
 // ---- deferred reductions: the parameter-gradient slab sums of a backward, queued while the
 // engine has deferral on and summed by ONE launch at tm_reduce_flush (a kernel boundary costs

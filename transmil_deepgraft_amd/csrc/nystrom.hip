@@ -1176,7 +1176,10 @@ struct BwdArgs {
 };
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
+#ifdef TM_DIAG
 int g_nys_variant = 0;
+#endif
+#define NYS_VARIANT TM_DIAG_VAR(g_nys_variant)
 
 template <typename T> struct BwdLay {
   static constexpr int QT_ROW = 32 + 4;              // Q^T / dO^T chunk [64 d][36]
@@ -1734,6 +1737,7 @@ __global__ void assemble_q_kernel(const float* __restrict__ dq, int dq_row, cons
 }  // namespace
 
 // ============================ C entry points ===============================
+#ifdef TM_DIAG
 extern "C" void tm_debug_set_nys_variant(int value) { g_nys_variant = value; }
 // copy the VAR 9 a1_fwd stamps ([block][wave][8] u64) to a host buffer (diagnostics only)
 extern "C" int tm_debug_a1_stamps(unsigned long long* host, int count) {
@@ -1744,6 +1748,7 @@ extern "C" int tm_debug_a1_stamps(unsigned long long* host, int count) {
   }
   return 0;
 }
+#endif
 
 #define TM_DTYPE_DISPATCH(dt, CALL)                               \
   if ((dt) == TM_BF16) { using T = bf16; CALL; }                  \
@@ -1808,14 +1813,18 @@ extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void
                              const float* wconv, int nbh, int nh, int n, void* merged, float* lse1, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0 && nbh % nh == 0, "a1_fwd: bad shape");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TM_BF16 && g_nys_variant != 14) {
+  if (dtype == TM_BF16 && NYS_VARIANT != 14) {
     const int cph = n / 32;
     int wpg = std::max(1, std::min(256 / std::max(nbh, 1), cph));
     wpg = std::max(wpg, (cph + A1P_MAXCH - 1) / A1P_MAXCH);  // <= A1P_MAXCH chunks per workgroup
+#ifdef TM_DIAG
     // ablation variants 11-19 (microbench only): 10 + VAR
-    auto kern = g_nys_variant == 11 ? a1_fwd_bf16_kernel<1> : g_nys_variant == 12 ? a1_fwd_bf16_kernel<2>
-              : g_nys_variant == 13 ? a1_fwd_bf16_kernel<3> : g_nys_variant == 19 ? a1_fwd_bf16_kernel<9>
+    auto kern = NYS_VARIANT == 11 ? a1_fwd_bf16_kernel<1> : NYS_VARIANT == 12 ? a1_fwd_bf16_kernel<2>
+              : NYS_VARIANT == 13 ? a1_fwd_bf16_kernel<3> : NYS_VARIANT == 19 ? a1_fwd_bf16_kernel<9>
               : a1_fwd_bf16_kernel<0>;
+#else
+    auto kern = a1_fwd_bf16_kernel<0>;
+#endif
     tm_allow_smem(kern, A1P_BYTES);
     kern<<<dim3(wpg, nbh), 256, A1P_BYTES, st>>>((const bf16*)q, (const bf16*)v, (const bf16*)kl_t,
                                                                (const bf16*)y_t, wconv, n, nh, wpg, (bf16*)merged,
@@ -1826,7 +1835,11 @@ extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void
   TM_DTYPE_DISPATCH(dtype, ({
     const size_t sm1 = ((size_t)NL * Lay<T>::KROW + Lay<T>::VELEMS) * sizeof(T);
     const size_t sm = sm1 > A1_EPI_BYTES ? sm1 : A1_EPI_BYTES;
-    auto kern = g_nys_variant == 1 ? a1_fwd_kernel<T, 1> : g_nys_variant == 2 ? a1_fwd_kernel<T, 2> : a1_fwd_kernel<T, 0>;
+#ifdef TM_DIAG
+    auto kern = NYS_VARIANT == 1 ? a1_fwd_kernel<T, 1> : NYS_VARIANT == 2 ? a1_fwd_kernel<T, 2> : a1_fwd_kernel<T, 0>;
+#else
+    auto kern = a1_fwd_kernel<T, 0>;
+#endif
     tm_allow_smem(kern, sm);
     kern<<<dim3(n / 128, nbh), 256, sm, st>>>((const T*)q, (const T*)v, (const T*)kl_t,
                                               (const T*)y_t, wconv, n, nh, (T*)merged, lse1);
@@ -1863,7 +1876,7 @@ extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merge
                                void* stream) {
   TM_REQUIRE(nbh % nh == 0 && n > 0, "conv_bwd: bad shape");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TM_BF16 && g_nys_variant != 7) {
+  if (dtype == TM_BF16 && NYS_VARIANT != 7) {
     const int r = conv_bwd_rows(nbh, n), nblk = (n + r - 1) / r;
     tm_allow_smem(conv_bwd_mfma_kernel, CbLay::BYTES);
     conv_bwd_mfma_kernel<<<dim3(nblk, nbh), 512, CbLay::BYTES, st>>>(
@@ -1898,7 +1911,7 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
                              const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
                              float* dq, float* work, float* dkl, float* dy, int accumulate, void* stream) {
   TM_REQUIRE(queries_per_wg % 32 == 0 && n % queries_per_wg == 0, "a1_bwd: queries_per_wg must divide n, x32");
-  const bool split = dtype == TM_BF16 && queries_per_wg <= NL && g_nys_variant != 3;
+  const bool split = dtype == TM_BF16 && queries_per_wg <= NL && NYS_VARIANT != 3;
   const int nqc = split ? a1_bwd_split(nbh, n) : n / queries_per_wg;
   BwdArgs a{};
   a.q = q; a.q_bag = (long long)nh * n * DH; a.q_head = (long long)n * DH; a.q_row = DH;
@@ -1982,7 +1995,7 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
   a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
   hipStream_t st = (hipStream_t)stream;
   int slabs = nkb;
-  if (dtype == TM_BF16 && g_nys_variant != 3) {
+  if (dtype == TM_BF16 && NYS_VARIANT != 3) {
     launch_a3_bwd_bf16(a, nbh, n, st, slabs);
   } else {
     TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A3>, bwd_smem_bytes<T>()),

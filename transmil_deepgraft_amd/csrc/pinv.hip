@@ -421,6 +421,7 @@ void add_term(tm_bmm_job& j, const float* A, int ta, const float* B, int tb) {
 
 }  // namespace
 
+#ifdef TM_DIAG
 // Debug/ablation switch for microbenchmarks only (not part of the supported ABI surface).
 __global__ void xcc_map_kernel(int* out) {
   if (threadIdx.x == 0) out[blockIdx.x] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
@@ -440,6 +441,7 @@ extern "C" void tm_debug_set_variant(int which, int value) {
   if (which == 1) tm_debug_set_nys_variant(value);
   if (which == 2) tm_debug_set_gemm_variant(value);
 }
+#endif
 
 extern "C" int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream) {
   TM_REQUIRE(prec == 0 || prec == 1, "bmm: prec must be 0 (fp32) or 1 (bf16x3)");

@@ -86,8 +86,15 @@ struct SLaunch {
   unsigned long long* stamps;  // diagnostic build only: per-wave s_memtime stamps, or null
 };
 
+#ifdef TM_DIAG
 int g_split_dbg = 0;
 unsigned long long* g_split_stamps = nullptr;
+#define SPLIT_DBG (L.dbg)
+#define SPLIT_STAMPS (L.stamps != nullptr)
+#else
+#define SPLIT_DBG 0
+#define SPLIT_STAMPS false
+#endif
 
 // one s_memtime stamp (shader clock), its own lgkmcnt wait inside the statement
 TM_DEV unsigned long long stamp() {
@@ -270,15 +277,15 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
     if (u < 2 * nbh) abssums(L, head, tile, (float*)smem);
     return;
   }
-  if (L.dbg == 5) return;
+  if (SPLIT_DBG == 5) return;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = (tile >> 2) * 64, n0 = (tile & 3) * 64;
   const size_t hoff = (size_t)head * MAT;
   const long long plane = L.plane;
   const int nch = J.nterms * 4;
-  const int nchl = L.dbg == 4 ? 0 : nch;
-  const bool st_on = L.stamps != nullptr;
+  const int nchl = SPLIT_DBG == 4 ? 0 : nch;
+  const bool st_on = SPLIT_STAMPS;
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (st_on) { ts[0] = rstamp(); ts[1] = stamp(); }
 
@@ -335,7 +342,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
         __builtin_amdgcn_global_load_lds((glb_t*)(base + (kr ? loff[1][i] : loff[0][i])), (lds_t*)(img + i * 1024),
                                          16, 0, 0);
     };
-    if (L.dbg != 1) {
+    if (SPLIT_DBG != 1) {
       issue(0);
       issue(1);  // nch >= 4
     }
@@ -343,7 +350,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
       if (c + 1 < nch) wait_vm<PPW>(); else wait_vm<0>();
       __builtin_amdgcn_s_barrier();  // chunk c landed (every producer); slot (c+2)%3 read by every consumer
       asm volatile("" ::: "memory");
-      if (c + 2 < nch && L.dbg != 1) issue(c + 2);
+      if (c + 2 < nch && SPLIT_DBG != 1) issue(c + 2);
     }
   } else {  // ---------------------------------------------------------------- consumer
     const int wm = wv >> 1, wn = wv & 1;
@@ -362,7 +369,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
       __builtin_amdgcn_s_barrier();  // chunk c landed; every consumer is done with chunk c-1
       asm volatile("" ::: "memory");
       if (st_on && c == 0) ts[3] = stamp();
-      if (L.dbg == 2) continue;
+      if (SPLIT_DBG == 2) continue;
       const unsigned sb = (c % NSLOT) * SLOT;
       switch ((c >> 2) ? code1 : code0) {
         case 0: chunk_mma<0, 0>(acc, sb, akr, bkr, akc, bkc); break;
@@ -378,7 +385,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
     for (int r = 0; r < 16; ++r) ep[(wm * 32 + acc_row(r, h)) * EROW + wn * 32 + cc] = acc[r];
   }
   __syncthreads();  // the tile is in `ep`; every wave (producers too) takes one 8-element row piece
-  if (L.dbg == 3 || !epi) return;
+  if (SPLIT_DBG == 3 || !epi) return;
   const float diag = J.diag, e1s = J.e1s, e2s = J.e2s;
   float ic = 1.f;
   if (need_c) ic = nbh <= 64 ? 1.f / (wave_max(mcv) * wave_max(mrv)) : inv_c(L.maxima, nbh);
@@ -572,8 +579,10 @@ struct Launcher {
   SLaunch L{};
   explicit Launcher(int nbh, long long plane, const float* maxima) {
     L.nbh = nbh; L.plane = plane; L.maxima = maxima;
+#ifdef TM_DIAG
     L.dbg = g_split_dbg;
     L.stamps = g_split_stamps;
+#endif
   }
   void add(const SJob& j) { L.j[L.njobs++] = j; }
   int go(hipStream_t st) {
@@ -581,7 +590,9 @@ struct Launcher {
     const dim3 grid(16 * L.nbh, L.njobs);
     pinv_stage_kernel<<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
     TM_CHECK_LAUNCH();
+#ifdef TM_DIAG
     if (g_split_stamps) g_split_stamps += (size_t)grid.x * grid.y * 4 * 8;  // the next launch's stamps follow
+#endif
     return 0;
   }
 };
@@ -750,9 +761,11 @@ extern "C" int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int it
   return 0;
 }
 
+#ifdef TM_DIAG
 extern "C" void tm_debug_set_split_variant(int v) { g_split_dbg = v; }
 // diagnostic: per-wave stamps (8 x u64 per wave, 8 waves per workgroup) of every later stage launch; null: off
 extern "C" void tm_debug_set_split_stamps(unsigned long long* buf) { g_split_stamps = buf; }
+#endif
 
 // fp32 -> split planes (hi at dst, lo at dst + count), count a multiple of 8
 __global__ void split_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long count) {

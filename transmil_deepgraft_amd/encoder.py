@@ -94,6 +94,7 @@ class RetCCLResNet50(nn.Module):
         self.chunk = chunk
         self.channels_last = True
         self._folded = None
+        self._folded_key = None
         for p in self.parameters():                     # model_interface.py:243-244
             p.requires_grad = False
 
@@ -129,6 +130,14 @@ class RetCCLResNet50(nn.Module):
         return self.load_state_dict({k: v for k, v in sd.items() if not k.startswith("fc.")}, strict=False)
 
     # ------------------------------------------------------------------ eval: folded convolutions
+    def _fold_key(self):
+        """Identity of every parameter and buffer the folded weights derive from (storage and
+        in-place version counter): a checkpoint loaded through a parent module, ``.to()``, an
+        in-place weight edit or a BatchNorm statistics update all change it, so the next eval
+        forward re-folds instead of reading stale conv+BN weights."""
+        return tuple((t.data_ptr(), t._version, t.dtype) for t in
+                     list(self.parameters()) + list(self.buffers()))
+
     def _fold_all(self):
         dt, cl = self.compute_dtype, self.channels_last
         f = {"stem": _fold(self.conv1, self.bn1, dt, cl), "blocks": []}
@@ -181,8 +190,11 @@ class RetCCLResNet50(nn.Module):
             raise RuntimeError("RetCCL encoder (MI355X path) needs a GPU tensor")
         dt = self.compute_dtype
         out = torch.empty(x.shape[0], 2048, dtype=torch.float32, device=x.device)
-        if not self.training and self._folded is None:
-            self._fold_all()
+        if not self.training:
+            key = self._fold_key()
+            if self._folded is None or self._folded_key != key:
+                self._fold_all()
+                self._folded_key = key
         if self.training and self.channels_last and \
                 not self.conv1.weight.is_contiguous(memory_format=torch.channels_last):
             self.to(memory_format=torch.channels_last)

@@ -537,7 +537,10 @@ class TransMILEngine:
             outs = [w.contiguous() for w in ws]
             p["xt"] = None if x2d is None else x2d.contiguous()
         else:
-            srcs = [w.contiguous() for w in ws] + ([x2d.contiguous()] if x2d is not None else [])
+            # the preparation launch casts whole 4-element pieces: a bag whose B*N*F is not a
+            # multiple of 4 (odd in_features) is cast by its own launch instead
+            x_in_table = x2d is not None and x2d.numel() % 4 == 0
+            srcs = [w.contiguous() for w in ws] + ([x2d.contiguous()] if x_in_table else [])
             outs, off = [], 0
             for i, w in enumerate(srcs):
                 o = pool(w.numel(), self.tdtype).view(w.shape)
@@ -546,7 +549,10 @@ class TransMILEngine:
                 outs.append(o)
             tab.count = len(srcs)
             tab.offset[len(srcs)] = off
-            p["xt"] = outs.pop() if x2d is not None else None
+            if x_in_table:
+                p["xt"] = outs.pop()
+            else:
+                p["xt"] = None if x2d is None else self._cast(x2d, pool)
         wqkv1, wo1, wqkv2, wo2 = outs[:4]
         if main is not None:
             p["w1"] = outs[4]

@@ -148,15 +148,26 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
         from . import _lib
         self._lib = _lib
         plist = [p for g in self.param_groups for p in g["params"]]
-        if len(plist) > _lib.OPTIM_MAX_TENSORS:
-            raise ValueError(f"fused RAdam: at most {_lib.OPTIM_MAX_TENSORS} parameter tensors")
         if any(p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous() for p in plist):
             raise ValueError("fused RAdam: parameters must be contiguous fp32 CUDA tensors")
         for g in self.param_groups:
             for key in ("betas", "eps", "lookahead_alpha", "lookahead_k"):
                 if g[key] != self.param_groups[0][key]:
                     raise ValueError(f"fused RAdam: '{key}' must be equal across groups")
+        self._all = plist
+        self._params = None     # the parameters that receive gradients: fixed at the first step
+
+    def _activate(self, plist):
+        """Lay the state of ``plist`` (the parameters with a gradient, in group order) out in three
+        flat fp32 buffers.  Parameters that never receive a gradient (modules kept only for the
+        state_dict, e.g. CTMIL._fc1) are skipped, as torch.optim.RAdam skips ``grad is None``."""
+        if len(plist) > self._lib.OPTIM_MAX_TENSORS:
+            raise ValueError(f"fused RAdam: at most {self._lib.OPTIM_MAX_TENSORS} parameter tensors with "
+                             "gradients (create_optimizer falls back to torch.optim.RAdam above that)")
+        if not plist:
+            raise RuntimeError("fused RAdam: no parameter has a gradient")
         self._params = plist
+        self._index = {id(p): i for i, p in enumerate(plist)}
         total = sum((p.numel() + 3) // 4 * 4 for p in plist)
         dev = plist[0].device
         self._flat = torch.zeros(3, total, dtype=torch.float32, device=dev)  # exp_avg, exp_avg_sq, slow
@@ -180,13 +191,22 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         lib = self._lib
+        if self._params is None:
+            self._activate([p for p in self._all if p.grad is not None])
         tab = lib.OptimTable()
         tab.count = len(self._params)
         i = 0
         for g in self.param_groups:
             for p in g["params"]:
+                if id(p) not in self._index:
+                    if p.grad is not None:
+                        raise RuntimeError("fused RAdam: a parameter without a gradient at the first step has "
+                                           "one now (its step count would differ from torch.optim.RAdam's); "
+                                           "use opt='radam' on a model whose parameter set is fixed")
+                    continue
                 if p.grad is None:
-                    raise RuntimeError("fused RAdam: every parameter needs a gradient each step")
+                    raise RuntimeError("fused RAdam: a parameter that had a gradient at the first step has "
+                                       "none now")
                 t = tab.t[i]
                 t.param, t.grad, t.numel = p.data_ptr(), p.grad.data_ptr(), p.numel()
                 t.lr, t.weight_decay = float(g["lr"]), float(g["weight_decay"])
@@ -204,15 +224,24 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
 
     def state_dict(self):
         sd = super().state_dict()
-        sd["fused_counters"] = self._counters.cpu()
+        if self._params is not None:
+            sd["fused_counters"] = self._counters.cpu()
         return sd
 
     def load_state_dict(self, state_dict):
         counters = state_dict.get("fused_counters")
         super().load_state_dict({k: v for k, v in state_dict.items() if k != "fused_counters"})
         with torch.no_grad():
+            loaded = {p: {k: v.detach().clone() for k, v in self.state[p].items() if torch.is_tensor(v)}
+                      for p in self._all if p in self.state}
+            if self._params is None:
+                stateful = [p for p in self._all if "exp_avg" in loaded.get(p, {})]
+                if not stateful:
+                    return
+                self._activate(stateful)
+            self._bind_state()
             for i, p in enumerate(self._params):
-                st = self.state[p]
+                st = loaded.get(p, {})
                 a, b = self._offsets[i], self._offsets[i] + p.numel()
                 for row, key in enumerate(("exp_avg", "exp_avg_sq", "slow_buffer")):
                     if key in st:
@@ -220,7 +249,6 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
             if counters is not None:
                 self._counters.zero_()
                 self._counters[:2].copy_(counters[:2])
-        self._bind_state()
 
 
 def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float = 2e-4,
@@ -236,7 +264,8 @@ def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float =
     name = parts[-1]
     fused = torch.cuda.is_available()
     on_gpu = fused and all(p.is_cuda for p in model.parameters())
-    if name == "radam" and on_gpu:
+    n_tensors = sum(1 for p in model.parameters() if p.requires_grad)
+    if name == "radam" and on_gpu and n_tensors <= _lib_max_tensors():
         la = len(parts) > 1 and parts[0] == "lookahead"
         return FusedRAdamLookahead(params, lookahead_k=6 if la else 0, **kw)
     if name == "radam":
@@ -253,6 +282,11 @@ def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float =
     if len(parts) > 1 and parts[0] == "lookahead":
         return Lookahead(base)
     return base
+
+
+def _lib_max_tensors():
+    from . import _lib
+    return _lib.OPTIM_MAX_TENSORS
 
 
 class GradBucket:
@@ -301,7 +335,9 @@ class GradBucket:
         return self.flat[a:b]
 
     def bind(self):
-        """Make every ``p.grad`` the bucket's view (keeps existing values by copying them in)."""
+        """Make every existing ``p.grad`` the bucket's view (keeps its values by copying them in).
+        A parameter without a gradient (a module kept only for the state_dict) keeps ``None``, so
+        the optimizer skips it as torch.optim.RAdam does; its slice is zeroed and sums zeros."""
         with torch.no_grad():
             for p in self.params:
                 if not self.owns(p):
@@ -310,7 +346,7 @@ class GradBucket:
                         v.zero_()
                     else:
                         v.copy_(p.grad)
-                    p.grad = v
+                        p.grad = v
 
     def ready(self, i):
         for h in self.hooks:
@@ -369,7 +405,7 @@ class GradAllReduce:
         if not self._active():
             self._works.clear()
             return
-        owned = all(self.bucket.owns(p) for p in self.params)
+        owned = all(self.bucket.owns(p) for p in self.params if p.grad is not None)
         if not owned:
             # gradients produced outside the fused backward (module-by-module path): bind them
             self._works.clear()
