@@ -141,10 +141,17 @@ def main():
     ssaved = torch.empty(_lib.query("tm_pinv_split_saved_floats", nbh, 6), device=dev)
     swork = torch.empty(_lib.query("tm_pinv_bwd_split_workspace_floats", nbh), device=dev)
     sout = torch.empty(nbh, 256, 256, device=dev)
-    for v, nm in ((1, "no DMA"), (2, "no MFMA"), (3, "no epilogue"), (4, "epilogue only"), (5, "empty"), (0, "full")):
+    sdz = torch.empty(2 * nbh * 65536, dtype=torch.bfloat16, device=dev)
+    _lib.call("tm_split_f32", E._p(pdz), E._p(sdz), nbh * 65536, st())
+    for v, nm in ((0, "per-level launches"), (8, "persistent team")):
         _lib.lib().tm_debug_set_split_variant(v)
         case(f"pinv_fwd split [{nm}]", lambda: _lib.call("tm_pinv_fwd_split", E._p(X), E._p(Xs), nbh, 6,
                                                            E._p(ssaved), st()), 24 * f)
+
+        def bwd():
+            swork[:2 * nbh * 65536 // 2].view(torch.bfloat16).copy_(sdz)
+            _lib.call("tm_pinv_bwd_split", E._p(X), E._p(Xs), nbh, 6, E._p(ssaved), E._p(swork), 1, E._p(sout), st())
+        case(f"pinv_bwd split [{nm}]", bwd, 48 * f)
     _lib.lib().tm_debug_set_split_variant(0)
     if args.split_stamps:
         import numpy as np

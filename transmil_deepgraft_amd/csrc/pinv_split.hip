@@ -47,6 +47,12 @@ constexpr int EPI_LDS = 64 * EROW * 4;  // the fp32 output tile (17 KB); one wor
 constexpr int MAXJ = 3;
 constexpr int NPROD = 8;                // producer (LDS-DMA) waves; 4 consumer waves
 constexpr int NTHREADS = 64 * (4 + NPROD);
+// persistent chain kernel (pinv_team_kernel): per XCD a ticket and a done counter on their own
+// 64-B lines, then one error word; a forward and a backward set live at the end of `saved`
+constexpr int TEAM_XCD = 8;
+constexpr int TEAM_STRIDE = 16;                          // u32 words between two XCDs' counters
+constexpr int TEAM_SET_WORDS = TEAM_XCD * TEAM_STRIDE + 16;
+constexpr int TEAM_CTR_WORDS = 2 * TEAM_SET_WORDS;
 
 typedef __attribute__((address_space(3))) void lds_t;
 typedef __attribute__((address_space(1))) void glb_t;
@@ -81,6 +87,7 @@ struct SLaunch {
   const float* X;           // fp32 X (abs-sum jobs)
   float* sums;              // [2][nbh][256] row / column sums (abs-sum jobs)
   float* maxima_out;        // [2][nbh] (abs-sum jobs)
+  unsigned* zero_ctr;       // abs-sum launch: the team kernels' counters to zero (TEAM_CTR_WORDS), or null
   int dbg;                  // ablation (microbench only): 1 no DMA, 2 no LDS reads / MFMA, 3 no epilogue,
                             // 4 epilogue only, 5 empty
   unsigned long long* stamps;  // diagnostic build only: per-wave s_memtime stamps, or null
@@ -89,8 +96,8 @@ struct SLaunch {
 #ifdef TM_DIAG
 int g_split_dbg = 0;
 unsigned long long* g_split_stamps = nullptr;
-#define SPLIT_DBG (L.dbg)
-#define SPLIT_STAMPS (L.stamps != nullptr)
+#define SPLIT_DBG (dbg_)
+#define SPLIT_STAMPS (stamp_out != nullptr)
 #else
 #define SPLIT_DBG 0
 #define SPLIT_STAMPS false
@@ -266,23 +273,18 @@ TM_DEV void abssums(const SLaunch& L, int head, int which, float* red) {
 // epilogue), waves 4-7 producers (wave 4+p issues plane p of every chunk by LDS-DMA: 0 A hi,
 // 1 A lo, 2 B hi, 3 B lo).  One s_barrier per chunk: a chunk is read after the barrier that
 // follows its producers' counted vmcnt wait, and its slot is refilled after the barrier that
-// follows the consumers' last read of it.  Grid: (16 * nbh, njobs); blockIdx.y is the job.
-__global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const SJob& J = L.j[blockIdx.y];
-  const int u = blockIdx.x;
-  const int nbh = L.nbh;
-  const int head = u % nbh, tile = u / nbh;
-  if (J.kind == KIND_ABSSUMS) {
-    if (u < 2 * nbh) abssums(L, head, tile, (float*)smem);
-    return;
-  }
-  if (SPLIT_DBG == 5) return;
+// follows the consumers' last read of it.
+// TEAM: the tile runs inside the persistent chain kernel (pinv_team_kernel): every operand it
+// reads was written by another workgroup of the same XCD in this launch, so the LDS-DMA reads
+// bypass the CU's L1 (sc1, served by the XCD's L2) and so do the epilogue operand loads (nt).
+template <bool TEAM>
+TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* maxima, int head, int tile,
+                       char* smem, unsigned long long* stamp_out, int dbg_) {
+  constexpr int DMA_POL = TEAM ? 16 : 0;   // cache policy of the LDS-DMA: sc1 in the team kernel
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = (tile >> 2) * 64, n0 = (tile & 3) * 64;
   const size_t hoff = (size_t)head * MAT;
-  const long long plane = L.plane;
   const int nch = J.nterms * 4;
   const int nchl = SPLIT_DBG == 4 ? 0 : nch;
   const bool st_on = SPLIT_STAMPS;
@@ -297,13 +299,17 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   const void* e2p = J.e2;
   const int e1f = J.e1_f32, e2f = J.e2_f32;
   f32x4 e1raw[2], e2raw[2];
+  auto ld4 = [&](const f32x4* a) {
+    if constexpr (TEAM) return __builtin_nontemporal_load(a);   // L1 bypass (written in this launch)
+    else return *a;
+  };
   auto eload = [&](const void* e, int f32, f32x4 (&r)[2]) {
     if (f32) {
       const float* q = (const float*)e;
-      r[0] = *(const f32x4*)(q + eoff); r[1] = *(const f32x4*)(q + eoff + 4);
+      r[0] = ld4((const f32x4*)(q + eoff)); r[1] = ld4((const f32x4*)(q + eoff + 4));
     } else {
       const bf16* q = (const bf16*)e;
-      r[0] = *(const f32x4*)(q + eoff); r[1] = *(const f32x4*)(q + plane + eoff);
+      r[0] = ld4((const f32x4*)(q + eoff)); r[1] = ld4((const f32x4*)(q + plane + eoff));
     }
   };
   const bool epi = tid < 512;  // the 512 threads that each own one 8-element piece of the 64x64 tile
@@ -312,7 +318,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   // per-head maxima for 1/c: one raw vector load per lane now, reduced in the epilogue
   const bool need_c = J.alpha_cpow || J.e1_cpow;
   float mcv = -INFINITY, mrv = -INFINITY;
-  if (need_c && nbh <= 64 && lane < nbh) { mcv = L.maxima[lane]; mrv = L.maxima[nbh + lane]; }
+  if (need_c && nbh <= 64 && lane < nbh) { mcv = maxima[lane]; mrv = maxima[nbh + lane]; }
   float* ep = (float*)(smem + STAGE_LDS);  // [64][EROW] fp32 tile for the epilogue
 
   if (wv >= 4) {  // ------------------------------------------------------------ producer
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
 #pragma unroll
       for (int i = 0; i < PPW; ++i)
         __builtin_amdgcn_global_load_lds((glb_t*)(base + (kr ? loff[1][i] : loff[0][i])), (lds_t*)(img + i * 1024),
-                                         16, 0, 0);
+                                         16, 0, DMA_POL);
     };
     if (SPLIT_DBG != 1) {
       issue(0);
@@ -388,7 +394,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   if (SPLIT_DBG == 3 || !epi) return;
   const float diag = J.diag, e1s = J.e1s, e2s = J.e2s;
   float ic = 1.f;
-  if (need_c) ic = nbh <= 64 ? 1.f / (wave_max(mcv) * wave_max(mrv)) : inv_c(L.maxima, nbh);
+  if (need_c) ic = nbh <= 64 ? 1.f / (wave_max(mcv) * wave_max(mrv)) : inv_c(maxima, nbh);
   const float alpha = J.alpha * powc(ic, J.alpha_cpow);
   const float e1m = powc(ic, J.e1_cpow);
   auto edecode = [&](const f32x4 (&r)[2], int f32, float* v) {
@@ -442,11 +448,30 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
     ts[6] = stamp();
     ts[7] = rstamp();
     if (lane == 0) {
-      unsigned long long* o = L.stamps + (((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + wv) * 8;
+      unsigned long long* o = stamp_out + wv * 8;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = ts[i];
     }
   }
+}
+
+// One launch = up to three independent jobs over all heads.  Grid: (16 * nbh, njobs);
+// blockIdx.y is the job.
+__global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const SJob& J = L.j[blockIdx.y];
+  const int u = blockIdx.x;
+  const int nbh = L.nbh;
+  const int head = u % nbh, tile = u / nbh;
+  if (J.kind == KIND_ABSSUMS) {
+    if (u < 2 * nbh) abssums(L, head, tile, (float*)smem);
+    if (L.zero_ctr && u == 0 && threadIdx.x < TEAM_CTR_WORDS) L.zero_ctr[threadIdx.x] = 0u;
+    return;
+  }
+  const int dbg_ = L.dbg;
+  if (SPLIT_DBG == 5) return;
+  unsigned long long* so = L.stamps ? L.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 * 8 : nullptr;
+  stage_tile<false>(J, nbh, L.plane, L.maxima, head, tile, smem, so, dbg_);
 }
 
 // ---------------------------------------------------------------------------
@@ -558,14 +583,13 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------------------
-// host side
-struct Split {  // one split matrix slot: nbh * MAT fp32-equivalents = hi plane + lo plane
-  bf16* p;
-};
+// The chain as levels of independent jobs (shared by the host launch path and the device-side
+// persistent kernel, so both run the same products).
+#define TM_HD __host__ __device__ inline
 
-SOp op(const void* p, int kr) { return SOp{(const bf16*)p, kr, 0}; }
+TM_HD SOp op(const void* p, int kr) { return SOp{(const bf16*)p, kr, 0}; }
 
-SJob product(SOp a, SOp b, void* c, float alpha, float diag = 0.f) {
+TM_HD SJob product(SOp a, SOp b, void* c, float alpha, float diag = 0.f) {
   SJob j{};
   j.kind = KIND_PRODUCT;
   j.nterms = 1;
@@ -575,6 +599,249 @@ SJob product(SOp a, SOp b, void* c, float alpha, float diag = 0.f) {
   return j;
 }
 
+// saved-buffer layout (floats); every slot is nbh*MAT floats
+struct FwdLayout {
+  long long mat;
+  int iters;
+  float* base;
+  TM_HD float* zf() const { return base; }                                      // Z_iters fp32
+  TM_HD bf16* z(int k) const { return (bf16*)(base + (long long)k * mat); }     // Z_k split, k = 1..iters
+  TM_HD bf16* p(int k) const { return (bf16*)(base + (long long)(iters + 1 + k) * mat); }  // P_k, k = 0..iters-1
+  TM_HD bf16* t3(int k) const { return (bf16*)(base + (long long)(2 * iters + 1 + k) * mat); }
+  TM_HD bf16* t5(int k) const { return (bf16*)(base + (long long)(3 * iters + 1 + k) * mat); }
+  TM_HD bf16* scratch(int i) const { return (bf16*)(base + (long long)(4 * iters + 1 + i) * mat); }
+  TM_HD float* sums() const { return base + (long long)(4 * iters + 3) * mat; }
+  TM_HD float* maxima(int nbh) const { return sums() + 2LL * nbh * NL; }
+  // the persistent kernel's counters (forward set 0, backward set 1), 64-B aligned after the maxima
+  TM_HD unsigned* team_ctr(int nbh, int set) const {
+    const uintptr_t e = (uintptr_t)(maxima(nbh) + 2 * nbh);
+    return (unsigned*)((e + 63) & ~(uintptr_t)63) + set * TEAM_SET_WORDS;
+  }
+};
+
+TM_HD FwdLayout fwd_layout(float* saved, int nbh, int iters) {
+  FwdLayout f;
+  f.mat = (long long)nbh * MAT;
+  f.iters = iters;
+  f.base = saved;
+  return f;
+}
+
+struct ChainArgs {
+  const bf16* Xs;   // split X (= A2)
+  float* saved;     // FwdLayout
+  float* work;      // backward workspace (G, dT5, dZa, dP, dT3, dXc, partial dots)
+  int nbh, iters;
+};
+
+// forward levels after L1 (S = X X^T + the |X| sums): A_0, B_0, A_1, B_1, ..., A_{it-1}, B_{it-1}, F
+TM_HD int fwd_levels(int iters) { return 2 * iters + 1; }
+TM_HD int fwd_level_njobs(int iters, int lvl) {
+  if (lvl == 2 * iters) return 1;
+  const int k = lvl >> 1;
+  return (lvl & 1) == 0 ? (k >= 1 ? 2 : 1) : (k + 1 < iters ? 2 : 1);
+}
+TM_HD SJob fwd_level_job(const ChainArgs& a, int lvl, int jn) {
+  const FwdLayout F = fwd_layout(a.saved, a.nbh, a.iters);
+  const int iters = a.iters;
+  if (lvl == 2 * iters) {  // F: Z_iters = 0.25 Z_{iters-1} T5_{iters-1}  (split + fp32)
+    SJob z = iters == 1 ? product(op(a.Xs, 1), op(F.t5(0), 1), F.z(1), 0.25f)
+                        : product(op(F.z(iters - 1), 0), op(F.t5(iters - 1), 1), F.z(iters), 0.25f);
+    if (iters == 1) z.alpha_cpow = 1;
+    z.cf = F.zf();
+    return z;
+  }
+  const int k = lvl >> 1;
+  bf16* R = F.scratch((k + 1) & 1);
+  if ((lvl & 1) == 0) {  // A_k: R = P P (T3 = R - 7P + 15I); Z_k = 0.25 Z_{k-1} T5_{k-1}
+    if (jn == 0) {
+      SJob r;
+      if (k == 0) {  // P_0 = S / c: R = S S / c^2, T3 = R - 7 S/c + 15I, P_0 written as a side output
+        r = product(op(F.scratch(0), 0), op(F.scratch(0), 1), R, 1.f);
+        r.alpha_cpow = 2;
+        r.e1 = F.scratch(0); r.e1_cpow = 1;
+        r.c3 = F.p(0); r.c3_e1 = 1.f;
+      } else {
+        r = product(op(F.p(k), 0), op(F.p(k), 1), R, 1.f);
+        r.e1 = F.p(k);
+      }
+      r.c2 = F.t3(k); r.c2_alpha = 1.f; r.c2_diag = 15.f; r.c2_e1 = -7.f;
+      return r;
+    }
+    SJob z = k == 1 ? product(op(a.Xs, 1), op(F.t5(0), 1), F.z(1), 0.25f)           // Z_0 = X^T / c
+                    : product(op(F.z(k - 1), 0), op(F.t5(k - 1), 1), F.z(k), 0.25f);
+    if (k == 1) z.alpha_cpow = 1;
+    return z;
+  }
+  // B_k: T5 = 13I - P T3; P_{k+1} = 3.25 P - 0.25 R T3
+  if (jn == 0) return product(op(F.p(k), 0), op(F.t3(k), 1), F.t5(k), -1.f, 13.f);
+  SJob p = product(op(R, 0), op(F.t3(k), 1), F.p(k + 1), -0.25f);
+  p.e1 = F.p(k); p.e1s = 3.25f;
+  return p;
+}
+
+// backward levels (the reference graph's adjoint), 4 per iteration, k = iters-1 .. 0
+TM_HD int bwd_levels(int iters) { return 4 * iters; }
+TM_HD int bwd_level_njobs(int iters, int lvl) { return (lvl & 3) == 2 ? 1 : 2; }
+TM_HD SJob bwd_level_job(const ChainArgs& a, int lvl, int jn) {
+  const FwdLayout F = fwd_layout(a.saved, a.nbh, a.iters);
+  const long long mat = F.mat;
+  float* work = a.work;
+  bf16* G = (bf16*)work;
+  bf16* dT5 = (bf16*)(work + mat);
+  bf16* dZa = (bf16*)(work + 2 * mat);
+  bf16* dP = (bf16*)(work + 3 * mat);
+  bf16* dT3 = (bf16*)(work + 4 * mat);
+  float* dXc = work + 5 * mat;
+  const int k = a.iters - 1 - (lvl >> 2);
+  switch (lvl & 3) {
+    case 0:  // dT5 = 0.25 Z_k^T G ; dZa = 0.25 G T5_k^T
+      if (jn == 0) {
+        SJob j = k == 0 ? product(op(a.Xs, 0), op(G, 1), dT5, 0.25f)          // Z_0^T = X / c
+                        : product(op(F.z(k), 1), op(G, 1), dT5, 0.25f);
+        if (k == 0) j.alpha_cpow = 1;
+        return j;
+      }
+      return product(op(G, 0), op(F.t5(k), 0), dZa, 0.25f);
+    case 1:  // dP = -dT5 T3^T ; dT3 = -P^T dT5
+      if (jn == 0) return product(op(dT5, 0), op(F.t3(k), 0), dP, -1.f);
+      return product(op(F.p(k), 1), op(dT5, 1), dT3, -1.f);
+    case 2: {  // dP += dT3 P^T + P^T dT3 - 7 dT3   (T3 = P P - 7P + 15I)
+      SJob j = product(op(dT3, 0), op(F.p(k), 0), dP, 1.f);
+      j.nterms = 2;
+      j.a[1] = op(F.p(k), 1); j.b[1] = op(dT3, 1);
+      j.e1 = dP; j.e1s = 1.f;
+      j.e2 = dT3; j.e2s = -7.f;
+      return j;
+    }
+    default:  // dX (+)= dP Z_k^T ; G = dZa + X^T dP
+      if (jn == 0) {
+        SJob j = k == 0 ? product(op(dP, 0), op(a.Xs, 1), dXc, 1.f)            // Z_0^T = X / c
+                        : product(op(dP, 0), op(F.z(k), 0), dXc, 1.f);
+        if (k == 0) j.alpha_cpow = 1;
+        j.c_f32 = 1;
+        if (k != a.iters - 1) { j.e1 = dXc; j.e1_f32 = 1; j.e1s = 1.f; }
+        return j;
+      }
+      SJob g = product(op(a.Xs, 1), op(dP, 1), G, 1.f);
+      g.e1 = dZa; g.e1s = 1.f;
+      return g;
+  }
+}
+
+#ifdef TM_DIAG
+// ---------------------------------------------------------------------------
+// Persistent chain kernel: every level of the forward (after L1) or of the backward in ONE
+// launch, instead of one launch per level (each launch boundary + ramp + first operand fetch
+// from beyond L2 costs ~3-4 us of the ~6.5 us a level took).
+//
+// Teams by XCD: a workgroup reads its XCD (HW_REG_XCC_ID) and works only on the heads
+// h = xcd (mod 8).  Every matrix of a head is then written and read by workgroups of ONE XCD
+// within this launch, so the hand-off stays in that XCD's L2 (the L2 is the coherence point of
+// its CUs): producers store plainly and drain (s_waitcnt vmcnt(0), barrier) before one
+// device-scope atomic add on the team's done counter; consumers poll it with L1-bypassing loads
+// and read every operand with L1-bypassing loads (LDS-DMA sc1, epilogue operands nt), so no
+// stale L1 line is ever used and no L2 write-back / invalidate is needed between levels.  The
+// operands written before this launch (X, the per-head maxima) come through the launch boundary.
+//
+// Work queue per team: a ticket counter hands out the team's tile-jobs in level order (level l
+// has njobs(l) x 16 tiles x its heads); a workgroup waits, before its tile-job, until the done
+// counter covers every tile-job of the earlier levels.  A ticket is only ever held by a running
+// workgroup and waits only on lower tickets, so the queue cannot deadlock whatever subset of the
+// grid is resident (another stream's kernels may hold CUs); every workgroup leaves once a
+// ticket is past the last level, and the last one to leave zeroes the counters for the next call.
+// A wait is bounded (~1 s): on expiry the error word is set and the workgroup leaves.
+//
+// Measured and rejected (diagnostic build only, variant 8): correct (test_pinv_split_gpu), but a
+// level still takes ~6 us -- a tile is bound by its own operand fill (128 KB per term into one
+// CU's LDS at ~31 B/clk: ~2 us, plus ~1.2 us to the first chunk and ~0.7 us of epilogue), and the
+// counter hand-off between levels costs ~1.1 us, the same as a launch boundary in graph replay.
+// Whole step in graph replay: 734 vs 758 slides/s with one launch per level
+// (scripts/dev/team_stamps.py, scripts/dev/ab_split_variant.py).
+struct TeamArgs {
+  ChainArgs c;
+  int dir;             // 0: forward levels, 1: backward levels
+  long long plane;
+  const float* maxima;
+  unsigned* ctr;       // TEAM_SET_WORDS: per XCD [ticket, .., done @ +16], then the exit count and error word
+  unsigned long long* stamps;   // diagnostic build: per ticket 40 u64 (stage stamps, then claim / ready / done / xcc / level)
+};
+
+constexpr int TEAM_GRID = 256;   // one workgroup per CU (113 KB of LDS each)
+// diagnostic stamps: ticket t of XCD x at record x * 512 + t
+TM_DEV unsigned t_global_base(int x, unsigned t) { return (unsigned)x * 512u + t; }
+
+__global__ __launch_bounds__(NTHREADS) void pinv_team_kernel(TeamArgs T) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  volatile unsigned* bc = (volatile unsigned*)(smem + STAGE_LDS + EPI_LDS);
+  const int tid = threadIdx.x;
+  const int x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7;   // HW_REG_XCC_ID
+  const int nbh = T.c.nbh, iters = T.c.iters;
+  const int nh = nbh > x ? (nbh - 1 - x) / TEAM_XCD + 1 : 0;       // heads x, x + 8, ... of this team
+  unsigned* ticket = T.ctr + x * TEAM_STRIDE;
+  unsigned* done = ticket + TEAM_STRIDE / 2;
+  unsigned* exits = T.ctr + TEAM_XCD * TEAM_STRIDE;
+  unsigned* err = exits + 1;
+  const int nlev = T.dir == 0 ? fwd_levels(iters) : bwd_levels(iters);
+  const unsigned per_job = 16u * (unsigned)nh;
+  unsigned prefix = 0;   // tile-jobs of the levels before `lev`
+  int lev = 0;
+  while (nh > 0) {
+#ifdef TM_DIAG
+    const unsigned long long t_claim = T.stamps ? rstamp() : 0;
+#endif
+    if (tid == 0) bc[0] = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned t = __builtin_amdgcn_readfirstlane(bc[0]);
+    while (lev < nlev) {
+      const unsigned cnt = per_job * (T.dir == 0 ? fwd_level_njobs(iters, lev) : bwd_level_njobs(iters, lev));
+      if (t < prefix + cnt) break;
+      prefix += cnt;
+      ++lev;
+    }
+    if (lev >= nlev) break;
+    if (tid == 0) {   // every tile-job of the earlier levels done (relaxed L1-bypassing polls, bounded)
+      unsigned polls = 0;
+      while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < prefix) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++polls > (1u << 24)) { __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+      }
+    }
+    __syncthreads();   // also: every wave has read bc[0]
+    const unsigned r = t - prefix;
+    const int jn = (int)(r / per_job), rem = (int)(r % per_job);
+    const int head = x + TEAM_XCD * (rem >> 4), tile = rem & 15;
+    const SJob J = T.dir == 0 ? fwd_level_job(T.c, lev, jn) : bwd_level_job(T.c, lev, jn);
+    unsigned long long* so = nullptr;
+#ifdef TM_DIAG
+    const unsigned long long t_ready = T.stamps ? rstamp() : 0;
+    if (T.stamps) so = T.stamps + (size_t)t_global_base(x, t) * 40;
+#endif
+    stage_tile<true>(J, nbh, T.plane, T.maxima, head, tile, smem, so, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tile stores have reached the L2
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef TM_DIAG
+    if (so && tid == 0) {
+      so[32] = t_claim; so[33] = t_ready; so[34] = rstamp(); so[35] = x; so[36] = lev; so[37] = jn; so[38] = tile;
+    }
+#endif
+  }
+  if (tid == 0) {
+    const unsigned e = __hip_atomic_fetch_add(exits, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e == gridDim.x - 1) {   // the last workgroup out: nothing of this launch touches the counters any more
+      for (int i = 0; i < TEAM_XCD; ++i) {
+        __hip_atomic_store(T.ctr + i * TEAM_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(T.ctr + i * TEAM_STRIDE + TEAM_STRIDE / 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+#endif  // TM_DIAG
+
+// ---------------------------------------------------------------------------
+// host side
 struct Launcher {
   SLaunch L{};
   explicit Launcher(int nbh, long long plane, const float* maxima) {
@@ -597,37 +864,41 @@ struct Launcher {
   }
 };
 
-// saved-buffer layout (floats); every slot is nbh*MAT floats
-struct FwdLayout {
-  long long mat;
-  int iters;
-  float* base;
-  float* zf() const { return base; }                                      // Z_iters fp32
-  bf16* z(int k) const { return (bf16*)(base + (long long)k * mat); }     // Z_k split, k = 1..iters
-  bf16* p(int k) const { return (bf16*)(base + (long long)(iters + 1 + k) * mat); }       // P_k, k = 0..iters-1
-  bf16* t3(int k) const { return (bf16*)(base + (long long)(2 * iters + 1 + k) * mat); }
-  bf16* t5(int k) const { return (bf16*)(base + (long long)(3 * iters + 1 + k) * mat); }
-  bf16* scratch(int i) const { return (bf16*)(base + (long long)(4 * iters + 1 + i) * mat); }
-  float* sums() const { return base + (long long)(4 * iters + 3) * mat; }
-  float* maxima(int nbh) const { return sums() + 2LL * nbh * NL; }
-};
-
-FwdLayout fwd_layout(float* saved, int nbh, int iters) {
-  FwdLayout f;
-  f.mat = (long long)nbh * MAT;
-  f.iters = iters;
-  f.base = saved;
-  return f;
+// the levels [0, nlev) of one direction: one launch per level (or, diagnostic build variant 8,
+// the persistent kernel)
+int run_levels(const ChainArgs& c, int dir, long long plane, const float* maxima, unsigned* ctr, hipStream_t st) {
+#ifdef TM_DIAG
+  if (g_split_dbg == 8) {
+    TeamArgs T{c, dir, plane, maxima, ctr, g_split_stamps};
+    tm_allow_smem(pinv_team_kernel, STAGE_LDS + EPI_LDS + 64);
+    pinv_team_kernel<<<TEAM_GRID, NTHREADS, STAGE_LDS + EPI_LDS + 64, st>>>(T);
+    TM_CHECK_LAUNCH();
+    return 0;
+  }
+#else
+  (void)ctr;
+#endif
+  const int nlev = dir == 0 ? fwd_levels(c.iters) : bwd_levels(c.iters);
+  for (int lvl = 0; lvl < nlev; ++lvl) {
+    Launcher l(c.nbh, plane, maxima);
+    const int nj = dir == 0 ? fwd_level_njobs(c.iters, lvl) : bwd_level_njobs(c.iters, lvl);
+    for (int j = 0; j < nj; ++j) l.add(dir == 0 ? fwd_level_job(c, lvl, j) : bwd_level_job(c, lvl, j));
+    if (int rc = l.go(st)) return rc;
+  }
+  return 0;
 }
 
 }  // namespace
 
 extern "C" long long tm_pinv_split_saved_floats(int nbh, int iters) {
-  return (4LL * iters + 3) * nbh * MAT + 2LL * nbh * NL + 2LL * nbh + 64;
+  // ... + the maxima, then the persistent kernel's two counter sets on 64-B lines
+  return (4LL * iters + 3) * nbh * MAT + 2LL * nbh * NL + 2LL * nbh + 16 + TEAM_CTR_WORDS + 64;
 }
 
 // X: fp32 [nbh][256][256]; Xs: its split planes (tm_nys_sim2_softmax_split).  saved: see FwdLayout;
-// Z_iters (fp32) sits at the start of `saved`.
+// Z_iters (fp32) sits at the start of `saved`.  Two launches: L1 (S = X X^T and the |X| sums /
+// maxima, which couple all heads through c, and the zeroed team counters), then every other
+// level in the persistent kernel.
 extern "C" int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* saved, void* stream) {
   TM_REQUIRE(X && Xs && saved && nbh > 0 && iters >= 1, "pinv_fwd_split: bad args (iters >= 1)");
   TM_REQUIRE(((uintptr_t)Xs % 16) == 0 && ((uintptr_t)saved % 16) == 0, "pinv_fwd_split: 16-B aligned buffers");
@@ -642,53 +913,11 @@ extern "C" int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int it
     s.kind = KIND_ABSSUMS;
     l.add(s);
     l.L.X = X; l.L.sums = F.sums(); l.L.maxima_out = maxima;
+    l.L.zero_ctr = F.team_ctr(nbh, 0);   // both counter sets (forward, then backward)
     if (int rc = l.go(st)) return rc;
   }
-  for (int k = 0; k < iters; ++k) {
-    bf16* R = F.scratch((k + 1) & 1);
-    {  // A_k: R = P P (T3 = R - 7P + 15I); Z_k = 0.25 Z_{k-1} T5_{k-1}
-      Launcher l(nbh, plane, maxima);
-      SJob r;
-      if (k == 0) {  // P_0 = S / c: R = S S / c^2, T3 = R - 7 S/c + 15I, P_0 written as a side output
-        r = product(op(F.scratch(0), 0), op(F.scratch(0), 1), R, 1.f);
-        r.alpha_cpow = 2;
-        r.e1 = F.scratch(0); r.e1_cpow = 1;
-        r.c3 = F.p(0); r.c3_e1 = 1.f;
-      } else {
-        r = product(op(F.p(k), 0), op(F.p(k), 1), R, 1.f);
-        r.e1 = F.p(k);
-      }
-      r.c2 = F.t3(k); r.c2_alpha = 1.f; r.c2_diag = 15.f; r.c2_e1 = -7.f;
-      l.add(r);
-      if (k >= 1) {
-        SJob z = k == 1 ? product(op(Xs, 1), op(F.t5(0), 1), F.z(1), 0.25f)           // Z_0 = X^T / c
-                        : product(op(F.z(k - 1), 0), op(F.t5(k - 1), 1), F.z(k), 0.25f);
-        if (k == 1) z.alpha_cpow = 1;
-        l.add(z);
-      }
-      if (int rc = l.go(st)) return rc;
-    }
-    {  // B_k: T5 = 13I - P T3; P_{k+1} = 3.25 P - 0.25 R T3
-      Launcher l(nbh, plane, maxima);
-      l.add(product(op(F.p(k), 0), op(F.t3(k), 1), F.t5(k), -1.f, 13.f));
-      if (k + 1 < iters) {
-        SJob p = product(op(R, 0), op(F.t3(k), 1), F.p(k + 1), -0.25f);
-        p.e1 = F.p(k); p.e1s = 3.25f;
-        l.add(p);
-      }
-      if (int rc = l.go(st)) return rc;
-    }
-  }
-  {  // F: Z_iters = 0.25 Z_{iters-1} T5_{iters-1}  (split + fp32)
-    Launcher l(nbh, plane, maxima);
-    SJob z = iters == 1 ? product(op(Xs, 1), op(F.t5(0), 1), F.z(1), 0.25f)
-                        : product(op(F.z(iters - 1), 0), op(F.t5(iters - 1), 1), F.z(iters), 0.25f);
-    if (iters == 1) z.alpha_cpow = 1;
-    z.cf = F.zf();
-    l.add(z);
-    if (int rc = l.go(st)) return rc;
-  }
-  return 0;
+  const ChainArgs c{(const bf16*)Xs, saved, nullptr, nbh, iters};
+  return run_levels(c, 0, plane, maxima, F.team_ctr(nbh, 0), st);
 }
 
 // workspace: G, dT5, dZa, dP, dT3 (split) + dX (fp32) + partial dots
@@ -698,7 +927,8 @@ extern "C" long long tm_pinv_bwd_split_workspace_floats(int nbh) {
 
 // dZ: the gradient w.r.t. Z_iters as split planes, placed by the caller at the start of `work`
 // (tm_bmm with c_split).  out: dL/dX (softmax == 0) or dL/d(sim2 logits) = softmax backward of
-// A2 = X (softmax != 0), fp32.
+// A2 = X (softmax != 0), fp32.  `saved` is the forward's; its backward counter set is used (and
+// left zeroed) by the persistent kernel.
 extern "C" int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int iters, const float* saved, float* work,
                                  int softmax, float* out, void* stream) {
   TM_REQUIRE(X && Xs && saved && work && out && nbh > 0 && iters >= 1, "pinv_bwd_split: bad args");
@@ -707,52 +937,10 @@ extern "C" int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int it
   const long long mat = F.mat, plane = mat;
   const float* maxima = F.maxima(nbh);
   bf16* G = (bf16*)work;
-  bf16* dT5 = (bf16*)(work + mat);
-  bf16* dZa = (bf16*)(work + 2 * mat);
-  bf16* dP = (bf16*)(work + 3 * mat);
-  bf16* dT3 = (bf16*)(work + 4 * mat);
   float* dXc = work + 5 * mat;
   float* part = work + 6 * mat;
-  for (int k = iters - 1; k >= 0; --k) {
-    {  // dT5 = 0.25 Z_k^T G ; dZa = 0.25 G T5_k^T
-      Launcher l(nbh, plane, maxima);
-      SJob a = k == 0 ? product(op(Xs, 0), op(G, 1), dT5, 0.25f)          // Z_0^T = X / c
-                      : product(op(F.z(k), 1), op(G, 1), dT5, 0.25f);
-      if (k == 0) a.alpha_cpow = 1;
-      l.add(a);
-      l.add(product(op(G, 0), op(F.t5(k), 0), dZa, 0.25f));
-      if (int rc = l.go(st)) return rc;
-    }
-    {  // dP = -dT5 T3^T ; dT3 = -P^T dT5
-      Launcher l(nbh, plane, maxima);
-      l.add(product(op(dT5, 0), op(F.t3(k), 0), dP, -1.f));
-      l.add(product(op(F.p(k), 1), op(dT5, 1), dT3, -1.f));
-      if (int rc = l.go(st)) return rc;
-    }
-    {  // dP += dT3 P^T + P^T dT3 - 7 dT3   (T3 = P P - 7P + 15I)
-      Launcher l(nbh, plane, maxima);
-      SJob j = product(op(dT3, 0), op(F.p(k), 0), dP, 1.f);
-      j.nterms = 2;
-      j.a[1] = op(F.p(k), 1); j.b[1] = op(dT3, 1);
-      j.e1 = dP; j.e1s = 1.f;
-      j.e2 = dT3; j.e2s = -7.f;
-      l.add(j);
-      if (int rc = l.go(st)) return rc;
-    }
-    {  // dX (+)= dP Z_k^T ; G = dZa + X^T dP
-      Launcher l(nbh, plane, maxima);
-      SJob a = k == 0 ? product(op(dP, 0), op(Xs, 1), dXc, 1.f)            // Z_0^T = X / c
-                      : product(op(dP, 0), op(F.z(k), 0), dXc, 1.f);
-      if (k == 0) a.alpha_cpow = 1;
-      a.c_f32 = 1;
-      if (k != iters - 1) { a.e1 = dXc; a.e1_f32 = 1; a.e1s = 1.f; }
-      l.add(a);
-      SJob g = product(op(Xs, 1), op(dP, 1), G, 1.f);
-      g.e1 = dZa; g.e1s = 1.f;
-      l.add(g);
-      if (int rc = l.go(st)) return rc;
-    }
-  }
+  const ChainArgs c{(const bf16*)Xs, (float*)saved, work, nbh, iters};
+  if (int rc = run_levels(c, 1, plane, maxima, F.team_ctr(nbh, 1), st)) return rc;
   // Z_0 = X^T / c: the c gradient's partial sums, then the transpose term, the max-tie terms and the softmax
   pinv_c_dot_kernel<<<dim3(nbh, 16), 256, 0, st>>>(G, plane, X, part);
   TM_CHECK_LAUNCH();
