@@ -17,9 +17,16 @@ Prints ONE JSON line on rank 0.  Extra objects:
                    forward chain (tm_pinv_fwd_split: 14 launches of pinv_stage_kernel, the
                    largest share of the step in profiles/r02_*_kernel_summary.txt), its
                    algorithmic flops / the HIP-event span of the call on its stream
+  hbm_roofline  -- the HBM-bound NystromAttention / PPEG / LayerNorm kernels (north_star: >= 50 %
+                   of HBM roofline): per call site and layer, algorithmic bytes (every compulsory
+                   tensor read or written once) / the HIP-event span of the
+                   launch in eager probe steps after the timed region (a GPU spin queued ahead, the
+                   span of an empty event pair subtracted), against 8 TB/s
   cpu_baseline  -- the fp32 CPU oracle (oracle/transmil_ref.py, logits path) on a
                    bounded sample of the same workload, rank 0 only: median of 5 steps after
                    2 warm-ups at 8 threads (code/train.py:93) and at the box's CPU share
+  cpu_baseline_as_written -- the same oracle as the reference is written: every TransLayer also
+                   forms the [B, h, n', n'] return_attn product (code/models/TransMIL.py:47)
   optimizer_ms  -- the Lookahead(RAdam) step alone (inside the timed step too)
 """
 from __future__ import annotations
@@ -57,8 +64,9 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of "
                     "replaying the captured hipGraph of the whole step")
     ap.add_argument("--cpu-steps", type=int, default=5, help="timed CPU steps per thread count (median)")
-    ap.add_argument("--cpu-as-written", action="store_true",
-                    help="also time the CPU oracle as the reference is written (the n'xn' return_attn product)")
+    ap.add_argument("--no-cpu-as-written", action="store_true",
+                    help="skip the CPU oracle timed as the reference is written (the n'xn' return_attn product)")
+    ap.add_argument("--no-hbm-probe", action="store_true", help="skip the per-kernel HBM roofline list")
     return ap.parse_args()
 
 
@@ -94,6 +102,80 @@ def roofline_model(site, n_patches, dtype_bytes):
     raise ValueError(site)
 
 
+HBM_SITES = ("ln_fwd", "landmarks", "a3_fwd", "a1_fwd", "ppeg_fwd", "ppeg_bwd", "conv_bwd", "a3_bwd")
+
+
+def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
+    """Algorithmic HBM bytes of one launch of each HBM-bound call site (bf16 mode: T = 2 B),
+    by (site, layer): every compulsory tensor read or written once.  G = ceil(sqrt(N)),
+    S = G^2 + 1 tokens, n' = S rounded up to 256."""
+    import math
+    G = math.ceil(math.sqrt(n_patches))
+    S = G * G + 1
+    n = (S + 255) // 256 * 256
+    t, f4 = dtype_bytes, 4
+    lm = heads * m * dh                              # one [h, 256, 64] landmark-sized tensor
+    ln = S * d * f4 + n * d * t + 2 * S * f4         # H (fp32) in, xn (T, pad rows included) out, mean / rstd
+    landmarks = 2 * n * d * t + 2 * lm * (f4 + t)    # q, k in; q~, k~ out (fp32 + T copies)
+    a3f = 2 * n * d * t + lm * f4 + lm * f4 + heads * m * f4   # k, v, q~ in; W, lse3 out
+    a1f = 2 * n * d * t + 2 * lm * t + n * d * t + heads * n * f4   # q, v, k~, Y in; merged, lse1 out
+    ppf = 2 * S * d * f4                             # H1 in, H2 out (fp32 residual stream)
+    ppb = 3 * S * d * f4 + n * d * t                 # H1, dH in; dH1 out; layer 1's padded dropout gradient out
+    cvb = 3 * n * d * t + n * d * f4 + heads * n * f4   # dmerged, merged, v in; dv (fp32), D1 out
+    a3b_small = 2 * lm * t + 2 * heads * m * f4 + lm * f4 + lm * f4   # q~, dW in, lse3, D3, dk~ in, dq~3 out
+    a3b_l2 = 2 * n * d * t + 2 * n * d * t + a3b_small                # k, v in; dk, dv (into dqkv) out
+    a3b_l1 = a3b_l2 + n * d * f4                                      # + the conv path's fp32 dv in
+    return {
+        ("ln_fwd", 1): ("ln_fwd_kernel", ln), ("ln_fwd", 2): ("ln_fwd_kernel", ln),
+        ("landmarks", 1): ("landmarks_kernel", landmarks), ("landmarks", 2): ("landmarks_kernel", landmarks),
+        ("a3_fwd", 1): ("a3_fwd_kernel + a3_combine_kernel", a3f), ("a3_fwd", 2): ("a3_fwd_kernel + a3_combine_kernel", a3f),
+        ("a1_fwd", 1): ("a1_fwd_bf16_kernel", a1f),
+        ("ppeg_fwd", 0): ("ppeg_stencil_kernel<false>", ppf),
+        ("ppeg_bwd", 0): ("ppeg_stencil_kernel<true> + ppeg_wgrad_kernel + ppeg_wgrad_reduce_kernel", ppb),
+        ("conv_bwd", 1): ("conv_bwd_mfma_kernel", cvb),
+        ("a3_bwd", 2): ("attn_bwd_bf16_kernel<0, 9> (fused dk / dv epilogue)", a3b_l2),
+        ("a3_bwd", 1): ("attn_bwd_bf16_kernel<0, 9> (fused dk / dv epilogue)", a3b_l1),
+    }
+
+
+# layer of the k-th call of a site within one step (forward: layer 1 then 2; backward: 2 then 1)
+SITE_LAYERS = {"ln_fwd": (1, 2), "landmarks": (1, 2), "a3_fwd": (1, 2), "a1_fwd": (1,), "ppeg_fwd": (0,),
+               "ppeg_bwd": (0,), "conv_bwd": (1,), "a3_bwd": (2, 1)}
+
+
+def hbm_roofline(engine, run_step, steps, n_patches, dtype_bytes):
+    """Eager probe steps with every HBM site timed (spin ahead, empty event pair subtracted)."""
+    engine.probe.target = set(HBM_SITES)
+    engine.probe.spin_cycles = 2_000_000
+    engine.probe.events.clear()
+    engine.probe.names.clear()
+    for i in range(steps):
+        run_step(i)
+    torch.cuda.synchronize()
+    engine.probe.target = None
+    engine.probe.spin_cycles = 0
+    per = {}
+    for name, ev in zip(engine.probe.names, engine.probe.events):
+        s, e, zs, ze = ev
+        per.setdefault(name, []).append(s.elapsed_time(e) - zs.elapsed_time(ze))
+    model = hbm_model(n_patches, dtype_bytes)
+    out = []
+    for site in HBM_SITES:
+        xs = per.get(site, [])
+        layers = SITE_LAYERS[site]
+        if not xs or len(xs) % len(layers):
+            continue
+        for k, layer in enumerate(layers):
+            if (site, layer) not in model:
+                continue
+            ms = sorted(xs[k::len(layers)])[len(xs[k::len(layers)]) // 2]   # median over the probe steps
+            kname, byts = model[(site, layer)]
+            gbs = byts / (ms / 1e3) / 1e9
+            out.append(dict(site=site, layer=layer, kernel=kname, algorithmic_bytes=byts, us=round(ms * 1e3, 2),
+                            achieved_gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4)))
+    return out
+
+
 def measured_traffic(site, n_patches, dtype):
     """HBM bytes per launch of `site` from the committed rocprofv3 PMC passes
     (profiles/traffic.json, written by scripts/gpu_traffic.sh + scripts/traffic_summary.py):
@@ -120,7 +202,7 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(n_patches, ncls, steps, feat=512, as_written=False):
+def cpu_baseline(n_patches, ncls, steps, feat=512, as_written=False, threads=None):
     """fp32 CPU oracle on this host: fwd + CE + bwd + RAdam, train mode, median of `steps` steps
     after 2 warm-ups, at 8 threads (code/train.py:93) and at the box's CPU share (16; the
     machine's physical cores belong to other jobs).  Logits path (no unused n'xn' product)
@@ -128,7 +210,7 @@ def cpu_baseline(n_patches, ncls, steps, feat=512, as_written=False):
     import statistics
     from oracle.transmil_ref import TransMIL as RefTransMIL, TransLayer
     share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
-    counts = sorted({8, max(1, min(share, os.cpu_count() or 1))})
+    counts = sorted(threads) if threads else sorted({8, max(1, min(share, os.cpu_count() or 1))})
     TransLayer.compute_attn = as_written
     torch.manual_seed(0)
     model = RefTransMIL(ncls, feat, 512).train()
@@ -294,6 +376,13 @@ def main():
         kernel_ms_samples = [s.elapsed_time(e) for s, e in engine.probe.events]
     kernel_ms = sum(kernel_ms_samples) / max(len(kernel_ms_samples), 1)
 
+    hbm = None
+    if rank == 0 and not args.no_hbm_probe and args.features == 512:
+        def probe_step(i):
+            load(i)
+            body()
+        hbm = hbm_roofline(engine, probe_step, 3, args.n, 2 if args.dtype == "bf16" else 4)
+
     # the optimizer step alone (it is also inside every timed step): a graph of opt.step()
     # replayed 20 times between two events (after the timed region; it advances the state)
     opt_ms = None
@@ -359,12 +448,14 @@ def main():
                        "execution": "eager" if args.eager else "hipGraph replay of the whole step",
                        "global_batch": world, "seq_len": args.n, "parallelism": f"dp{world}"},
             "roofline": roof,
+            "hbm_roofline": hbm,
             "optimizer_ms": round(opt_ms, 5) if opt_ms is not None else None,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.n, args.classes, args.cpu_steps, args.features)
-            if args.cpu_as_written:
-                out["cpu_baseline_as_written"] = cpu_baseline(args.n, args.classes, 2, args.features, as_written=True)
+            if not args.no_cpu_as_written:
+                out["cpu_baseline_as_written"] = cpu_baseline(args.n, args.classes, 2, args.features, as_written=True,
+                                                              threads=(out["cpu_baseline"]["cores"],))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -143,7 +143,7 @@ def main():
     sout = torch.empty(nbh, 256, 256, device=dev)
     sdz = torch.empty(2 * nbh * 65536, dtype=torch.bfloat16, device=dev)
     _lib.call("tm_split_f32", E._p(pdz), E._p(sdz), nbh * 65536, st())
-    for v, nm in ((0, "per-level launches"), (8, "persistent team")):
+    for v, nm in ((0, "per-level launches"), (8, "persistent team"), (9, "team, plain DMA (probe)")):
         _lib.lib().tm_debug_set_split_variant(v)
         case(f"pinv_fwd split [{nm}]", lambda: _lib.call("tm_pinv_fwd_split", E._p(X), E._p(Xs), nbh, 6,
                                                            E._p(ssaved), st()), 24 * f)
@@ -188,9 +188,9 @@ def main():
     _lib.call("tm_split_f32", E._p(pdz), E._p(swork), nbh * 65536, st())
     case("pinv_bwd split (+softmax bwd)", lambda: _lib.call("tm_pinv_bwd_split", E._p(X), E._p(Xs), nbh, 6,
                                                             E._p(ssaved), E._p(swork), 1, E._p(sout), st()), 32 * f)
-    for gv in ((0, 1, 2) if args.gemm_ab else (0,)):
+    for gv in ((0, 1, 2, 4, 7) if args.gemm_ab else (0,)):
         _lib.lib().tm_debug_set_variant(2, gv)
-        tag[0] = ("", "[2 LDS buf] ", "[glds ring] ")[gv]
+        tag[0] = {0: "", 1: "[2 LDS buf] ", 2: "[4-stage ring] ", 4: "[persistent ring] ", 7: "[big tile] "}[gv]
         # ---------------- GEMMs ----------------
         pool = E.Pool(dev)
         xn = torch.randn(n, 512, device=dev).to(bf)

@@ -468,6 +468,32 @@ def _a3_bwd_ref(ql, dw, k, v):
     return lse, d, ds.transpose(1, 2) @ ql, a.transpose(1, 2) @ dw, ds @ k
 
 
+@pytest.mark.parametrize("nbh,n", [(8, 256), (8, 1280), (8, 8448), (16, 8448), (8, 33280), (24, 2048)])
+def test_a3_fwd_bf16(nbh, n):
+    """W = softmax(q~ k^T) v and lse3 (SURVEY App. A eq. 5-8, the A3 factor): the bf16 kernel (all
+    256 landmark queries per workgroup against an even share of the keys, online softmax across
+    chunks, fixed-order combine of the partials) against fp64 on the same bf16-rounded operands."""
+    L = _lib()
+    from transmil_deepgraft_amd._lib import BF16
+    from transmil_deepgraft_amd.engine import _p, _stream
+    g = torch.Generator(device="cpu").manual_seed(n + 7 * nbh)
+    ql = torch.randn(nbh, 256, 64, generator=g) * 0.4
+    k = (torch.randn(nbh, n, 64, generator=g) * 0.4).to(torch.bfloat16)
+    v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16)
+    s = ql.to(torch.bfloat16).double() @ k.double().transpose(1, 2)
+    ref_lse = torch.logsumexp(s, -1)
+    ref_w = torch.softmax(s, -1) @ v.double()
+    w = torch.full((nbh, 256, 64), float("nan"), device=DEV)
+    lse = torch.full((nbh, 256), float("nan"), device=DEV)
+    work = torch.empty(L.query("tm_nys_a3_workspace", nbh, n) // 4 + 16, device=DEV)
+    qd, kd, vd = ql.to(DEV).contiguous(), k.to(DEV).contiguous(), v.to(DEV).contiguous()
+    L.call("tm_nys_a3_fwd", BF16, _p(qd), _p(kd), _p(vd), nbh, n, _p(work), _p(w), _p(lse), _stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(w).all() and torch.isfinite(lse).all()
+    assert _rel(w.cpu(), ref_w) < 1e-2
+    assert (lse.cpu().double() - ref_lse).abs().max().item() < 1e-3
+
+
 @pytest.mark.parametrize("nbh,n", [(8, 256), (2, 1280), (8, 1280), (8, 8448), (16, 8448)])
 def test_a3_bwd_bf16_even_split(nbh, n):
     """The bf16 A3 backward (key units split evenly over the workgroups of a head: the 9-wave

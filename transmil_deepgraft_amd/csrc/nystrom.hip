@@ -767,6 +767,190 @@ __global__ __launch_bounds__(256, 2) void a3_fwd_kernel(const float* __restrict_
   }
 }
 
+// A3 path forward, bf16 (bench mode): one 512-thread workgroup per CU holds ALL 256 landmark
+// queries of its head (8 waves x 32) against an even share of the head's keys, so k and v are read
+// from HBM once (the 128-query form read them twice) and a head has P (<= 32) partials instead of
+// 2 x n/256 half-slabs.  grid (P, nbh); workgroup p takes the 32-key sub-blocks
+// [p S32 / P, (p + 1) S32 / P) (S32 = n / 32) in chunks of up to A3V_G sub-blocks, double-buffered
+// in LDS (k [key][72], v [key][80]): the next chunk's 16-B pieces are requested into registers before
+// the current chunk's scores, so its HBM round trip overlaps them; online softmax across chunks.
+//   part_o[p][bh][q][d] = sum_keys exp(s - m) v ; part_m, part_l[p][bh][q] = (m, l)
+constexpr int A3V_G = 5;                                           // sub-blocks (32 keys) per chunk
+constexpr int A3V_KEYS = A3V_G * 32;
+constexpr size_t A3V_KS = (size_t)A3V_KEYS * Lay<bf16>::KROW * 2;  // 23040 B
+constexpr size_t A3V_BUF = A3V_KS + (size_t)A3V_KEYS * Lay<bf16>::VROW * 2;   // + 25600 B
+constexpr size_t A3V_BYTES = 2 * A3V_BUF;                          // two chunk buffers: 97280 B
+constexpr int A3V_PIECES = (A3V_KEYS * 8 + 511) / 512;             // 16-B pieces per thread per operand
+
+// partials per head of the v2 kernel
+inline int a3v_splits(int nbh, int n) { return std::max(1, std::min(n / 32, 256 / std::max(nbh, 1))); }
+
+__global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict__ ql, const bf16* __restrict__ k,
+                                                        const bf16* __restrict__ v, int n, int P,
+                                                        float* __restrict__ part_o, float* __restrict__ part_m,
+                                                        float* __restrict__ part_l) {
+  constexpr int KROW = Lay<bf16>::KROW, VROW = Lay<bf16>::VROW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int p = blockIdx.x, bh = blockIdx.y, nbh = gridDim.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int S32 = n / 32;
+  const int sb0 = (int)((long long)p * S32 / P), sb1 = (int)((long long)(p + 1) * S32 / P);
+  const int qi = wave * 32 + r;
+  const bf16* kh = k + (size_t)bh * n * DH;
+  const bf16* vh = v + (size_t)bh * n * DH;
+  f32x4 kr[A3V_PIECES], vr[A3V_PIECES];
+  // the 16-B pieces of the chunk starting at sub-block c0 (rows clamped into the chunk)
+  auto fetch = [&](int c0) {
+    const int rows = min(A3V_G, sb1 - c0) * 32;
+#pragma unroll
+    for (int j = 0; j < A3V_PIECES; ++j) {
+      const int i = tid + 512 * j, row = min(i >> 3, rows - 1), c = (i & 7) * 8;
+      const size_t o = ((size_t)c0 * 32 + row) * DH + c;
+      kr[j] = *(const f32x4*)(kh + o);
+      vr[j] = *(const f32x4*)(vh + o);
+    }
+  };
+  auto stage = [&](int c0, int buf) {
+    const int rows = min(A3V_G, sb1 - c0) * 32;
+    bf16* ks = (bf16*)(smem + buf * A3V_BUF);
+    bf16* vs = (bf16*)(smem + buf * A3V_BUF + A3V_KS);
+#pragma unroll
+    for (int j = 0; j < A3V_PIECES; ++j) {
+      const int i = tid + 512 * j, row = i >> 3, c = (i & 7) * 8;
+      if (row < rows) {
+        *(f32x4*)(ks + row * KROW + c) = kr[j];
+        *(f32x4*)(vs + row * VROW + c) = vr[j];
+      }
+    }
+  };
+  fetch(sb0);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) qf[st] = cvt8<bf16>(ql + ((size_t)bh * NL + qi) * DH + st * 16 + 8 * h);
+  stage(sb0, 0);
+  __syncthreads();
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x16 o[2];
+  o[0] = (f32x16){};
+  o[1] = (f32x16){};
+  int buf = 0;
+  for (int c0 = sb0; c0 < sb1; c0 += A3V_G) {
+    const int ng = min(A3V_G, sb1 - c0);
+    const bool more = c0 + A3V_G < sb1;
+    if (more) fetch(c0 + A3V_G);   // in flight through this chunk's scores
+    const bf16* ks = (const bf16*)(smem + buf * A3V_BUF);
+    const bf16* vs = (const bf16*)(smem + buf * A3V_BUF + A3V_KS);
+    f32x16 s[A3V_G];   // S^T tiles (rows = keys, col = this lane's query)
+#pragma unroll
+    for (int kt = 0; kt < A3V_G; ++kt) {
+      s[kt] = (f32x16){};
+      if (kt < ng) {
+#pragma unroll
+        for (int st = 0; st < 4; ++st) mma16(s[kt], load8(ks + (kt * 32 + r) * KROW + st * 16 + 8 * h), qf[st]);
+      }
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < A3V_G; ++kt)
+      if (kt < ng) m = fmaxf(m, tree_max16(s[kt]));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float m_new = fmaxf(m_run, m);
+    const float corr = __builtin_amdgcn_exp2f((m_run - m_new) * LOG2E);   // 0 on the first chunk
+    const float ml = m_new * LOG2E;
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < A3V_G; ++kt) {
+      if (kt < ng) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s[kt][i] = __builtin_amdgcn_exp2f(fmaf(s[kt][i], LOG2E, -ml));
+        l += tree_sum16(s[kt]);
+      }
+    }
+    l += __shfl_xor(l, 32, 64);
+    l_run = l_run * corr + l;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      o[dt] *= corr;
+#pragma unroll
+      for (int kt = 0; kt < A3V_G; ++kt)
+        if (kt < ng) {
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp)
+            mma16(o[dt], value_frag<bf16>(vs, dt, kt * 32 + 16 * sp, lane), acc_as_operand<bf16>(s[kt], sp));
+        }
+    }
+    if (more) {
+      stage(c0 + A3V_G, buf ^ 1);   // the other buffer: last read two chunks ago, before the barrier below
+      __syncthreads();
+      buf ^= 1;
+    }
+  }
+  const size_t pidx = ((size_t)p * nbh + bh) * NL + qi;
+  if (h == 0) { part_m[pidx] = m_run; part_l[pidx] = l_run; }
+  float* po = part_o + pidx * DH;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      f32x4 val;
+      val[0] = o[dt][4 * g4]; val[1] = o[dt][4 * g4 + 1]; val[2] = o[dt][4 * g4 + 2]; val[3] = o[dt][4 * g4 + 3];
+      *(f32x4*)(po + dt * 32 + 8 * g4 + 4 * h) = val;
+    }
+}
+
+// combine of the v2 partials: grid (nbh, 32), block 256: item = (query blockIdx.y * 8 + (tid & 127) / 16,
+// 4 d); the two thread halves take the even / odd partials (every load issued first), merged through
+// LDS in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void a3_combine_v2_kernel(const float* __restrict__ part_o,
+                                                            const float* __restrict__ part_m,
+                                                            const float* __restrict__ part_l, int P, int nbh,
+                                                            float* __restrict__ w, float* __restrict__ lse3) {
+  constexpr int U = 16;   // partials per thread per burst
+  __shared__ f32x4 xo[128];
+  __shared__ float xm[128], xl[128];
+  const int bh = blockIdx.x, item = threadIdx.x & 127, half = threadIdx.x >> 7;
+  const int qi = blockIdx.y * 8 + (item >> 4), d4 = (item & 15) * 4;
+  const size_t q0 = (size_t)bh * NL + qi, pstride = (size_t)nbh * NL;
+  float M = -INFINITY, L = 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int p0 = half; p0 < P; p0 += 2 * U) {
+    float mv[U], lv[U];
+    f32x4 ov[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t pidx = (size_t)min(p0 + 2 * u, P - 1) * pstride + q0;
+      mv[u] = part_m[pidx];
+      lv[u] = part_l[pidx];
+      ov[u] = *(const f32x4*)(part_o + pidx * DH + d4);
+    }
+    float mb = M;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (p0 + 2 * u < P) mb = fmaxf(mb, mv[u]);
+    const float c = __expf(M - mb);    // M = -inf on the first burst: 0
+    L *= c;
+    acc *= c;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (p0 + 2 * u < P) {
+        const float sc = __expf(mv[u] - mb);
+        L += lv[u] * sc;
+        acc += ov[u] * sc;
+      }
+    M = mb;
+  }
+  if (half) { xo[item] = acc; xm[item] = M; xl[item] = L; }
+  __syncthreads();
+  if (half) return;
+  const float Mo = xm[item], Mt = fmaxf(M, Mo);
+  const float ca = M == -INFINITY ? 0.f : __expf(M - Mt), cb = Mo == -INFINITY ? 0.f : __expf(Mo - Mt);
+  const float Lt = L * ca + xl[item] * cb;
+  const f32x4 at = acc * ca + xo[item] * cb;
+  *(f32x4*)(w + q0 * DH + d4) = at / Lt;
+  if (d4 == 0) lse3[q0] = Mt + __logf(Lt);
+}
+
 // combine the key-block partials: W[bh][q][d], lse3[bh][q]; grid (nbh, 16), block 256: thread =
 // (query blockIdx.y * 16 + tid / 16, 4 consecutive d).  The partials of U key blocks are requested
 // in one burst (clamped indices, masked adds), key blocks summed in index order.
@@ -1786,18 +1970,30 @@ extern "C" int tm_softmax_bwd_rows256(const float* a, const float* da, float* ds
 }
 
 extern "C" long long tm_nys_a3_workspace(int nbh, int n) {
-  const long long nkb = n / NL;
-  return nkb * nbh * NL * (DH + 2) * (long long)sizeof(float);
+  const long long parts = std::max((long long)(n / NL), (long long)a3v_splits(nbh, n));
+  return parts * nbh * NL * (DH + 2) * (long long)sizeof(float);
 }
 
 extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
                              float* w, float* lse3, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0, "a3_fwd: n must be a positive multiple of 256");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TM_BF16) {
+    const int P = a3v_splits(nbh, n);
+    float* po = work;
+    float* pm = po + (size_t)P * nbh * NL * DH;
+    float* pl = pm + (size_t)P * nbh * NL;
+    tm_allow_smem(a3_fwd_v2_kernel, A3V_BYTES);
+    a3_fwd_v2_kernel<<<dim3(P, nbh), 512, A3V_BYTES, st>>>(ql, (const bf16*)k, (const bf16*)v, n, P, po, pm, pl);
+    TM_CHECK_LAUNCH();
+    a3_combine_v2_kernel<<<dim3(nbh, NL / 8), 256, 0, st>>>(po, pm, pl, P, nbh, w, lse3);
+    TM_CHECK_LAUNCH();
+    return 0;
+  }
   const int nkb = n / NL;
   float* po = work;
   float* pm = po + (size_t)nkb * nbh * NL * DH;
   float* pl = pm + (size_t)nkb * nbh * NL;
-  hipStream_t st = (hipStream_t)stream;
   TM_DTYPE_DISPATCH(dtype, ({
     const size_t sm = ((size_t)NL * Lay<T>::KROW + Lay<T>::VELEMS) * sizeof(T);
     tm_allow_smem(a3_fwd_kernel<T>, sm);

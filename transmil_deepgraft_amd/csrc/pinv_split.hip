@@ -277,10 +277,10 @@ TM_DEV void abssums(const SLaunch& L, int head, int which, float* red) {
 // TEAM: the tile runs inside the persistent chain kernel (pinv_team_kernel): every operand it
 // reads was written by another workgroup of the same XCD in this launch, so the LDS-DMA reads
 // bypass the CU's L1 (sc1, served by the XCD's L2) and so do the epilogue operand loads (nt).
-template <bool TEAM>
+template <bool TEAM, int TEAM_POL = 16>
 TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* maxima, int head, int tile,
                        char* smem, unsigned long long* stamp_out, int dbg_) {
-  constexpr int DMA_POL = TEAM ? 16 : 0;   // cache policy of the LDS-DMA: sc1 in the team kernel
+  constexpr int DMA_POL = TEAM ? TEAM_POL : 0;   // cache policy of the LDS-DMA: sc1 in the team kernel
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int m0 = (tile >> 2) * 64, n0 = (tile & 3) * 64;
@@ -771,6 +771,7 @@ constexpr int TEAM_GRID = 256;   // one workgroup per CU (113 KB of LDS each)
 // diagnostic stamps: ticket t of XCD x at record x * 512 + t
 TM_DEV unsigned t_global_base(int x, unsigned t) { return (unsigned)x * 512u + t; }
 
+template <int POL>
 __global__ __launch_bounds__(NTHREADS) void pinv_team_kernel(TeamArgs T) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   volatile unsigned* bc = (volatile unsigned*)(smem + STAGE_LDS + EPI_LDS);
@@ -817,7 +818,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_team_kernel(TeamArgs T) {
     const unsigned long long t_ready = T.stamps ? rstamp() : 0;
     if (T.stamps) so = T.stamps + (size_t)t_global_base(x, t) * 40;
 #endif
-    stage_tile<true>(J, nbh, T.plane, T.maxima, head, tile, smem, so, 0);
+    stage_tile<true, POL>(J, nbh, T.plane, T.maxima, head, tile, smem, so, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tile stores have reached the L2
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -868,10 +869,11 @@ struct Launcher {
 // the persistent kernel)
 int run_levels(const ChainArgs& c, int dir, long long plane, const float* maxima, unsigned* ctr, hipStream_t st) {
 #ifdef TM_DIAG
-  if (g_split_dbg == 8) {
+  if (g_split_dbg == 8 || g_split_dbg == 9) {   // 9: plain-policy DMA (timing probe only: L1 may be stale)
     TeamArgs T{c, dir, plane, maxima, ctr, g_split_stamps};
-    tm_allow_smem(pinv_team_kernel, STAGE_LDS + EPI_LDS + 64);
-    pinv_team_kernel<<<TEAM_GRID, NTHREADS, STAGE_LDS + EPI_LDS + 64, st>>>(T);
+    auto kern = g_split_dbg == 8 ? pinv_team_kernel<16> : pinv_team_kernel<0>;
+    tm_allow_smem(kern, STAGE_LDS + EPI_LDS + 64);
+    kern<<<TEAM_GRID, NTHREADS, STAGE_LDS + EPI_LDS + 64, st>>>(T);
     TM_CHECK_LAUNCH();
     return 0;
   }

@@ -33,14 +33,16 @@ LN_EPS = 1e-5
 
 
 class _Probe:
-    """Optional HIP-event timing of ONE named call site (bench.py's roofline leg).
+    """Optional HIP-event timing of named call sites (bench.py's roofline legs).
 
-    Events are recorded on the current stream -- the stream the kernel is
-    launched on -- so their difference is that launch's duration."""
+    ``target``: one site name, or a set of names.  Events are recorded on the current stream --
+    the stream the kernel is launched on -- so their difference is that launch's duration;
+    ``names[i]`` is the site of ``events[i]``."""
 
     def __init__(self):
         self.target = None
         self.events = []
+        self.names = []
         # > 0: a GPU spin of this many cycles is queued ahead of the start event, so the host
         # has already submitted the kernel when the event fires and the pair times the kernel,
         # not the host's launch latency (used only outside any timed region or graph capture)
@@ -51,13 +53,18 @@ class _Probe:
     def __call__(self, name):
         return _ProbeCtx(self, name)
 
+    def on(self, name):
+        t = self.target
+        return t is not None and (name == t if isinstance(t, str) else name in t)
+
 
 class _ProbeCtx:
     def __init__(self, probe, name):
         self.p, self.name = probe, name
 
     def __enter__(self):
-        if self.p.target == self.name:
+        self.active = self.p.on(self.name)
+        if self.active:
             self.z = None
             if self.p.spin_cycles > 0:
                 torch.cuda._sleep(self.p.spin_cycles)
@@ -71,9 +78,10 @@ class _ProbeCtx:
         return self
 
     def __exit__(self, *exc):
-        if self.p.target == self.name:
+        if self.active:
             self.e.record()
             self.p.events.append((self.s, self.e) if self.z is None else (self.s, self.e, *self.z))
+            self.p.names.append(self.name)
         return False
 
 
@@ -248,7 +256,8 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool, cls_r
     kl = pool(nbh * NL * DH).view(nbh, NL, DH)
     ql_t = pool(nbh * NL * DH, tdtype).view(nbh, NL, DH)
     kl_t = pool(nbh * NL * DH, tdtype).view(nbh, NL, DH)
-    _lib.call("tm_nys_landmarks", dt_code, _p(q), _p(k), nbh, n, _p(ql), _p(kl), _p(ql_t), _p(kl_t), st)
+    with probe("landmarks"):
+        _lib.call("tm_nys_landmarks", dt_code, _p(q), _p(k), nbh, n, _p(ql), _p(kl), _p(ql_t), _p(kl_t), st)
     a2 = pool(nbh * NL * NL).view(nbh, NL, NL)
     w = pool(nbh * NL * DH).view(nbh, NL, DH)
     lse3 = pool(nbh * NL)
@@ -400,8 +409,9 @@ def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, see
     xn = pool(B * n * D, tdtype).view(B, n, D)
     mean = pool(B * S)
     rstd = pool(B * S)
-    _lib.call("tm_layernorm_fwd", _p(H), _p(prm["norm_w"]), _p(prm["norm_b"]), C.c_float(LN_EPS), B * S, D,
-              S, n, pad, dt_code, _p(xn), _p(mean), _p(rstd), st)
+    with probe("ln_fwd"):
+        _lib.call("tm_layernorm_fwd", _p(H), _p(prm["norm_w"]), _p(prm["norm_b"]), C.c_float(LN_EPS), B * S, D,
+                  S, n, pad, dt_code, _p(xn), _p(mean), _p(rstd), st)
     qkv = pool(3 * geo.nbh * n * DH, tdtype).view(3, geo.nbh, n, DH)
     with probe("qkv_gemm"):
         gemm(xn, prm["wqkv"], qkv, B * n, 3 * D, D, lda=D, ldb=D, ldc=0, dtype=dt_code,
@@ -635,7 +645,8 @@ class TransMILEngine:
                  bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
         H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0], seed_dev)
         H2 = pool(B * geo.S * D).view(B * geo.S, D)
-        _lib.call("tm_ppeg_fwd", _p(H1), B, geo.G, D, _p(prm["wfold"]), _p(prm["bfold"]), _p(H2), st)
+        with probe("ppeg_fwd"):
+            _lib.call("tm_ppeg_fwd", _p(H1), B, geo.G, D, _p(prm["wfold"]), _p(prm["bfold"]), _p(H2), st)
         # layer 2: the head reads its output only at the class rows (code/models/TransMIL.py:201-203)
         H3, s2 = translayer_forward(H2, geo, prm[2], self.tdtype, self.dt_code, pool, drop_p, seeds[1], seed_dev,
                                     cls_only=self.cls_only)
@@ -684,11 +695,13 @@ class TransMILEngine:
                 # the stencil also writes layer 1's padded to_out-dropout gradient (its first step)
                 s1 = ctx["s1"]
                 dout1 = pool(B * geo.n * D, self.tdtype).view(B, geo.n, D)
-                _lib.call("tm_ppeg_bwd", _p(ctx["H1"]), _p(dH), B, geo.G, D, _p(prm["wfold"]), _p(dH1), _p(work),
-                          _p(dwsum), _p(g["pos_layer.proj.weight"]), _p(g["pos_layer.proj.bias"]),
-                          _p(g["pos_layer.proj1.weight"]), _p(g["pos_layer.proj1.bias"]),
-                          _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), self.dt_code, _p(dout1),
-                          geo.n, geo.pad, C.c_float(s1["drop_p"]), C.c_uint64(s1["seed"]), _p(s1["seed_dev"]), st)
+                with probe("ppeg_bwd"):
+                    _lib.call("tm_ppeg_bwd", _p(ctx["H1"]), _p(dH), B, geo.G, D, _p(prm["wfold"]), _p(dH1),
+                              _p(work), _p(dwsum), _p(g["pos_layer.proj.weight"]), _p(g["pos_layer.proj.bias"]),
+                              _p(g["pos_layer.proj1.weight"]), _p(g["pos_layer.proj1.bias"]),
+                              _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), self.dt_code,
+                              _p(dout1), geo.n, geo.pad, C.c_float(s1["drop_p"]), C.c_uint64(s1["seed"]),
+                              _p(s1["seed_dev"]), st)
                 dH = dH1
                 flush_reductions()     # head, norm, layer2 and PPEG parameter gradients final
                 if ready is not None:
