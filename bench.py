@@ -128,7 +128,9 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
     return {
         ("ln_fwd", 1): ("ln_fwd_kernel", ln), ("ln_fwd", 2): ("ln_fwd_kernel", ln),
         ("landmarks", 1): ("landmarks_kernel", landmarks), ("landmarks", 2): ("landmarks_kernel", landmarks),
-        ("a3_fwd", 1): ("a3_fwd_kernel + a3_combine_kernel", a3f), ("a3_fwd", 2): ("a3_fwd_kernel + a3_combine_kernel", a3f),
+        # the key-split kernel; its partials' combine runs inside the pseudo-inverse chain's last launch
+        ("a3_fwd", 1): ("a3_fwd_v2_kernel (combine inside pinv F launch)", a3f),
+        ("a3_fwd", 2): ("a3_fwd_v2_kernel (combine inside pinv F launch)", a3f),
         ("a1_fwd", 1): ("a1_fwd_bf16_kernel", a1f),
         ("ppeg_fwd", 0): ("ppeg_stencil_kernel<false>", ppf),
         ("ppeg_bwd", 0): ("ppeg_stencil_kernel<true> + ppeg_wgrad_kernel + ppeg_wgrad_reduce_kernel", ppb),

@@ -99,6 +99,18 @@ int tm_head_fwd(const float* h, int B, int S, int D, const float* gamma, const f
 int tm_head_bwd(const float* dlogits, int B, int C, int S, int D, const float* xhat, const float* rstd,
                 const float* gamma, const float* beta, const float* W, float* dW, float* dbias,
                 float* dgamma, float* dbeta, float* dh, void* stream);
+/* The training step's head and loss in one launch each way (replaces tm_head_fwd + tm_ce_fwd and
+ * tm_ce_bwd + tm_head_bwd on the fused TransMILTask path): forward = tm_head_fwd, then
+ * CrossEntropyLoss(logits, one_hot(label).float()) / Y_prob / Y_hat / class stats as tm_ce_fwd
+ * (code/models/model_interface.py:339-356); backward: dlogits = gloss (prob - one_hot) / B
+ * (+ dlogits_in, nullable), then tm_head_bwd.  scratch: B*C floats (may be null if B == 1, C <= 4). */
+int tm_head_ce_fwd(const float* h, int B, int S, int D, const float* gamma, const float* beta, float eps,
+                   const float* W, const float* bias, int C, const long long* label, float* logits, float* xhat,
+                   float* rstd, float* loss, float* prob, long long* yhat, int* class_stats, void* stream);
+int tm_head_ce_bwd(const float* prob, const long long* label, const float* gloss, const float* dlogits_in, int B,
+                   int C, int S, int D, const float* xhat, const float* rstd, const float* gamma,
+                   const float* beta, const float* W, float* dW, float* dbias, float* dgamma, float* dbeta,
+                   float* dh, float* scratch, void* stream);
 
 /* ---- NystromAttention core (nystrom.hip) --------------------------------
  * SURVEY.md App. A eq. 4-9 of the third-party nystrom_attention package
@@ -110,6 +122,9 @@ int tm_nys_sim2_softmax(const float* ql, const float* kl, int nbh, float* a2, vo
 int tm_softmax_bwd_rows256(const float* a, const float* da, float* ds, int rows, void* stream);
 long long tm_nys_a3_workspace(int nbh, int n);
 /* W = softmax(ql k^T) v  [B*h,256,64] fp32, lse3 [B*h,256] */
+/* bf16: w = lse3 = NULL leaves the tm_nys_a3_partials(nbh, n) key-split partials in work for
+ * tm_pinv_fwd_split_a3 to combine */
+long long tm_nys_a3_partials(int nbh, int n);
 int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
                   float* w, float* lse3, void* stream);
 /* merged[b][t][head*64+d] = softmax(q kl^T) y + conv33(v); lse1 [B*h, n]; kl_t, y_t: T copies */
@@ -125,6 +140,8 @@ int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_
                   const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
                   float* dq, float* work, float* dkl, float* dy, int accumulate, void* stream);
 long long tm_nys_a3_bwd_workspace(int nbh, int n);
+/* d3 (here and in tm_nys_a3_bwd_fused): D = rowsum(dW o W) as [2][B*h][256] partials, the two
+ * 32-column halves of dW (tm_bmm_job.Rd of the dW = Z^T dY product); the kernels sum them */
 int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
                   const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
                   float* work, float* dql, int accumulate, void* stream);
@@ -164,6 +181,10 @@ typedef struct tm_bmm_job {
    * 2 = split planes hi = bf16(C) at Ct and lo = bf16(C - hi) at Ct + ct_plane elements
    * (the operand format of tm_pinv_bwd_split), 0 = none */
   void* Ct; long long ct_plane; int ct_mode; int ct_reserved;
+  /* optional partial row dots of C with Rw (C's layout), one per 32-column tile:
+   * Rd[(n / 32) * nbatch + b][m] = sum over that tile's columns of C[b][m][n] * Rw[b][m][n]
+   * (null: none).  D = rowsum(dW o W) of the A3 backward as N / 32 = 2 partials. */
+  float* Rd; const float* Rw;
 } tm_bmm_job;
 /* prec 0: exact fp32 MFMA; prec 1: bf16x3 (hi/lo split, ~16-bit operands, fp32 accumulate) */
 int tm_bmm(const tm_bmm_job* jobs, int njobs, int nbatch, int prec, void* stream);
@@ -183,6 +204,11 @@ int tm_nys_sim2_softmax_split(const float* ql, const float* kl, int nbh, float* 
 /* saved: Z_iters fp32 at saved[0 .. nbh*65536), then the split chain matrices, sums and maxima */
 long long tm_pinv_split_saved_floats(int nbh, int iters);
 int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* saved, void* stream);
+/* tm_pinv_fwd_split with the A3 forward's partial combine in the chain's last launch (its idle CUs):
+ * a3_work / a3_parts = the partials tm_nys_a3_fwd(TM_BF16, ..., w = NULL, lse3 = NULL) left,
+ * a3_parts = tm_nys_a3_partials(nbh, n); writes W [B*h,256,64] and lse3 [B*h,256] as tm_nys_a3_fwd. */
+int tm_pinv_fwd_split_a3(const float* X, const void* Xs, int nbh, int iters, float* saved, const float* a3_work,
+                         int a3_parts, float* w, float* lse3, void* stream);
 /* work: the gradient w.r.t. Z_iters as split planes at work[0 .. nbh*65536) on entry (tm_split_f32);
  * out = dL/dX (softmax == 0) or the backward of A2 = softmax(.) through X (softmax != 0), fp32 */
 long long tm_pinv_bwd_split_workspace_floats(int nbh);

@@ -309,7 +309,7 @@ def main():
                                                   E._p(y_t), E._p(lse1), E._p(d1), nbh, 8, n, 256, E._p(dqf),
                                                   E._p(a1w), E._p(dkl), E._p(dy), 0, st()), 10 * nbh * n * 256 * 64)
     a3bw = torch.empty(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4, device=dev)
-    d3 = torch.randn(nbh, 256, device=dev)
+    d3 = torch.randn(2, nbh, 256, device=dev)   # [2][nbh][256] partials
     dw_t = torch.randn(nbh, 256, 64, device=dev).to(bf)
     dk = torch.empty(nbh, n, 64, device=dev)
     dql = torch.zeros(nbh, 256, 64, device=dev)

@@ -304,3 +304,42 @@ def test_fused_cross_entropy_matches_torch(B, C):
         want[y, 0] += 1
         want[y, 1] += int(y == h)
     assert torch.equal(stats.cpu(), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,train", [(1, 2, True), (1, 3, False), (2, 3, True), (3, 5, False)])
+def test_head_fused_cross_entropy_matches_separate_launches(B, C, train):
+    """TransMILTask.training_step through TransMIL.forward_ce (head + CE in one launch each way,
+    tm_head_ce_fwd / tm_head_ce_bwd) against the same model through forward + tm_ce_fwd / tm_ce_bwd
+    + tm_head_bwd: loss, Y_prob, Y_hat, class stats and every parameter gradient (fp32 mode; train
+    mode replays the same dropout counter)."""
+    from transmil_deepgraft_amd.models import TransMIL
+    from transmil_deepgraft_amd.interface import TransMILTask
+    torch.manual_seed(0)
+    model = TransMIL(C, 512, 512).cuda().set_compute_dtype(torch.float32)
+    model.train(train)
+    g = torch.Generator().manual_seed(B + 10 * C)
+    x = torch.rand(B, 300, 512, generator=g).cuda()
+    label = torch.randint(0, C, (B,), generator=g).cuda()
+    outs = []
+    for fused in (True, False):
+        task = TransMILTask(model)
+        if not fused:
+            model.forward_ce = lambda *a, **k: None     # the task falls back to forward + tm_ce_*
+        counter = model._dropout_counter.clone()
+        model.zero_grad(set_to_none=True)
+        loss = task.training_step((x, label, None))
+        task.backward(loss)
+        if fused:
+            model._dropout_counter.copy_(counter)
+        else:
+            del model.forward_ce
+        y_prob, y_hat = task._last_outputs
+        grads = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+        outs.append((loss.detach().clone(), y_prob.clone(), y_hat.clone(), task.class_stats.clone(), grads))
+    (l1, p1, h1, s1, g1), (l2, p2, h2, s2, g2) = outs
+    torch.testing.assert_close(l1, l2, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(p1, p2, rtol=1e-6, atol=1e-7)
+    assert torch.equal(h1, h2) and torch.equal(s1, s2)
+    for n in g2:
+        torch.testing.assert_close(g1[n], g2[n], rtol=1e-5, atol=1e-7, msg=n)

@@ -512,7 +512,11 @@ def test_a3_bwd_bf16_even_split(nbh, n):
     dql = torch.full((nbh, 256, 64), float("nan"), device=DEV)
     work = torch.empty(L.query("tm_nys_a3_bwd_workspace", nbh, n) // 4 + 16, device=DEV)
     qd, wd, kd, vd = (t.to(DEV).contiguous() for t in (ql, dw, k, v))
-    lsed, dd = lse.float().to(DEV).contiguous(), d.float().to(DEV).contiguous()
+    # D as the [2][nbh][256] partials over the two 32-column halves (tm_bmm_job.Rd of dW = Z^T dY)
+    wv = torch.softmax(ql.double() @ k.double().transpose(1, 2), -1) @ v.double()
+    dparts = torch.stack([(dw.double() * wv)[..., :32].sum(-1), (dw.double() * wv)[..., 32:].sum(-1)])
+    assert torch.allclose(dparts.sum(0), d)
+    lsed, dd = lse.float().to(DEV).contiguous(), dparts.float().to(DEV).contiguous()
     L.call("tm_nys_a3_bwd", BF16, _p(qd), _p(wd), _p(kd), _p(vd), _p(lsed), _p(dd), nbh, 8, n,
            _p(dk), _p(dv), _p(work), _p(dql), 0, _stream())
     torch.cuda.synchronize()
@@ -544,3 +548,28 @@ def test_landmarks_segment_means(dtype, nbh, n):
     assert (ql.cpu().double() - ref_q).abs().max().item() < 1e-5
     assert (kl.cpu().double() - ref_k).abs().max().item() < 1e-5
     assert torch.equal(qt.cpu(), ql.cpu().to(dtype)) and torch.equal(kt.cpu(), kl.cpu().to(dtype))
+
+
+def test_bmm_rowdot_partials():
+    """tm_bmm_job.Rd: per 32-column tile the partial row dots of C with Rw (D = rowsum(dW o W) of
+    the A3 backward as 2 partials), beside C itself, in both precisions."""
+    from transmil_deepgraft_amd import engine as E
+    g = torch.Generator(device="cpu").manual_seed(5)
+    nbh = 8
+    z = torch.randn(nbh, 256, 256, generator=g).to(DEV) * 0.1
+    dy = torch.randn(nbh, 256, 64, generator=g).to(DEV)
+    w = torch.randn(nbh, 256, 64, generator=g).to(DEV)
+    ref = z.double().transpose(1, 2) @ dy.double()
+    for prec in (0, 1):
+        dw = torch.empty(nbh, 256, 64, device=DEV)
+        rd = torch.full((2, nbh, 256), float("nan"), device=DEV)
+        dw_t = torch.empty(nbh, 256, 64, dtype=torch.bfloat16, device=DEV)
+        j = E.bmm_job(z, 1, dy, 0, dw, 256, 64, 256, Ct=dw_t, ct_mode=1)
+        j.Rd, j.Rw = rd.data_ptr(), w.data_ptr()
+        E.bmm([j], nbh, prec)
+        torch.cuda.synchronize()
+        assert _rel(dw.cpu(), ref.cpu()) < (1e-6 if prec == 0 else 1e-5)
+        assert torch.equal(dw_t, dw.to(torch.bfloat16))
+        prod = dw.double() * w.double()
+        exp = torch.stack([prod[..., :32].sum(-1), prod[..., 32:].sum(-1)])
+        assert torch.allclose(rd.double(), exp, rtol=1e-5, atol=1e-5)

@@ -39,7 +39,7 @@ class BmmJob(C.Structure):
                 ("E1", P), ("e1", Fl), ("E2", P), ("e2", Fl), ("alpha", Fl), ("diag", Fl),
                 ("C", P), ("ldc", I), ("sc", L), ("M", I), ("N", I), ("K", I),
                 ("C2", P), ("c2_alpha", Fl), ("c2_diag", Fl), ("c2_e1", Fl),
-                ("Ct", P), ("ct_plane", L), ("ct_mode", I), ("ct_reserved", I)]
+                ("Ct", P), ("ct_plane", L), ("ct_mode", I), ("ct_reserved", I), ("Rd", P), ("Rw", P)]
 
 
 OPTIM_MAX_TENSORS = 40
@@ -75,10 +75,13 @@ _SIGS = {
     "tm_layernorm_bwd": (I, [P, I, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P]),
     "tm_head_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P]),
     "tm_head_bwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
+    "tm_head_ce_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P, P, P, P, P, P]),
+    "tm_head_ce_bwd": (I, [P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P]),
     "tm_nys_landmarks": (I, [I, P, P, I, I, P, P, P, P, P]),
     "tm_nys_sim2_softmax": (I, [P, P, I, P, P]),
     "tm_softmax_bwd_rows256": (I, [P, P, P, I, P]),
     "tm_nys_a3_workspace": (L, [I, I]),
+    "tm_nys_a3_partials": (L, [I, I]),
     "tm_nys_a3_fwd": (I, [I, P, P, P, I, I, P, P, P, P]),
     "tm_nys_a1_fwd": (I, [I, P, P, P, P, P, I, I, I, P, P, P]),
     "tm_nys_rowdot_cast": (I, [I, P, P, I, P, P, P]),
@@ -101,6 +104,7 @@ _SIGS = {
     "tm_nys_sim2_softmax_split": (I, [P, P, I, P, P, P]),
     "tm_pinv_split_saved_floats": (L, [I, I]),
     "tm_pinv_fwd_split": (I, [P, P, I, I, P, P]),
+    "tm_pinv_fwd_split_a3": (I, [P, P, I, I, P, P, I, P, P, P]),
     "tm_pinv_bwd_split_workspace_floats": (L, [I]),
     "tm_pinv_bwd_split": (I, [P, P, I, I, P, P, I, P, P]),
     "tm_split_f32": (I, [P, P, L, P]),

@@ -284,6 +284,180 @@ __global__ void head_bwd_kernel(const float* __restrict__ dlogits, int B, int C,
   for (int i = 0; i < VPL; ++i) { dgamma[lane * VPL + i] = dgm[i]; dbeta[lane * VPL + i] = dbt[i]; }
 }
 
+// Head + loss of the training step in ONE launch (the step's tail was four latency-bound launches:
+// head, CE, CE backward, head backward -- two of them now):
+// forward: the head above for every bag (wave w takes bags w, w + NW, ...), then
+// CrossEntropyLoss(logits, one_hot(label).float()) averaged over the bags with Y_prob, Y_hat and
+// the per-class count / correct (as ce_fwd_kernel, glue.hip), from the logits through LDS.
+constexpr int HEAD_CE_WAVES = 4;
+template <int VPL>
+__global__ __launch_bounds__(64 * HEAD_CE_WAVES) void head_ce_fwd_kernel(
+    const float* __restrict__ h, int B, int S, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float eps, const float* __restrict__ W, const float* __restrict__ bias, int C, const long long* __restrict__ label,
+    float* __restrict__ logits, float* __restrict__ xhat, float* __restrict__ rstd_out, float* __restrict__ loss,
+    float* __restrict__ prob, long long* __restrict__ yhat, int* __restrict__ stats) {
+  constexpr int D = VPL * 64;
+  __shared__ float red[HEAD_CE_WAVES];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int b = wave; b < B; b += HEAD_CE_WAVES) {
+    float v[VPL];
+    load_row<VPL>(v, h + (size_t)b * S * D, lane);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) s += v[i];
+    const float mu = wave_sum(s) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) { const float d = v[i] - mu; q += d * d; }
+    const float rs = 1.0f / sqrtf(wave_sum(q) * (1.0f / D) + eps);
+    float y[VPL];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane * VPL + i;
+      const float xh = (v[i] - mu) * rs;
+      xhat[(size_t)b * D + c] = xh;
+      y[i] = xh * gamma[c] + beta[c];
+    }
+    if (lane == 0) rstd_out[b] = rs;
+    for (int k = 0; k < C; ++k) {
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) acc += y[i] * W[(size_t)k * D + lane * VPL + i];
+      acc = wave_sum(acc);
+      if (lane == 0) logits[b * C + k] = acc + bias[k];
+    }
+  }
+  __syncthreads();   // the block's logits stores are visible to the block (same workgroup)
+  float acc = 0.f;
+  for (int b = threadIdx.x; b < B; b += 64 * HEAD_CE_WAVES) {
+    const float* l = logits + (size_t)b * C;
+    float m = l[0];
+    int am = 0;
+    for (int c = 1; c < C; ++c)
+      if (l[c] > m) { m = l[c]; am = c; }
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += expf(l[c] - m);
+    const float inv = 1.f / s, lse = m + logf(s);
+    for (int c = 0; c < C; ++c) prob[(size_t)b * C + c] = expf(l[c] - m) * inv;
+    acc += lse - l[label[b]];
+    yhat[b] = am;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) red[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < HEAD_CE_WAVES; ++w) t += red[w];
+    loss[0] = t / (float)B;
+    if (stats)
+      for (int b = 0; b < B; ++b) {
+        const int yv = (int)label[b];
+        stats[2 * yv] += 1;
+        stats[2 * yv + 1] += yhat[b] == yv;
+      }
+  }
+}
+
+// backward of the above: dlogits = g (prob - one_hot(label)) / B (+ dlogits_in, the gradient
+// reaching the logits from other uses; null: none), then the head backward of head_bwd_kernel.
+template <int VPL>
+__global__ void head_ce_bwd_kernel(const float* __restrict__ prob, const long long* __restrict__ label,
+                                   const float* __restrict__ g, const float* __restrict__ dlogits_in, int B, int C,
+                                   int S, const float* __restrict__ xhat, const float* __restrict__ rstd,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   const float* __restrict__ W, float* __restrict__ dW, float* __restrict__ dbias,
+                                   float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dh,
+                                   float* __restrict__ dl_scratch) {
+  constexpr int D = VPL * 64;
+  const int lane = threadIdx.x;
+  const float gs = g[0] / (float)B;
+  if (B == 1 && C <= 4) {
+    const int lab = (int)label[0];
+    float dl[4], gm[VPL], bt[VPL], xh[VPL], w[4][VPL];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      dl[k] = k < C ? gs * (prob[k] - (k == lab ? 1.f : 0.f)) + (dlogits_in ? dlogits_in[k] : 0.f) : 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane * VPL + i;
+      gm[i] = gamma[c]; bt[i] = beta[c]; xh[i] = xhat[c];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[k][i] = k < C ? W[(size_t)k * D + c] : 0.f;
+    }
+    float gg[VPL], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane * VPL + i;
+      float dy = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < C) {
+          dW[(size_t)k * D + c] = 0.f + dl[k] * (xh[i] * gm[i] + bt[i]);
+          dy += dl[k] * w[k][i];
+        }
+      dgamma[c] = 0.f + dy * xh[i];
+      dbeta[c] = 0.f + dy;
+      gg[i] = dy * gm[i];
+      s1 += gg[i];
+      s2 += gg[i] * xh[i];
+    }
+    if (lane == 0)
+      for (int k = 0; k < C; ++k) dbias[k] = 0.f + dl[k];
+    s1 = wave_sum(s1) * (1.0f / D);
+    s2 = wave_sum(s2) * (1.0f / D);
+    const float rs = rstd[0];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) dh[lane * VPL + i] = rs * (gg[i] - s1 - xh[i] * s2);
+    return;
+  }
+  // general B / C: dlogits into the scratch, then the general head backward
+  for (int i = lane; i < B * C; i += 64) {
+    const int b = i / C, c = i % C;
+    dl_scratch[i] = gs * (prob[i] - (c == (int)label[b] ? 1.f : 0.f)) + (dlogits_in ? dlogits_in[i] : 0.f);
+  }
+  __syncthreads();
+  const float* dlogits = dl_scratch;
+  float dgm[VPL], dbt[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) { dgm[i] = 0.f; dbt[i] = 0.f; }
+  for (int k = 0; k < C; ++k) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dlogits[b * C + k];
+    if (lane == 0) dbias[k] = s;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane * VPL + i;
+      float acc = 0.f;
+      for (int b = 0; b < B; ++b) acc += dlogits[b * C + k] * (xhat[(size_t)b * D + c] * gamma[c] + beta[c]);
+      dW[(size_t)k * D + c] = acc;
+    }
+  }
+  for (int b = 0; b < B; ++b) {
+    float gg[VPL], xh[VPL];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane * VPL + i;
+      float dy = 0.f;
+      for (int k = 0; k < C; ++k) dy += dlogits[b * C + k] * W[(size_t)k * D + c];
+      xh[i] = xhat[(size_t)b * D + c];
+      dgm[i] += dy * xh[i];
+      dbt[i] += dy;
+      gg[i] = dy * gamma[c];
+      s1 += gg[i];
+      s2 += gg[i] * xh[i];
+    }
+    s1 = wave_sum(s1) * (1.0f / D);
+    s2 = wave_sum(s2) * (1.0f / D);
+    const float rs = rstd[b];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) dh[(size_t)b * S * D + lane * VPL + i] = rs * (gg[i] - s1 - xh[i] * s2);
+  }
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) { dgamma[lane * VPL + i] = dgm[i]; dbeta[lane * VPL + i] = dbt[i]; }
+}
+
 }  // namespace
 
 #define TM_VPL_DISPATCH(D, CALL)                        \
@@ -348,6 +522,35 @@ extern "C" int tm_head_fwd(const float* h, int B, int S, int D, const float* gam
   TM_REQUIRE(h && gamma && beta && W && bias && logits && xhat && rstd && B > 0 && C > 0, "head_fwd: bad args");
   hipStream_t st = (hipStream_t)stream;
   TM_VPL_DISPATCH(D, (head_fwd_kernel<VPL><<<B, 64, 0, st>>>(h, S, gamma, beta, eps, W, bias, C, logits, xhat, rstd)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_head_ce_fwd(const float* h, int B, int S, int D, const float* gamma, const float* beta, float eps,
+                              const float* W, const float* bias, int C, const long long* label, float* logits,
+                              float* xhat, float* rstd, float* loss, float* prob, long long* yhat, int* class_stats,
+                              void* stream) {
+  TM_REQUIRE(h && gamma && beta && W && bias && label && logits && xhat && rstd && loss && prob && yhat && B > 0 &&
+                 C > 0, "head_ce_fwd: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  TM_VPL_DISPATCH(D, (head_ce_fwd_kernel<VPL><<<1, 64 * HEAD_CE_WAVES, 0, st>>>(
+                         h, B, S, gamma, beta, eps, W, bias, C, label, logits, xhat, rstd, loss, prob, yhat,
+                         class_stats)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_head_ce_bwd(const float* prob, const long long* label, const float* gloss, const float* dlogits_in,
+                              int B, int C, int S, int D, const float* xhat, const float* rstd, const float* gamma,
+                              const float* beta, const float* W, float* dW, float* dbias, float* dgamma, float* dbeta,
+                              float* dh, float* scratch, void* stream) {
+  TM_REQUIRE(prob && label && gloss && xhat && rstd && gamma && beta && W && dW && dbias && dgamma && dbeta && dh,
+             "head_ce_bwd: null arg");
+  TM_REQUIRE((B == 1 && C <= 4) || scratch, "head_ce_bwd: scratch [B*C] needed unless B == 1 and C <= 4");
+  hipStream_t st = (hipStream_t)stream;
+  TM_VPL_DISPATCH(D, (head_ce_bwd_kernel<VPL><<<1, 64, 0, st>>>(prob, label, gloss, dlogits_in, B, C, S, xhat, rstd,
+                                                                gamma, beta, W, dW, dbias, dgamma, dbeta, dh,
+                                                                scratch)));
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <type_traits>
 #include "common.h"
+#include "a3_combine.h"
 #include "../../include/transmil_hip.h"
 
 namespace {
@@ -178,6 +179,90 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
     }
   }
 }
+
+// bench-mode A2 = softmax_j(ql_i . kl_j) on the MFMA: the logits as bf16x3 products (x = hi + lo,
+// hi*hi + hi*lo + lo*hi, fp32 accumulation: ~2^-17 relative, the precision of the split planes
+// the chain then reads).  grid (nbh, 8), block 512: rows 32 by .. of one head; wave w owns
+// columns 32 w .. 32 w + 31 (one 32x32 tile, 4 k-steps x 3 MFMAs).  Every operand load is issued
+// before the first MFMA (64 floats per lane); row max / sum: 32-lane shuffles, then the 8 waves'
+// partials through LDS in a fixed order.  Writes A2 (fp32) and its hi / lo planes.
+#ifdef TM_DIAG
+__global__ __launch_bounds__(512) void sim2_softmax_mfma_kernel(const float* __restrict__ ql,
+                                                                const float* __restrict__ kl, float* __restrict__ a2,
+                                                                bf16* __restrict__ a2s) {
+  __shared__ float red[2][8][32];
+  const int bh = blockIdx.x, r0 = blockIdx.y * 32, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5, c0 = wave * 32;
+  const float* qa = ql + ((size_t)bh * NL + r0 + r) * DH + 8 * h;
+  const float* kb = kl + ((size_t)bh * NL + c0 + r) * DH + 8 * h;
+  f32x4 av[8], bv[8];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    av[2 * s] = *(const f32x4*)(qa + 16 * s);
+    av[2 * s + 1] = *(const f32x4*)(qa + 16 * s + 4);
+    bv[2 * s] = *(const f32x4*)(kb + 16 * s);
+    bv[2 * s + 1] = *(const f32x4*)(kb + 16 * s + 4);
+  }
+  f32x16 acc = (f32x16){};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    bf16x8 ah, al, bhi, blo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = e < 4 ? av[2 * s][e] : av[2 * s + 1][e - 4];
+      const float y = e < 4 ? bv[2 * s][e] : bv[2 * s + 1][e - 4];
+      ah[e] = (bf16)x;
+      al[e] = (bf16)(x - (float)ah[e]);
+      bhi[e] = (bf16)y;
+      blo[e] = (bf16)(y - (float)bhi[e]);
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bhi, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, blo, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bhi, acc, 0, 0, 0);
+  }
+  // row i (reg i, half h) holds columns c0 + (lane & 31): max / sum over the 32 lanes of the half
+  auto half_max = [](float v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+  };
+  auto half_sum = [](float v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float m = half_max(acc[i]);
+    if (r == 0) red[0][wave][acc_row(i, h)] = m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = acc_row(i, h);
+    float m = red[0][0][row];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) m = fmaxf(m, red[0][w][row]);
+    acc[i] = __expf(acc[i] - m);
+    const float t = half_sum(acc[i]);
+    if (r == 0) red[1][wave][row] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = acc_row(i, h);
+    const float tot = ((red[1][0][row] + red[1][1][row]) + (red[1][2][row] + red[1][3][row])) +
+                      ((red[1][4][row] + red[1][5][row]) + (red[1][6][row] + red[1][7][row]));
+    const size_t o = ((size_t)bh * NL + r0 + row) * NL + c0 + r;
+    const float v = acc[i] / tot;
+    a2[o] = v;
+    const bf16 hi = (bf16)v;
+    a2s[o] = hi;
+    a2s[o + (size_t)gridDim.x * NL * NL] = (bf16)(v - (float)hi);
+  }
+}
+
+#endif  // TM_DIAG
 
 // dS2 = A2 * (dA2 - rowsum(dA2 * A2)); grid (nbh*256/4), block 256 (one wave per row)
 __global__ void softmax_bwd_rows_kernel(const float* __restrict__ a, const float* __restrict__ da,
@@ -899,56 +984,13 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
     }
 }
 
-// combine of the v2 partials: grid (nbh, 32), block 256: item = (query blockIdx.y * 8 + (tid & 127) / 16,
-// 4 d); the two thread halves take the even / odd partials (every load issued first), merged through
-// LDS in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void a3_combine_v2_kernel(const float* __restrict__ part_o,
-                                                            const float* __restrict__ part_m,
-                                                            const float* __restrict__ part_l, int P, int nbh,
-                                                            float* __restrict__ w, float* __restrict__ lse3) {
-  constexpr int U = 16;   // partials per thread per burst
-  __shared__ f32x4 xo[128];
-  __shared__ float xm[128], xl[128];
-  const int bh = blockIdx.x, item = threadIdx.x & 127, half = threadIdx.x >> 7;
-  const int qi = blockIdx.y * 8 + (item >> 4), d4 = (item & 15) * 4;
-  const size_t q0 = (size_t)bh * NL + qi, pstride = (size_t)nbh * NL;
-  float M = -INFINITY, L = 0.f;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int p0 = half; p0 < P; p0 += 2 * U) {
-    float mv[U], lv[U];
-    f32x4 ov[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t pidx = (size_t)min(p0 + 2 * u, P - 1) * pstride + q0;
-      mv[u] = part_m[pidx];
-      lv[u] = part_l[pidx];
-      ov[u] = *(const f32x4*)(part_o + pidx * DH + d4);
-    }
-    float mb = M;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (p0 + 2 * u < P) mb = fmaxf(mb, mv[u]);
-    const float c = __expf(M - mb);    // M = -inf on the first burst: 0
-    L *= c;
-    acc *= c;
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (p0 + 2 * u < P) {
-        const float sc = __expf(mv[u] - mb);
-        L += lv[u] * sc;
-        acc += ov[u] * sc;
-      }
-    M = mb;
-  }
-  if (half) { xo[item] = acc; xm[item] = M; xl[item] = L; }
+// combine of the v2 partials: grid (nbh, 32), block 256 (a3_combine.h; the bench step runs the same
+// routine inside the pseudo-inverse chain's last launch instead, tm_pinv_fwd_split_a3)
+__global__ __launch_bounds__(256) void a3_combine_v2_kernel(A3Combine c) {
+  __shared__ A3CombineLds lds;
+  const A3CombineState st = a3_combine_phase1(c, blockIdx.x, blockIdx.y, threadIdx.x, lds, true);
   __syncthreads();
-  if (half) return;
-  const float Mo = xm[item], Mt = fmaxf(M, Mo);
-  const float ca = M == -INFINITY ? 0.f : __expf(M - Mt), cb = Mo == -INFINITY ? 0.f : __expf(Mo - Mt);
-  const float Lt = L * ca + xl[item] * cb;
-  const f32x4 at = acc * ca + xo[item] * cb;
-  *(f32x4*)(w + q0 * DH + d4) = at / Lt;
-  if (d4 == 0) lse3[q0] = Mt + __logf(Lt);
+  a3_combine_phase2(c, blockIdx.x, blockIdx.y, threadIdx.x, lds, st, true);
 }
 
 // combine the key-block partials: W[bh][q][d], lse3[bh][q]; grid (nbh, 16), block 256: thread =
@@ -1347,6 +1389,7 @@ struct BwdArgs {
   const void* v; long long v_bag, v_head;               // values (T), row stride 64
   const float* lse;  long long lse_bh;                  // [bh][...]
   const float* dd;   long long dd_bh;                   // D per query
+  const float* dd2;                                     // optional second partial of D (summed: dd + dd2)
   float* dq; long long dq_bh;                           // query-side grad (fp32, row stride 64)
   float* dk; long long dk_bh;                           // key-side grads (fp32, row stride 64)
   float* dv; long long dv_bh;
@@ -1409,6 +1452,7 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
   const T* V = (const T*)a.v + hoff(bh, nh, a.v_bag, a.v_head) + (size_t)key0 * DH;
   const float* lse = a.lse + bh * a.lse_bh;
   const float* dd = a.dd + bh * a.dd_bh;
+  const float* dd2 = a.dd2 ? a.dd2 + bh * a.dd_bh : nullptr;
 
   // K^T into LDS (all 256 keys): 16-B row loads, transposed element writes
   {
@@ -1463,7 +1507,7 @@ __global__ __launch_bounds__(512) void attn_bwd_kernel(BwdArgs a) {
         }
       }
     }
-    if (tid < 32) { lse_s[tid] = lse[qa + tid]; dd_s[tid] = dd[qa + tid]; }
+    if (tid < 32) { lse_s[tid] = lse[qa + tid]; dd_s[tid] = dd[qa + tid] + (dd2 ? dd2[qa + tid] : 0.f); }
     __syncthreads();
     // S = Q K^T, dP = dO V^T: rows = queries (registers), cols = this wave's keys (lanes)
     f32x16 s = (f32x16){}, dp = (f32x16){};
@@ -1674,6 +1718,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   const bf16* V = (const bf16*)a.v + hoff(bh, nh, a.v_bag, a.v_head) + (size_t)key0 * DH;
   const float* lse = a.lse + bh * a.lse_bh + q_begin;
   const float* dd = a.dd + bh * a.dd_bh + q_begin;
+  const float* dd2 = a.dd2 ? a.dd2 + bh * a.dd_bh + q_begin : nullptr;
 
   // ---- one burst of loads: K rows (for K^T), Q / dO rows, K / V fragments, lse / D ----
   constexpr int QP = (LY::MAXQ * 8 + NT - 1) / NT;  // 16-B query-row pieces per thread (5 | 4)
@@ -1703,7 +1748,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   if (tid < LY::MAXQ) {
     const int qq = min(tid, q_count - 1);
     lsev = lse[qq];
-    ddv = dd[qq];
+    ddv = dd[qq] + (dd2 ? dd2[qq] : 0.f);
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1958,7 +2003,12 @@ extern "C" int tm_nys_sim2_softmax(const float* ql, const float* kl, int nbh, fl
 extern "C" int tm_nys_sim2_softmax_split(const float* ql, const float* kl, int nbh, float* a2, void* a2s,
                                          void* stream) {
   TM_REQUIRE(a2s, "sim2_softmax_split: a2s is required");
-  sim2_softmax_kernel<<<dim3(nbh, NL / S2_ROWS), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, (bf16*)a2s);
+#ifdef TM_DIAG
+  if (NYS_VARIANT == 21)   // the MFMA form (measured slower: 15.1 vs 12 us with 64 workgroups)
+    sim2_softmax_mfma_kernel<<<dim3(nbh, NL / 32), 512, 0, (hipStream_t)stream>>>(ql, kl, a2, (bf16*)a2s);
+  else
+#endif
+    sim2_softmax_kernel<<<dim3(nbh, NL / S2_ROWS), 256, 0, (hipStream_t)stream>>>(ql, kl, a2, (bf16*)a2s);
   TM_CHECK_LAUNCH();
   return 0;
 }
@@ -1969,6 +2019,9 @@ extern "C" int tm_softmax_bwd_rows256(const float* a, const float* da, float* ds
   return 0;
 }
 
+// key splits (partials per head) of the bf16 A3 forward
+extern "C" long long tm_nys_a3_partials(int nbh, int n) { return a3v_splits(nbh, n); }
+
 extern "C" long long tm_nys_a3_workspace(int nbh, int n) {
   const long long parts = std::max((long long)(n / NL), (long long)a3v_splits(nbh, n));
   return parts * nbh * NL * (DH + 2) * (long long)sizeof(float);
@@ -1977,6 +2030,7 @@ extern "C" long long tm_nys_a3_workspace(int nbh, int n) {
 extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
                              float* w, float* lse3, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0, "a3_fwd: n must be a positive multiple of 256");
+  TM_REQUIRE((w && lse3) || dtype == TM_BF16, "a3_fwd: w / lse3 may be null (deferred combine) in bf16 mode only");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TM_BF16) {
     const int P = a3v_splits(nbh, n);
@@ -1986,7 +2040,8 @@ extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const vo
     tm_allow_smem(a3_fwd_v2_kernel, A3V_BYTES);
     a3_fwd_v2_kernel<<<dim3(P, nbh), 512, A3V_BYTES, st>>>(ql, (const bf16*)k, (const bf16*)v, n, P, po, pm, pl);
     TM_CHECK_LAUNCH();
-    a3_combine_v2_kernel<<<dim3(nbh, NL / 8), 256, 0, st>>>(po, pm, pl, P, nbh, w, lse3);
+    if (!w) return 0;   // deferred: the combine runs in the pseudo-inverse chain (tm_pinv_fwd_split_a3)
+    a3_combine_v2_kernel<<<dim3(nbh, NL / 8), 256, 0, st>>>(A3Combine{po, pm, pl, P, nbh, w, lse3});
     TM_CHECK_LAUNCH();
     return 0;
   }
@@ -2183,7 +2238,7 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
   a.dO = dw_t; a.o_bag = a.q_bag; a.o_head = a.q_head; a.o_row = DH;
   a.k = k; a.k_bag = (long long)nh * n * DH; a.k_head = (long long)n * DH;
   a.v = v; a.v_bag = a.k_bag; a.v_head = a.k_head;
-  a.lse = lse3; a.lse_bh = NL; a.dd = d3; a.dd_bh = NL;
+  a.lse = lse3; a.lse_bh = NL; a.dd = d3; a.dd2 = d3 + (size_t)nbh * NL; a.dd_bh = NL;   // [2][nbh][256] partials
   a.dq = work; a.dq_bh = (long long)NL * DH;
   a.slab_stride = (long long)nbh * NL * DH;
   a.dk = dk; a.dk_bh = (long long)n * DH;
@@ -2216,7 +2271,7 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   a.dO = dw_t; a.o_bag = a.q_bag; a.o_head = a.q_head; a.o_row = DH;
   a.k = k; a.k_bag = (long long)nh * n * DH; a.k_head = (long long)n * DH;
   a.v = v; a.v_bag = a.k_bag; a.v_head = a.k_head;
-  a.lse = lse3; a.lse_bh = NL; a.dd = d3; a.dd_bh = NL;
+  a.lse = lse3; a.lse_bh = NL; a.dd = d3; a.dd2 = d3 + (size_t)nbh * NL; a.dd_bh = NL;   // [2][nbh][256] partials
   a.dq = work; a.dq_bh = (long long)NL * DH;
   a.slab_stride = (long long)nbh * NL * DH;
   a.dv = (float*)dv_conv; a.dv_bh = (long long)n * DH;

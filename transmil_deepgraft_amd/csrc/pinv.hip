@@ -43,6 +43,14 @@ TM_DEV void store_ct(const tm_bmm_job& J, size_t off, float v) {
 
 
 
+// the partial row dot of an output element's 32-column tile (tm_bmm_job.Rd): a row's 32 columns are
+// the 32 lanes of one wave half (ln = lane, same register), summed by a fixed xor tree
+TM_DEV void store_rowdot(const tm_bmm_job& J, int bh, int nbatch, int row, int col, float d, int ln) {
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+  if ((ln & 31) == 0) J.Rd[((size_t)(col / 32) * nbatch + bh) * J.M + row] = d;
+}
+
 TM_DEV f32x8 frag_a(const float* A, int ta, int lda, int m, int k) {
   if (ta == 0) return load8<float>(A + (size_t)m * lda + k);
   f32x8 r;
@@ -141,6 +149,7 @@ __global__ __launch_bounds__(512) void bmm_kernel(JobPair jp, int nbatch) {
     J.C[off] = v;
     if (J.C2) J.C2[off] = J.c2_alpha * s + (row == col ? J.c2_diag : 0.f) + J.c2_e1 * e1v;
     store_ct(J, off, v);
+    if (J.Rd) store_rowdot(J, bh, nbatch, row, col, v * J.Rw[off], ln);
   }
 }
 
@@ -272,7 +281,7 @@ TM_DEV f32x8 fb(const float* B, int ldb, int k, int n) {
 }
 
 template <int PREC, int C>
-TM_DEV void bmm_tile(const tm_bmm_job& J, int bh, int tile, float (*red)[16][64]) {
+TM_DEV void bmm_tile(const tm_bmm_job& J, int bh, int tile, int nbatch, float (*red)[16][64]) {
   constexpr int TA = C & 1, TB = (C >> 1) & 1, TWO = (C >> 2) & 1, TA2 = (C >> 3) & 1, TB2 = (C >> 4) & 1;
   constexpr int SK = (C >> 5) & 3;
   constexpr int NSLOT = SK == 0 ? 2 : (SK == 1 ? 1 : 4);
@@ -292,6 +301,8 @@ TM_DEV void bmm_tile(const tm_bmm_job& J, int bh, int tile, float (*red)[16][64]
   }
   if (J.E1) { ev1[0] = J.E1[off[0]]; ev1[1] = J.E1[off[1]]; }
   if (J.E2) { ev2[0] = J.E2[off[0]]; ev2[1] = J.E2[off[1]]; }
+  float rw[2] = {0.f, 0.f};
+  if (J.Rd) { rw[0] = J.Rw[off[0]]; rw[1] = J.Rw[off[1]]; }
   f32x16 acc = (f32x16){};
   if (NSLOT > 1 || wave * 16 < J.K) {
     const float* A = J.A + bh * J.sa;
@@ -329,6 +340,7 @@ TM_DEV void bmm_tile(const tm_bmm_job& J, int bh, int tile, float (*red)[16][64]
     J.C[off[q]] = v;
     if (J.C2) J.C2[off[q]] = J.c2_alpha * sum + (row[q] == col[q] ? J.c2_diag : 0.f) + J.c2_e1 * ev1[q];
     store_ct(J, off[q], v);
+    if (J.Rd) store_rowdot(J, bh, nbatch, row[q], col[q], v * rw[q], ln);
   }
 }
 
@@ -337,10 +349,10 @@ __global__ __launch_bounds__(512) void bmm_spec_kernel(JobPair jp, int nbatch) {
   __shared__ float red[BMM_WAVES][16][64];
   const int b = blockIdx.x;
   if (C1 < 0 || b < jp.tiles0 * nbatch) {
-    bmm_tile<PREC, C0>(jp.j[0], b % nbatch, b / nbatch, red);
+    bmm_tile<PREC, C0>(jp.j[0], b % nbatch, b / nbatch, nbatch, red);
   } else {
     const int b1 = b - jp.tiles0 * nbatch;
-    bmm_tile<PREC, (C1 < 0 ? 0 : C1)>(jp.j[1], b1 % nbatch, b1 / nbatch, red);
+    bmm_tile<PREC, (C1 < 0 ? 0 : C1)>(jp.j[1], b1 % nbatch, b1 / nbatch, nbatch, red);
   }
 }
 

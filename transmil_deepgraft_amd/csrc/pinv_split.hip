@@ -32,6 +32,7 @@
 // iteration), then one launch for the partial sums of the c gradient and one that applies the
 // Z_0 = X^T / c terms and (optionally) the softmax backward of A2 = X.
 #include "common.h"
+#include "a3_combine.h"
 #include "../../include/transmil_hip.h"
 
 namespace {
@@ -88,6 +89,8 @@ struct SLaunch {
   float* sums;              // [2][nbh][256] row / column sums (abs-sum jobs)
   float* maxima_out;        // [2][nbh] (abs-sum jobs)
   unsigned* zero_ctr;       // abs-sum launch: the team kernels' counters to zero (TEAM_CTR_WORDS), or null
+  A3Combine a3;             // a3.w non-null: the row blockIdx.y == njobs runs the A3 forward's partial
+                            // combine (a3_combine.h) on the CUs the chain's tiles leave idle
   int dbg;                  // ablation (microbench only): 1 no DMA, 2 no LDS reads / MFMA, 3 no epilogue,
                             // 4 epilogue only, 5 empty
   unsigned long long* stamps;  // diagnostic build only: per-wave s_memtime stamps, or null
@@ -459,6 +462,18 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
 // blockIdx.y is the job.
 __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (blockIdx.y == (unsigned)L.njobs) {
+    // the A3 combine row: three 256-thread groups per workgroup, one item (head, 8 queries) each
+    A3CombineLds* lds = (A3CombineLds*)smem;
+    const int g = threadIdx.x >> 8, t = threadIdx.x & 255;
+    const int item = blockIdx.x * (NTHREADS / 256) + g;
+    const bool active = item < L.a3.nbh * 32;
+    const int bh = active ? item >> 5 : 0, qy = item & 31;
+    const A3CombineState st = a3_combine_phase1(L.a3, bh, qy, t, lds[g], active);
+    __syncthreads();
+    a3_combine_phase2(L.a3, bh, qy, t, lds[g], st, active);
+    return;
+  }
   const SJob& J = L.j[blockIdx.y];
   const int u = blockIdx.x;
   const int nbh = L.nbh;
@@ -507,6 +522,7 @@ __global__ __launch_bounds__(256) void pinv_c_dot_kernel(const bf16* __restrict_
 // dc = -sum(G0 o Z0)/c = -T/c^2,  dMc = dc * maxr, dMr = dc * maxc  (max ties share the gradient);
 // softmax != 0: out = X o (dX - rowsum(X o dX)) (the backward of A2 = softmax, X = A2), else out = dX.
 // grid (nbh, 16), block 256: 16 rows of one head, thread = column j.
+constexpr int APPLY_SUMS = 8;   // |X| sums per thread per kind in one burst (nbh <= 8); larger nbh loops
 __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __restrict__ X, const float* __restrict__ sums,
                                                              const float* __restrict__ maxima, const bf16* __restrict__ G0,
                                                              long long plane, const float* __restrict__ part, int nbh,
@@ -517,7 +533,9 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
   const int bh = blockIdx.x, i0 = blockIdx.y * 16, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const size_t hb = (size_t)bh * MAT;
   // every load is issued up front (one memory round trip): G0[t][i0..i0+15] (the transpose term of
-  // column t, 32 contiguous bytes per plane), X and dXc rows i0..i0+15 at column t, the sums
+  // column t, 32 contiguous bytes per plane), X and dXc rows i0..i0+15 at column t, this block's
+  // row sums and column sum, the per-head maxima (lane h), the |X| sums for the tie counts and the
+  // partial dots (lane-strided, clamped, masked)
   float g0[16], xv[16], dx[16];
   {
     const size_t o = hb + (size_t)t * NL + i0;
@@ -532,18 +550,34 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
     xv[ii] = X[off];
     dx[ii] = dXc[off];
   }
-  // maxima, tie counts and the fixed-order sum of the partial dots
-  float mc = -INFINITY, mr = -INFINITY;
-  for (int h = 0; h < nbh; ++h) { mc = fmaxf(mc, maxima[h]); mr = fmaxf(mr, maxima[nbh + h]); }
-  float nc = 0.f, nr = 0.f, ps = 0.f;
-  for (int e = t; e < nbh * NL; e += 256) { nc += sums[e] == mc; nr += sums[nbh * NL + e] == mr; }
-  for (int e = t; e < nbh * 16; e += 256) ps += part[e];
   const float* rs = sums + (size_t)bh * NL;
   const float* cs = sums + (size_t)(nbh + bh) * NL;
   const float csv = cs[t];
   float rsv[16];
 #pragma unroll
-  for (int ii = 0; ii < 16; ++ii) rsv[ii] = rs[i0 + ii];
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 v = *(const f32x4*)(rs + i0 + 4 * q);
+    rsv[4 * q] = v[0]; rsv[4 * q + 1] = v[1]; rsv[4 * q + 2] = v[2]; rsv[4 * q + 3] = v[3];
+  }
+  const int total = nbh * NL;
+  float sc[APPLY_SUMS], sr[APPLY_SUMS];
+#pragma unroll
+  for (int u = 0; u < APPLY_SUMS; ++u) {
+    const int e = min(t + 256 * u, total - 1);
+    sc[u] = sums[e];
+    sr[u] = sums[total + e];
+  }
+  const float mcl = lane < nbh ? maxima[lane] : -INFINITY, mrl = lane < nbh ? maxima[nbh + lane] : -INFINITY;
+  float ps = t < nbh * 16 ? part[t] : 0.f;
+  // global maxima (nbh <= 64: one lane per head), tie counts, the fixed-order partial-dot sum
+  float mc = wave_max(mcl), mr = wave_max(mrl);
+  for (int h = 64; h < nbh; ++h) { mc = fmaxf(mc, maxima[h]); mr = fmaxf(mr, maxima[nbh + h]); }
+  float nc = 0.f, nr = 0.f;
+#pragma unroll
+  for (int u = 0; u < APPLY_SUMS; ++u)
+    if (t + 256 * u < total) { nc += sc[u] == mc; nr += sr[u] == mr; }
+  for (int e = t + 256 * APPLY_SUMS; e < total; e += 256) { nc += sums[e] == mc; nr += sums[total + e] == mr; }
+  for (int e = t + 256; e < nbh * 16; e += 256) ps += part[e];
   nc = wave_sum(nc); nr = wave_sum(nr); ps = wave_sum(ps);
   if (lane == 0) { red[wave][0] = nc; red[wave][1] = nr; red[wave][2] = ps; }
   __syncthreads();
@@ -855,7 +889,8 @@ struct Launcher {
   void add(const SJob& j) { L.j[L.njobs++] = j; }
   int go(hipStream_t st) {
     tm_allow_smem(pinv_stage_kernel, STAGE_LDS + EPI_LDS);
-    const dim3 grid(16 * L.nbh, L.njobs);
+    dim3 grid(16 * L.nbh, L.njobs);
+    if (L.a3.w) grid.y += 1;   // one more row for the A3 combine: ceil(nbh * 32 / 3) <= 16 nbh items
     pinv_stage_kernel<<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
     TM_CHECK_LAUNCH();
 #ifdef TM_DIAG
@@ -867,7 +902,8 @@ struct Launcher {
 
 // the levels [0, nlev) of one direction: one launch per level (or, diagnostic build variant 8,
 // the persistent kernel)
-int run_levels(const ChainArgs& c, int dir, long long plane, const float* maxima, unsigned* ctr, hipStream_t st) {
+int run_levels(const ChainArgs& c, int dir, long long plane, const float* maxima, unsigned* ctr, hipStream_t st,
+               const A3Combine* a3 = nullptr) {
 #ifdef TM_DIAG
   if (g_split_dbg == 8 || g_split_dbg == 9) {   // 9: plain-policy DMA (timing probe only: L1 may be stale)
     TeamArgs T{c, dir, plane, maxima, ctr, g_split_stamps};
@@ -885,6 +921,7 @@ int run_levels(const ChainArgs& c, int dir, long long plane, const float* maxima
     Launcher l(c.nbh, plane, maxima);
     const int nj = dir == 0 ? fwd_level_njobs(c.iters, lvl) : bwd_level_njobs(c.iters, lvl);
     for (int j = 0; j < nj; ++j) l.add(dir == 0 ? fwd_level_job(c, lvl, j) : bwd_level_job(c, lvl, j));
+    if (a3 && dir == 0 && lvl == nlev - 1) l.L.a3 = *a3;   // the forward's last level: one 128-tile job
     if (int rc = l.go(st)) return rc;
   }
   return 0;
@@ -901,7 +938,28 @@ extern "C" long long tm_pinv_split_saved_floats(int nbh, int iters) {
 // Z_iters (fp32) sits at the start of `saved`.  Two launches: L1 (S = X X^T and the |X| sums /
 // maxima, which couple all heads through c, and the zeroed team counters), then every other
 // level in the persistent kernel.
+int pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* saved, const A3Combine* a3,
+                   void* stream);
+
 extern "C" int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* saved, void* stream) {
+  return pinv_fwd_split(X, Xs, nbh, iters, saved, nullptr, stream);
+}
+
+// as tm_pinv_fwd_split, and the A3 forward's partial combine (tm_nys_a3_fwd with w = null left the
+// partials in a3_work: part_o [P][nbh][256][64], then part_m, part_l [P][nbh][256]) runs beside the
+// chain's last product: W and lse3 are written by the same launch that writes Z_iters.
+extern "C" int tm_pinv_fwd_split_a3(const float* X, const void* Xs, int nbh, int iters, float* saved,
+                                    const float* a3_work, int a3_parts, float* w, float* lse3, void* stream) {
+  TM_REQUIRE(a3_work && w && lse3 && a3_parts >= 1, "pinv_fwd_split_a3: bad A3 args");
+  const float* po = a3_work;
+  const float* pm = po + (size_t)a3_parts * nbh * NL * 64;
+  const float* pl = pm + (size_t)a3_parts * nbh * NL;
+  const A3Combine a3{po, pm, pl, a3_parts, nbh, w, lse3};
+  return pinv_fwd_split(X, Xs, nbh, iters, saved, &a3, stream);
+}
+
+int pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* saved, const A3Combine* a3,
+                   void* stream) {
   TM_REQUIRE(X && Xs && saved && nbh > 0 && iters >= 1, "pinv_fwd_split: bad args (iters >= 1)");
   TM_REQUIRE(((uintptr_t)Xs % 16) == 0 && ((uintptr_t)saved % 16) == 0, "pinv_fwd_split: 16-B aligned buffers");
   hipStream_t st = (hipStream_t)stream;
@@ -919,7 +977,7 @@ extern "C" int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int it
     if (int rc = l.go(st)) return rc;
   }
   const ChainArgs c{(const bf16*)Xs, saved, nullptr, nbh, iters};
-  return run_levels(c, 0, plane, maxima, F.team_ctr(nbh, 0), st);
+  return run_levels(c, 0, plane, maxima, F.team_ctr(nbh, 0), st, a3);
 }
 
 // workspace: G, dT5, dZa, dP, dT3 (split) + dX (fp32) + partial dots

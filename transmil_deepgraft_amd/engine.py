@@ -263,10 +263,14 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool, cls_r
     lse3 = pool(nbh * NL)
     work = pool(_lib.query("tm_nys_a3_workspace", nbh, n) // 4)
     # (measured: running A3 V on a second stream beside the pseudo-inverse chain slowed
-    #  the step -- the chain's launches then wait for CUs -- so the path stays serial)
-    with probe("a3_fwd"):
-        _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
+    #  the step -- the chain's launches then wait for CUs -- so the path stays serial; in bench
+    #  mode the partials' combine runs inside the chain's last launch, on the CUs it leaves idle)
     prec = 1 if dt_code == BF16 else 0
+    with probe("a3_fwd"):
+        if prec:
+            _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(None), _p(None), st)
+        else:
+            _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
     a2s = None
     if prec:
         # bench mode: the pseudo-inverse chain on split bf16 hi/lo operands (pinv_split.hip)
@@ -274,7 +278,8 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool, cls_r
         saved = pool(_lib.query("tm_pinv_split_saved_floats", nbh, PINV_ITERS))
         _lib.call("tm_nys_sim2_softmax_split", _p(ql), _p(kl), nbh, _p(a2), _p(a2s), st)
         with probe("pinv_fwd"):
-            _lib.call("tm_pinv_fwd_split", _p(a2), _p(a2s), nbh, PINV_ITERS, _p(saved), st)
+            _lib.call("tm_pinv_fwd_split_a3", _p(a2), _p(a2s), nbh, PINV_ITERS, _p(saved), _p(work),
+                      _lib.query("tm_nys_a3_partials", nbh, n), _p(w), _p(lse3), st)
         z = saved[:nbh * NL * NL].view(nbh, NL, NL)
     else:
         saved = pool(_lib.query("tm_pinv_saved_floats", nbh, PINV_ITERS))
@@ -352,12 +357,19 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         dz_job = bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH, Ct=pwork, ct_mode=2, ct_plane=mat)
     else:
         dz_job = bmm_job(dy, 0, state["w"], 1, dz, NL, NL, DH)
-    bmm([dz_job, bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)], nbh, prec)
-    d3 = pool(nbh * NL)
-    dw_t = pool(nbh * NL * DH, tdtype)
+    # dW = Z^T dY with, from the same launch, its T copy (the A3 backward's dO) and D3 =
+    # rowsum(dW o W) as the two 32-column partials the A3 backward sums
+    d3 = pool(2 * nbh * NL)
+    if dt_code == BF16:
+        dw_t = pool(nbh * NL * DH, tdtype)
+        dw_job = bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL, Ct=dw_t, ct_mode=1)
+    else:
+        dw_t = dw
+        dw_job = bmm_job(state["z"], 1, dy, 0, dw, NL, DH, NL)
+    dw_job.Rd, dw_job.Rw = d3.data_ptr(), state["w"].data_ptr()
+    bmm([dz_job, dw_job], nbh, prec)
     dql3 = pool(nbh * NL * DH).view(nbh, NL, DH)
     work3 = pool(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4)
-    _lib.call("tm_nys_rowdot_cast", dt_code, _p(dw), _p(state["w"]), nbh * NL, _p(d3), _p(dw_t), st)
     if not fused:
         # A3 product backward: dk (=), dv (+=), dql3 (=)
         with probe("a3_bwd"):
@@ -593,8 +605,13 @@ class TransMILEngine:
         p["fc_w"], p["fc_b"] = params[self.head + ".weight"], params[self.head + ".bias"]
         return p
 
-    def forward(self, x, params, drop_p=0.0, seeds=(0x1F123BB5, 0x2A9F4C61), seed_dev=None, counter=None):
+    def forward(self, x, params, drop_p=0.0, seeds=(0x1F123BB5, 0x2A9F4C61), seed_dev=None, counter=None, ce=None):
         """x [B, N, F] fp32 (on the GPU) -> logits [B, C] fp32 and the saved context.
+
+        ``ce = (label int64 [B], class_stats int32 [C, 2] or None)``: the training step's
+        CrossEntropyLoss(logits, one_hot(label)) with Y_prob / Y_hat in the head's launch
+        (tm_head_ce_fwd); ctx["ce"] = (label, prob, loss, yhat) and backward(gloss=...) takes
+        the loss gradient straight into the head backward (tm_head_ce_bwd).
 
         Dropout (train mode) hashes (row, col) with a per-layer seed; with ``seed_dev``
         (a 1-element int64 device tensor) the seed is read on the device, so a
@@ -654,21 +671,35 @@ class TransMILEngine:
         logits = torch.empty(B, Ccls, dtype=torch.float32, device=dev)
         xhat = pool(B * D)
         hrstd = pool(B)
-        _lib.call("tm_head_fwd", _p(H3), B, geo.S, D, _p(prm["norm_w"]), _p(prm["norm_b"]), C.c_float(LN_EPS),
-                  _p(prm["fc_w"]), _p(prm["fc_b"]), Ccls, _p(logits), _p(xhat), _p(hrstd), st)
+        ce_out = None
+        if ce is None:
+            _lib.call("tm_head_fwd", _p(H3), B, geo.S, D, _p(prm["norm_w"]), _p(prm["norm_b"]), C.c_float(LN_EPS),
+                      _p(prm["fc_w"]), _p(prm["fc_b"]), Ccls, _p(logits), _p(xhat), _p(hrstd), st)
+        else:
+            label, stats = ce
+            loss = torch.empty((), dtype=torch.float32, device=dev)
+            prob = torch.empty(B, Ccls, dtype=torch.float32, device=dev)
+            yhat = torch.empty(B, dtype=torch.int64, device=dev)
+            _lib.call("tm_head_ce_fwd", _p(H3), B, geo.S, D, _p(prm["norm_w"]), _p(prm["norm_b"]),
+                      C.c_float(LN_EPS), _p(prm["fc_w"]), _p(prm["fc_b"]), Ccls, _p(label), _p(logits), _p(xhat),
+                      _p(hrstd), _p(loss), _p(prob), _p(yhat), _p(stats), st)
+            ce_out = (label, prob, loss, yhat)
         ctx = dict(geo=geo, prm=prm, xt=xt, pre=pre, H0=H0, H1=H1, H2=H2, s1=s1, s2=s2, xhat=xhat, hrstd=hrstd,
-                   inner=inner)
+                   inner=inner, ce=ce_out)
         return logits, ctx
 
-    def backward(self, dlogits, ctx, params, out=None, ready=None):
+    def backward(self, dlogits, ctx, params, out=None, ready=None, gloss=None):
         """Returns a dict name -> fp32 gradient with the reference parameter names.
+
+        ``gloss``: the gradient of the forward's fused loss (``ce``; a 0-d device tensor); then
+        ``dlogits`` is the gradient reaching the logits from other uses, or None.
 
         ``out``: name -> preallocated fp32 tensor to write each gradient into (the views of a
         ``GradBucket``); ``ready(part)``: called once the head, norm, layer2 and PPEG gradients
         are final (part 0, before layer1's backward is enqueued) and at the end (part 1), so
         a bucketed all-reduce of part 0 overlaps layer1 / _fc1 backward."""
         geo, prm = ctx["geo"], ctx["prm"]
-        dev = dlogits.device
+        dev = ctx["H0"].device
         pool = Pool(dev)
         B, N, F, D, S = geo.B, geo.N, geo.F, geo.D, geo.S
         st = _stream()
@@ -677,10 +708,19 @@ class TransMILEngine:
         Ccls = prm["fc_w"].shape[0]
         # layer 2 on the class rows reads dL/dH3 only there (its LayerNorm backward writes the rest)
         dH = (torch.empty if self.cls_only else torch.zeros)(B * S, D, dtype=torch.float32, device=dev)
-        _lib.call("tm_head_bwd", _p(dlogits.contiguous()), B, Ccls, S, D, _p(ctx["xhat"]), _p(ctx["hrstd"]),
-                  _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g[self.head + ".weight"]),
-                  _p(g[self.head + ".bias"]),
-                  _p(g["norm.weight"]), _p(g["norm.bias"]), _p(dH), st)
+        if gloss is not None:
+            label, prob = ctx["ce"][0], ctx["ce"][1]
+            scratch = None if (B == 1 and Ccls <= 4) else pool(B * Ccls)
+            dl_in = None if dlogits is None else dlogits.float().contiguous()
+            _lib.call("tm_head_ce_bwd", _p(prob), _p(label), _p(gloss.float().contiguous()), _p(dl_in), B, Ccls, S,
+                      D, _p(ctx["xhat"]), _p(ctx["hrstd"]), _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]),
+                      _p(g[self.head + ".weight"]), _p(g[self.head + ".bias"]), _p(g["norm.weight"]),
+                      _p(g["norm.bias"]), _p(dH), _p(scratch), st)
+        else:
+            _lib.call("tm_head_bwd", _p(dlogits.contiguous()), B, Ccls, S, D, _p(ctx["xhat"]), _p(ctx["hrstd"]),
+                      _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g[self.head + ".weight"]),
+                      _p(g[self.head + ".bias"]),
+                      _p(g["norm.weight"]), _p(g["norm.bias"]), _p(dH), st)
         dout1 = None
         for li, Hin, saved in ((2, ctx["H2"], ctx["s2"]), (1, ctx["H0"], ctx["s1"])):
             pre = f"layer{li}."

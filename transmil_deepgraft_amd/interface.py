@@ -482,11 +482,18 @@ class TransMILTask(nn.Module):
     def training_step(self, batch):
         bags, label, _ = batch
         if bags.is_cuda and isinstance(self.loss, nn.CrossEntropyLoss):
-            # fused: loss, Y_prob, Y_hat and the per-class count/correct of :350-356 in one launch
-            logits = self(bags.float().contiguous())
-            if self.class_stats is None or self.class_stats.device != logits.device:
-                self.class_stats = torch.zeros(self.n_classes, 2, dtype=torch.int32, device=logits.device)
-            loss, y_prob, y_hat = _CrossEntropyOneHot.apply(logits, label, self.class_stats)
+            # fused: loss, Y_prob, Y_hat and the per-class count/correct of :350-356 in one launch --
+            # the head's own launch where the model offers it (TransMIL.forward_ce), else tm_ce_fwd
+            x = bags.float().contiguous()
+            if self.class_stats is None or self.class_stats.device != x.device:
+                self.class_stats = torch.zeros(self.n_classes, 2, dtype=torch.int32, device=x.device)
+            fused = getattr(self.model, "forward_ce", None)
+            out = fused(x, label, self.class_stats) if fused is not None else None
+            if out is not None:
+                logits, loss, y_prob, y_hat = out
+            else:
+                logits = self(x)
+                loss, y_prob, y_hat = _CrossEntropyOneHot.apply(logits, label, self.class_stats)
         else:
             logits, y_prob, y_hat = self.step(bags)
             one_hot = F.one_hot(label, num_classes=self.n_classes).float()

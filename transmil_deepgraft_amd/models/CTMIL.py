@@ -68,6 +68,10 @@ class CTMIL(TransMIL):
     def grad_bucket_parts(self):
         return [[p for _, p in self.named_parameters()]]
 
+    def forward_ce(self, x, label, class_stats=None):
+        """No fused loss on this head: the task runs ``forward`` and its own CE launch."""
+        return None
+
     def forward(self, x):
         x = x.squeeze(0)                                            # :134
         if not x.is_cuda:

@@ -31,6 +31,10 @@ class MDMIL(TransMIL):
         self.register_buffer("_dropout_counter", torch.randint(0, 2 ** 62, (1,), dtype=torch.int64),
                              persistent=False)
 
+    def forward_ce(self, x, label, class_stats=None):
+        """No fused loss on this head: the task runs ``forward`` and its own CE launch."""
+        return None
+
     def forward(self, x):
         logits, (attn2, _padding) = super().forward(x, return_attn=True)
         return logits, attn2

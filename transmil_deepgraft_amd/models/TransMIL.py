@@ -65,37 +65,49 @@ class PPEG(nn.Module):
 
 
 class _TransMILFn(torch.autograd.Function):
+    """The fused engine as one autograd node.  ``ce = (label, class_stats)`` (TransMILTask's
+    training step): the node also returns the CrossEntropy loss, Y_prob and Y_hat from the head's
+    launch, and its backward takes the loss gradient into the head backward's launch."""
+
     @staticmethod
-    def forward(ctx, engine, names, drop_p, seed_dev, holder, bucket, counter, x, *params):
+    def forward(ctx, engine, names, drop_p, seed_dev, holder, bucket, counter, ce, x, *params):
         prm = dict(zip(names, params))
         with torch.cuda.device(x.device):   # kernels go to x's device and its current stream
-            logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev, counter=counter)
+            logits, c = engine.forward(x, prm, drop_p, seed_dev=seed_dev, counter=counter, ce=ce)
         ctx.engine, ctx.c, ctx.names, ctx.prm, ctx.bucket = engine, c, names, prm, bucket
         if holder is not None:
             holder["ctx"] = c
-        return logits
+        if ce is None:
+            return logits
+        _label, prob, loss, yhat = c["ce"]
+        ctx.mark_non_differentiable(prob, yhat)
+        ctx.set_materialize_grads(False)    # no zero-filled gradients for unused outputs
+        return logits, loss, prob, yhat
 
     @staticmethod
-    def backward(ctx, dlogits):
+    def backward(ctx, dlogits, *rest):
         if ctx.c is None:
             raise RuntimeError("TransMIL (fused HIP path): the saved activations were freed by the first "
                                "backward; retain_graph=True is not supported on the fused path -- set "
                                "model.fused = False (module-by-module path) to backpropagate twice")
-        head = (None,) * 8
+        head = (None,) * 9
+        gloss = rest[0] if rest else None
         bucket, prm = ctx.bucket, ctx.prm
-        dl = dlogits.float().contiguous()
-        with torch.cuda.device(dlogits.device):
+        dl = None if dlogits is None else dlogits.float().contiguous()
+        dev = ctx.c["H0"].device
+        with torch.cuda.device(dev):
             if bucket is not None and all(p.grad is None for p in prm.values()):
                 # first micro-batch after zero_grad: the kernels write straight into the bucket and
                 # the parameters' .grad become its views (stable addresses: hipGraph-safe, no copy)
                 views = {n: bucket.view(p) for n, p in prm.items()}
-                dx = ctx.engine.backward(dl, ctx.c, prm, out=views, ready=bucket.ready).pop("__dx__", None)
+                dx = ctx.engine.backward(dl, ctx.c, prm, out=views, ready=bucket.ready,
+                                         gloss=gloss).pop("__dx__", None)
                 ctx.c = None
                 with torch.no_grad():
                     for n, p in prm.items():
                         p.grad = views[n]
-                return head[:7] + (dx,) + (None,) * len(ctx.names)
-            g = ctx.engine.backward(dl, ctx.c, prm)
+                return head[:8] + (dx,) + (None,) * len(ctx.names)
+            g = ctx.engine.backward(dl, ctx.c, prm, gloss=gloss)
             dx = g.pop("__dx__", None)
             ctx.c = None
             if bucket is not None and all(bucket.owns(p) for p in prm.values()):
@@ -104,8 +116,8 @@ class _TransMILFn(torch.autograd.Function):
                     torch._foreach_add_([p.grad for p in prm.values()], [g[n] for n in ctx.names])
                 bucket.ready(0)
                 bucket.ready(1)
-                return head[:7] + (dx,) + (None,) * len(ctx.names)
-        return head[:7] + (dx,) + tuple(g[n] for n in ctx.names)
+                return head[:8] + (dx,) + (None,) * len(ctx.names)
+        return head[:8] + (dx,) + tuple(g[n] for n in ctx.names)
 
 
 class TransMIL(nn.Module):
@@ -248,8 +260,32 @@ class TransMIL(nn.Module):
             x = self._pre_embed(x).contiguous()
         return self._fused(x, layout, return_attn)
 
-    def _fused(self, x, layout, return_attn):
-        """The fused engine node: x [B, N, F] (F = D for a pre-embedded input) -> logits."""
+    def forward_ce(self, x, label, class_stats=None):
+        """The training step's forward + CrossEntropyLoss(logits, one_hot(label).float()) with
+        Y_prob / Y_hat / the per-class count-correct (code/models/model_interface.py:333-356) on
+        the fused path, the loss computed in the head's launch: returns (logits, loss, Y_prob,
+        Y_hat), or None where the fused path does not apply (hooks, input gradients,
+        ``fused = False``) -- the caller then runs ``forward`` and the loss itself."""
+        if x.dim() > 3:
+            x = x.squeeze(0)
+        elif x.dim() == 2:
+            x = x.unsqueeze(0)
+        if not x.is_cuda:
+            raise RuntimeError("TransMIL (HIP) needs a GPU tensor: there is no CPU path")
+        layout = self._fc1_layout()
+        x = x.float().contiguous()
+        if not self.fused or self._hooked() or x.requires_grad:
+            return None
+        if layout is FC1_EMBED:
+            x = self._pre_embed(x).contiguous()
+        lab = label.reshape(-1).to(device=x.device, dtype=torch.int64).contiguous()
+        if lab.numel() != x.shape[0]:
+            raise ValueError(f"forward_ce: {lab.numel()} labels for {x.shape[0]} bags")
+        return self._fused(x, layout, False, ce=(lab, class_stats))
+
+    def _fused(self, x, layout, return_attn, ce=None):
+        """The fused engine node: x [B, N, F] (F = D for a pre-embedded input) -> logits
+        (with ``ce``: logits, loss, Y_prob, Y_hat)."""
         names, params = self._engine_params(layout)
         drop_p = self.layer1.attn.to_out[1].p if self.training else 0.0
         seed_dev = None
@@ -259,8 +295,11 @@ class TransMIL(nn.Module):
             seed_dev = torch.empty(1, dtype=torch.int64, device=x.device)
         holder = {} if return_attn else None
         engine = TransMILEngine(self.compute_dtype, fc1=layout, head=self._head)
-        logits = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, self._grad_bucket,
-                                   self._dropout_counter if drop_p > 0 else None, x, *params)
+        out = _TransMILFn.apply(engine, names, drop_p, seed_dev, holder, self._grad_bucket,
+                                self._dropout_counter if drop_p > 0 else None, ce, x, *params)
+        if ce is not None:
+            return out
+        logits = out
         if return_attn:
             c = holder["ctx"]
             S = c["geo"].S
