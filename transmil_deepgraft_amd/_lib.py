@@ -148,6 +148,7 @@ DIAG_SIGS = {
     "tm_debug_set_split_stamps": (None, [P]),
     "tm_debug_a1_stamps": (I, [P, I]),
     "tm_debug_gemm_stamps": (I, [P, I]),
+    "tm_debug_set_ppeg_wt": (None, [I]),
 }
 
 _lib = None

@@ -111,19 +111,37 @@ __global__ void dropout_bwd_pad_kernel(const float* __restrict__ dH, int S, int 
   }
 }
 
-// dpre[b*N + i][c] = (dH[b*S + 1 + i][c] + (i < add ? dH[b*S + 1 + N + i][c] : 0)) * gelu'(pre[b*N+i][c])
-// grid (N, B), block 256
+// dpre = (dH[token] + dH[duplicated pad row]) * GELU'(pre) for the N token rows of every bag, 8
+// columns per thread (16-B loads, one 16-B T store), 4 rows per 256-thread block; block (0, 0) also
+// writes the class-token gradient dcls = sum_b dH[b, 0, :] (one launch for both).
 template <typename T>
-__global__ void fc1_gelu_bwd_kernel(const float* __restrict__ dH, const float* __restrict__ pre, int N, int S, int add,
-                                    int D, T* __restrict__ dpre) {
-  const int i = blockIdx.x, b = blockIdx.y;
+__global__ __launch_bounds__(256) void fc1_gelu_bwd_kernel(const float* __restrict__ dH, const float* __restrict__ pre,
+                                                           int B, int N, int S, int add, int D, T* __restrict__ dpre,
+                                                           float* __restrict__ dcls) {
+  const int b = blockIdx.y, i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && b == 0 && dcls) {
+    for (int c = threadIdx.x; c < D; c += 256) {
+      float sacc = 0.f;
+      for (int bb = 0; bb < B; ++bb) sacc += dH[(size_t)bb * S * D + c];
+      dcls[c] = sacc;
+    }
+  }
+  if (i >= N) return;
   const float* g0 = dH + ((size_t)b * S + 1 + i) * D;
   const float* g1 = dH + ((size_t)b * S + 1 + N + i) * D;
   const size_t o = ((size_t)b * N + i) * D;
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float g = g0[c];
-    if (i < add) g += g1[c];
-    dpre[o + c] = from_f<T>(g * gelu_erf_grad(pre[o + c]));
+  for (int c = lane * 8; c < D; c += 64 * 8) {
+    const f32x4 a0 = *(const f32x4*)(g0 + c), a1 = *(const f32x4*)(g0 + c + 4);
+    const f32x4 p0 = *(const f32x4*)(pre + o + c), p1 = *(const f32x4*)(pre + o + c + 4);
+    f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+    if (i < add) { d0 = *(const f32x4*)(g1 + c); d1 = *(const f32x4*)(g1 + c + 4); }
+    vec8<T> out;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      out[e] = from_f<T>((a0[e] + d0[e]) * gelu_erf_grad(p0[e]));
+      out[4 + e] = from_f<T>((a1[e] + d1[e]) * gelu_erf_grad(p1[e]));
+    }
+    store8<T>(dpre + o + c, out);
   }
 }
 
@@ -154,14 +172,6 @@ __global__ void pad_rows_kernel(const float* __restrict__ x, int S, int n_pad, i
     dst[c] = from_f<T>(i >= 0 ? x[((size_t)b * S + i) * D + c] : 0.f);
 }
 
-// dcls[c] = sum_b dH[b*S][c]
-__global__ void cls_grad_kernel(const float* __restrict__ dH, int B, int S, int D, float* __restrict__ dcls) {
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dH[(size_t)b * S * D + c];
-    dcls[c] = s;
-  }
-}
 
 // y = max(a + b, 0), elementwise over 8-element pieces (the C5 encoder's residual add + ReLU in
 // one pass instead of two; a and y may alias).  grid-stride, block 256.
@@ -278,10 +288,10 @@ extern "C" int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, i
 extern "C" int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
                                void* dpre, float* dcls, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  TM_DTYPE_DISPATCH(dtype, (fc1_gelu_bwd_kernel<T><<<dim3(N, B), 256, 0, st>>>(dH, pre, N, S, add, D,
-                                                                               (T*)dpre)));
-  TM_CHECK_LAUNCH();
-  cls_grad_kernel<<<1, 256, 0, st>>>(dH, B, S, D, dcls);
+  TM_REQUIRE(D % 8 == 0 && ((uintptr_t)dH % 16) == 0 && ((uintptr_t)pre % 16) == 0 && ((uintptr_t)dpre % 16) == 0,
+             "fc1_gelu_bwd: D % 8 == 0 and 16-B aligned rows");
+  TM_DTYPE_DISPATCH(dtype, (fc1_gelu_bwd_kernel<T><<<dim3((N + 3) / 4, B), 256, 0, st>>>(dH, pre, B, N, S, add, D,
+                                                                                         (T*)dpre, dcls)));
   TM_CHECK_LAUNCH();
   return 0;
 }

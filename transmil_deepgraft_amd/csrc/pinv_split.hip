@@ -460,9 +460,12 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
 
 // One launch = up to three independent jobs over all heads.  Grid: (16 * nbh, njobs);
 // blockIdx.y is the job.
+// AUX: the launch carries the A3 combine row (only the forward's last level; a separate
+// instantiation, so the other levels' code is not touched by the combine's registers)
+template <bool AUX>
 __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (blockIdx.y == (unsigned)L.njobs) {
+  if (AUX && blockIdx.y == (unsigned)L.njobs) {
     // the A3 combine row: three 256-thread groups per workgroup, one item (head, 8 queries) each
     A3CombineLds* lds = (A3CombineLds*)smem;
     const int g = threadIdx.x >> 8, t = threadIdx.x & 255;
@@ -888,10 +891,15 @@ struct Launcher {
   }
   void add(const SJob& j) { L.j[L.njobs++] = j; }
   int go(hipStream_t st) {
-    tm_allow_smem(pinv_stage_kernel, STAGE_LDS + EPI_LDS);
     dim3 grid(16 * L.nbh, L.njobs);
-    if (L.a3.w) grid.y += 1;   // one more row for the A3 combine: ceil(nbh * 32 / 3) <= 16 nbh items
-    pinv_stage_kernel<<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
+    if (L.a3.w) {   // one more row for the A3 combine: ceil(nbh * 32 / 3) <= 16 nbh items
+      grid.y += 1;
+      tm_allow_smem(pinv_stage_kernel<true>, STAGE_LDS + EPI_LDS);
+      pinv_stage_kernel<true><<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
+    } else {
+      tm_allow_smem(pinv_stage_kernel<false>, STAGE_LDS + EPI_LDS);
+      pinv_stage_kernel<false><<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
+    }
     TM_CHECK_LAUNCH();
 #ifdef TM_DIAG
     if (g_split_stamps) g_split_stamps += (size_t)grid.x * grid.y * 4 * 8;  // the next launch's stamps follow

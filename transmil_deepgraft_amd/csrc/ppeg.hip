@@ -150,10 +150,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void p
 // tile through LDS, as the stencil), thread (channel, g) accumulating its 16 cells x 49 taps;
 // the 4 g partials are summed in order through LDS.  grid (ceil(nTC / WT) * D / 64, nTR, B),
 // partial slab index = (b * gridDim.y + by) * gridDim.x/nchunk + bx/nchunk, layout [slab][ch][50].
-constexpr int WT = 4;
+constexpr int WT_DEFAULT = 3;   // G = 91: 4 column groups x 12 row tiles x 8 channel chunks = 384 blocks (scripts/dev/ppeg_wt.py: 43.0 vs 48.3 us at 4)
+#ifdef TM_DIAG
+int g_ppeg_wt = 0;   // diagnostic build: tiles per wgrad block (0: WT_DEFAULT)
+#define PPEG_WT (g_ppeg_wt > 0 ? g_ppeg_wt : WT_DEFAULT)
+#else
+#define PPEG_WT WT_DEFAULT
+#endif
 constexpr int DY_LDS = TR * TC * 64 * 4;   // 16 KB
 __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy_,
-                                                         int S, int G, int D, float* __restrict__ part) {
+                                                         int S, int G, int D, int WT, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float win[];
   float* dyt = win + WIN * 64;
   const int nchunk = D / 64;
@@ -238,6 +244,10 @@ __global__ __launch_bounds__(256) void ppeg_wgrad_reduce_kernel(const float* __r
 
 }  // namespace
 
+#ifdef TM_DIAG
+extern "C" void tm_debug_set_ppeg_wt(int v) { g_ppeg_wt = v; }
+#endif
+
 extern "C" int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, const float* b5, const float* w3,
                             const float* b3, int D, float* wfold, float* bfold, void* stream) {
   ppeg_fold_kernel<<<(D + 63) / 64, 64, 0, (hipStream_t)stream>>>(w7, b7, w5, b5, w3, b3, D, wfold, bfold);
@@ -256,18 +266,23 @@ extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfo
   return 0;
 }
 
-static dim3 wgrad_grid(int B, int G, int D) {
+static dim3 wgrad_grid(int B, int G, int D, int wt) {
   const int ntc = (G + TC - 1) / TC;
-  return dim3(((ntc + WT - 1) / WT) * (D / 64), (G + TR - 1) / TR, B);
+  return dim3(((ntc + wt - 1) / wt) * (D / 64), (G + TR - 1) / TR, B);
 }
 
-static int ppeg_wgrad_slabs(int B, int G) {
-  const dim3 g = wgrad_grid(B, G, 64);
+static int ppeg_wgrad_slabs(int B, int G, int wt) {
+  const dim3 g = wgrad_grid(B, G, 64, wt);
   return (int)(g.x * g.y * g.z);
 }
 
 extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
-  return (long long)ppeg_wgrad_slabs(B, G) * D * 50 * (long long)sizeof(float);
+#ifdef TM_DIAG
+  const int wt = 1;   // the largest slab count any diagnostic WT needs
+#else
+  const int wt = PPEG_WT;
+#endif
+  return (long long)ppeg_wgrad_slabs(B, G, wt) * D * 50 * (long long)sizeof(float);
 }
 
 // dy: [B,S,D] upstream gradient; x: PPEG input.  dx written (=); weight grads written.
@@ -285,10 +300,11 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
       dy, S, G, D, wfold, nullptr, dx, dp);
   TM_CHECK_LAUNCH();
   tm_allow_smem(ppeg_wgrad_kernel, TILE_LDS + DY_LDS);
-  ppeg_wgrad_kernel<<<wgrad_grid(B, G, D), 256, TILE_LDS + DY_LDS, st>>>(x, dy, S, G, D, work);
+  const int wt = PPEG_WT;
+  ppeg_wgrad_kernel<<<wgrad_grid(B, G, D, wt), 256, TILE_LDS + DY_LDS, st>>>(x, dy, S, G, D, wt, work);
   TM_CHECK_LAUNCH();
   (void)dwsum;
-  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, ppeg_wgrad_slabs(B, G), D, dw7, db7, dw5,
+  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, ppeg_wgrad_slabs(B, G, wt), D, dw7, db7, dw5,
                                                                      db5, dw3, db3);
   TM_CHECK_LAUNCH();
   return 0;
