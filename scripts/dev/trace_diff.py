@@ -1,11 +1,15 @@
-"""Per-kernel time per step of two rocprofv3 kernel traces (A vs B), matched by name, over the
-timed graph replays (steps found by the head kernel)."""
-import csv, sys, collections
+"""Per-kernel time per step of rocprofv3 kernel traces, A runs vs B runs (each side: the minimum
+over its runs of the per-step mean, so clock drift between runs counts against neither), matched
+by name, over the middle half of the timed graph replays (steps found by a marker kernel).
+    python scripts/dev/trace_diff.py "gpurun_out/prof_A*" "gpurun_out/prof_B*" [marker]"""
+import csv, glob, sys, collections
+
+
 def load(path, marker):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
     idx = [i for i, r in enumerate(rows) if marker in r['Kernel_Name']]
-    idx = idx[len(idx) // 4: 3 * len(idx) // 4]      # middle half of the steps
+    idx = idx[len(idx) // 4: 3 * len(idx) // 4]
     per = collections.defaultdict(float); cnt = collections.defaultdict(int)
     for a, b in zip(idx[:-1], idx[1:]):
         for r in rows[a:b]:
@@ -14,10 +18,22 @@ def load(path, marker):
             cnt[n] += 1
     k = max(len(idx) - 1, 1)
     return {n: (per[n] / k, cnt[n] / k) for n in per}
-A = load(sys.argv[1], sys.argv[3] if len(sys.argv) > 3 else 'head_')
-B = load(sys.argv[2], sys.argv[4] if len(sys.argv) > 4 else 'head_')
+
+
+def side(pattern, marker):
+    runs = [load(f, marker) for f in sorted(glob.glob(pattern + "/run_kernel_trace.csv"))]
+    out = {}
+    for r in runs:
+        for n, v in r.items():
+            out[n] = min(out.get(n, v), v, key=lambda t: t[0])
+    return out, len(runs)
+
+
+marker = sys.argv[3] if len(sys.argv) > 3 else 'head_ce_fwd'
+A, na = side(sys.argv[1], marker)
+B, nb = side(sys.argv[2], marker)
 names = sorted(set(A) | set(B), key=lambda n: -max(A.get(n, (0, 0))[0], B.get(n, (0, 0))[0]))
-print(f"{'A us':>8} {'B us':>8} {'diff':>7}  kernel (calls A/B)")
+print(f"{'A us':>8} {'B us':>8} {'diff':>7}  kernel (calls A/B)   [{na} A runs, {nb} B runs]")
 for n in names:
     a, ca = A.get(n, (0, 0)); b, cb = B.get(n, (0, 0))
     if max(a, b) < 0.5: continue

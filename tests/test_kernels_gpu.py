@@ -156,6 +156,50 @@ def test_gemm_qkv_scatter(dtype):
     assert _rel(out.cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("N,K,b_kn,mode", [(512, 1536, 1, "plain"), (512, 512, 1, "plain"),
+                                          (512, 512, 0, "to_out"), (1536, 512, 0, "qkv")])
+def test_gemm_160_row_tiles_at_bench_rows(N, K, b_kn, mode):
+    """The step's bf16 GEMMs at M = n' = 8448 rows (33 x 256), which run on 160-row tiles (53 row
+    tiles: 212 / 636 tiles instead of 264 / 792): dxn / dmerged (B [K, N]), to_out (bias, dropout,
+    residual, the front-pad row map), QKV (head-major scatter, q x 1/8) against fp64."""
+    from transmil_deepgraft_amd.engine import gemm
+    from transmil_deepgraft_amd._lib import BF16, F32
+    M = 8448
+    g = torch.Generator().manual_seed(N + K + b_kn)
+    A = (torch.randn(M, K, generator=g) * 0.5).to(torch.bfloat16)
+    W = (torch.randn(K, N, generator=g) if b_kn else torch.randn(N, K, generator=g)) * 0.05
+    W = W.to(torch.bfloat16)
+    Wt = W.double() if b_kn else W.double().t()
+    full = A.double() @ Wt
+    if mode == "plain":
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        gemm(A.to(DEV), W.to(DEV), out, M, N, K, lda=K, ldb=N if b_kn else K, ldc=N, b_kn=b_kn, dtype=BF16)
+        torch.cuda.synchronize()
+        assert _rel(out.cpu(), full) < 8e-3
+    elif mode == "to_out":
+        # rows of the padded layout [n' = 8448] -> residual rows (pad 166 dropped): S = 8282
+        pad, S = 166, 8282
+        bias = torch.randn(N, generator=g)
+        R = torch.randn(S, N, generator=g)
+        out = torch.full((S, N), float("nan"), device=DEV)
+        gemm(A.to(DEV), W.to(DEV), out, M, N, K, lda=K, ldb=K, ldc=N, dtype=BF16, c_dtype=F32, bias=bias.to(DEV),
+             drop_p=0.7, seed=99, resid=R.to(DEV), rowmap=(M, pad, S, 0, 0, 0))
+        torch.cuda.synchronize()
+        o = out.cpu().double() - R.double()
+        ref = (full[pad:] + bias.double()) / 0.3
+        kept = o.abs() > 0
+        assert abs(kept.double().mean().item() - 0.3) < 0.01
+        assert _rel(o[kept], ref[kept]) < 8e-3
+    else:
+        Bg, nh = 1, 8
+        out = torch.empty(3, nh, M, 64, dtype=torch.bfloat16, device=DEV)
+        gemm(A.to(DEV), W.to(DEV), out, M, N, K, lda=K, ldb=K, ldc=0, dtype=BF16, qkv=(Bg, nh, 64, M, 0.125))
+        torch.cuda.synchronize()
+        ref = full.view(M, 3, nh, 64).permute(1, 2, 0, 3).clone()
+        ref[0] *= 0.125
+        assert _rel(out.cpu(), ref) < 8e-3
+
+
 # ----------------------------------------------------------------------------- LayerNorm
 def test_layernorm_fwd_bwd():
     from transmil_deepgraft_amd import ops

@@ -732,6 +732,99 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
 }
 
 // ---------------------------------------------------------------------------
+// 160 x 128 tiles for the M = n' = 8448-row GEMMs of the step (k-contiguous A only).  At 8448 rows
+// a 128-row tiling is 66 row tiles: 264 tiles for N = 512 (8 more than 256 CUs: eight CUs take two
+// tiles and set the launch time) and 792 for N = 1536 (3.1 per CU); 160 rows give 53 row tiles:
+// 212 tiles (one round) and 636.  10 waves = 5 (M) x 2 (N) of the ring kernel's 32 x 64 subtiles,
+// the same 2-stage LDS-DMA ring (A 20 KB + B 16 KB per stage: 72 KB, two workgroups per CU), the
+// same fragment reads; the epilogue stages the tile in three row passes (64, 64, 32 rows) through
+// the ring memory.
+constexpr int BM160 = 160;
+constexpr int R160_A = BM160 * 128, R160_STAGE = R160_A + 128 * 128;   // bytes: A image, A + B image
+
+// XCD-contiguous renumbering as tile_split_of_block, 160-row tiles, no split
+TM_DEV void tile160_of_block(int& m0, int& n0) {
+  const int ntx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int orig = blockIdx.y * ntx + blockIdx.x;
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+  m0 = (id / ntx) * BM160;
+  n0 = (id % ntx) * BN;
+}
+
+template <typename OutT, bool B_KN, int KIND = EK_ANY>
+__global__ __launch_bounds__(640) void gemm_ring160_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                           OutT* __restrict__ C, tm_gemm_args g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;   // 5 (M) x 2 (N) waves of 32 x 64
+  int m0, n0;
+  tile160_of_block(m0, n0);
+  const int nk = g.K / 64;                   // host guarantees 64 | K
+
+  f32x16 acc[2];
+  acc[0] = (f32x16){};
+  acc[1] = (f32x16){};
+  unsigned akc[4], bkc0[4] = {0, 0, 0, 0}, bkc1[4] = {0, 0, 0, 0};
+  unsigned bks0 = 0, bks1 = 0;
+  kc_addrs(akc, wm * 32, lane);
+  if constexpr (B_KN) {
+    bks0 = ks_addr(wn * 64, lane) + R160_A;
+    bks1 = ks_addr(wn * 64 + 32, lane) + R160_A;
+  } else {
+    kc_addrs(bkc0, wn * 64, lane);
+    kc_addrs(bkc1, wn * 64 + 32, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { bkc0[s] += R160_A; bkc1[s] += R160_A; }
+  }
+  const unsigned ring = lds_u32(smem);
+  // DMA pieces (1 KB wave-instructions): A = 20 (wave w: 2w, 2w + 1), B = 16 (waves 0-7: 2w, 2w + 1)
+  auto issue = [&](int kt) {
+    char* st = smem + (kt & 1) * R160_STAGE;
+    const int k0 = kt * 64;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = wave * 2 + i;
+      const int r = j * 8 + (lane >> 3), slot = lane & 7;
+      const int c = slot ^ ((r >> 1) & 7);
+      const int gr = min(m0 + r, g.M - 1);
+      __builtin_amdgcn_global_load_lds((glb_t*)(A + (size_t)gr * g.lda + k0 + c * 8), (lds_t*)(st + j * 1024), 16, 0, 0);
+    }
+    if (wave < 8) glds_tile<B_KN>(st + R160_A, B, g.ldb, n0, g.N, k0, wave, lane);
+  };
+  issue(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's pieces of tile kt landed (tile kt + 1 not yet issued: wait for all)
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();   // every wave's pieces landed; every wave done reading tile kt - 1
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1);  // overwrites tile kt - 1's buffer
+    const unsigned sb = ring + (kt & 1) * R160_STAGE;
+    ring_tile_mma<false, B_KN>(acc, sb, (B_KN ? bks0 : 0) + sb, (B_KN ? bks1 : 0) + sb, akc, bkc0, bkc1);
+  }
+  __syncthreads();   // all fragment reads done before the epilogue reuses the ring
+  float* ep = (float*)smem;
+  // three row passes: waves rows [0, 64), [64, 128), [128, 160)
+#pragma unroll 1
+  for (int pass = 0; pass < 3; ++pass) {
+    const int rlo = pass * 64, rows = pass < 2 ? 64 : 32;
+    if (wm * 32 >= rlo && wm * 32 < rlo + rows) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) stage_acc(ep, acc[j], wm * 32 - rlo, wn * 64 + j * 32, lane);
+    }
+    __syncthreads();
+    if (tid < 512) {
+      if (rows == 64) gemm_epilogue_rows<OutT, BN, 64, 512, KIND>(smem, C, g, m0 + rlo, n0, 0);
+      else gemm_epilogue_rows<OutT, BN, 32, 512, KIND>(smem, C, g, m0 + rlo, n0, 0);
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Persistent bf16 GEMM: one 512-thread workgroup per CU walks its tiles (t = blockIdx.x +
 // i * gridDim.x, XCD-clustered) as ONE stream of 64-deep k-steps, so the global_load_lds ring
 // keeps prefetching across tile boundaries: the next tile's first k-tiles are in flight while
@@ -1054,13 +1147,31 @@ inline int epilogue_kind(const tm_gemm_args& g) {
 
 template <typename OutT>
 bool ring_ok(const tm_gemm_args& g) {
-  if (GEMM_VARIANT != 0 && GEMM_VARIANT != 8 && (GEMM_VARIANT < 2 || GEMM_VARIANT > 6 || GEMM_VARIANT == 3)) return false;
+  if (GEMM_VARIANT != 0 && GEMM_VARIANT != 8 && GEMM_VARIANT != 9 && (GEMM_VARIANT < 2 || GEMM_VARIANT > 6 || GEMM_VARIANT == 3)) return false;
   // whole 64-deep k-tiles in every split; k-strided operands need >= 8 rows/cols (clamped 16-B pieces)
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if ((g.a_trans && g.M < 8) || (g.b_kn && g.N < 8)) return false;
   if (g.a_trans && g.M % 8 != 0) return false;
   if (g.b_kn && g.N % 8 != 0) return false;
   return true;
+}
+
+// 160-row tiles (k-contiguous A, no split)
+// (diagnostic build: variant 9 never, 10 wherever valid)
+inline bool use_ring160(const tm_gemm_args& g) {
+  if (g.a_trans || g.splits != 1 || g.K % 64 != 0 || g.M < BM160 || g.mode == TM_EPI_SPLITK) return false;
+  if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
+  if (GEMM_VARIANT == 10) return true;
+  if (GEMM_VARIANT != 0) return false;
+  // the heavy runtime-mode epilogue (dropout hash, residual, row map: to_out) stays on 128-row
+  // tiles: in the step it ran 22.6 vs 20 us there (three staging passes of 512 of 640 threads)
+  if (epilogue_kind(g) == EK_ANY) return false;
+  // where 128-row tiles spill past one per CU and 160-row tiles do not (N = 512 at 8448 rows: dxn
+  // 28.8 -> 22.9 us, to_out 16.2 -> 13.9, dmerged 13.3 -> 11.4); at N = 1536 (QKV, 3.1 vs 2.5 tiles
+  // per CU) the 128-row ring stays faster (24.5 vs 27.6 us; scripts/dev/gemm_variants.py 9,10)
+  const long long tn = (g.N + BN - 1) / BN;
+  const long long t128 = (g.M + 127) / 128 * tn, t160 = (g.M + BM160 - 1) / BM160 * tn;
+  return t128 > 256 && t160 <= 256;
 }
 
 template <typename OutT>
@@ -1110,6 +1221,24 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
 #undef TM_PERSIST_CASE
     }
 #endif
+    if (use_ring160(g)) {
+      constexpr size_t sm = 2 * R160_STAGE;
+      const dim3 g160((g.N + BN - 1) / BN, (g.M + BM160 - 1) / BM160);
+      const int kind = epilogue_kind(g);
+#define TM_R160(BKN, K)                                                                             \
+      {                                                                                             \
+        tm_allow_smem(gemm_ring160_kernel<OutT, BKN, K>, sm);                                       \
+        gemm_ring160_kernel<OutT, BKN, K><<<g160, 640, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+      }
+      if (g.b_kn) {
+        if (kind == EK_PLAIN) TM_R160(true, EK_PLAIN) else if (kind == EK_QKV) TM_R160(true, EK_QKV) else TM_R160(true, EK_ANY)
+      } else {
+        if (kind == EK_PLAIN) TM_R160(false, EK_PLAIN) else if (kind == EK_QKV) TM_R160(false, EK_QKV) else TM_R160(false, EK_ANY)
+      }
+#undef TM_R160
+      TM_CHECK_LAUNCH();
+      return 0;
+    }
     if (ring_ok<OutT>(g)) {
       constexpr size_t epi = (size_t)BM * EP_ROW * sizeof(float);
 #ifdef TM_DIAG
@@ -1132,7 +1261,7 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
 #endif
 #define TM_RING_CASE(AT, BKN)                                                                   \
       if (g.a_trans == AT && g.b_kn == BKN) {                                                   \
-        if (GEMM_VARIANT == 0 || GEMM_VARIANT == 5) {                                       \
+        if (GEMM_VARIANT == 0 || GEMM_VARIANT == 5 || GEMM_VARIANT == 9) {                  \
           constexpr size_t sm = 2 * STAGE_BYTES > epi ? 2 * STAGE_BYTES : epi;                  \
           const int kind = epilogue_kind(g);                                                    \
           if (kind == EK_PLAIN) {                                                               \
