@@ -1669,7 +1669,7 @@ TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) {
   return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int MODE, int NW = 8>
+template <int MODE, int NW = 8, int ST = 0>   // ST: diagnostic s_memtime stamps (g_a1_stamps): 1 phases, 2 one chunk
 __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   using LY = std::conditional_t<NW == 9, BwdLay9, BwdLay16>;
   static_assert(NW == 8 || (NW == 9 && MODE == MODE_A3), "9-wave form: A3 even split only");
@@ -1689,6 +1689,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int blk = blockIdx.x, bh = blockIdx.y, nh = a.nh;
+  auto stamp = [&](int slot) { if (ST == 1 && wave < 8) a1p_stamp<ST ? 9 : 0>(slot, wave); };
+  auto cstamp = [&](int c0, int slot) { if (ST == 2 && c0 == 64 && wave < 8) a1p_stamp<ST ? 9 : 0>(slot, wave); };
+  stamp(0);
   int key0 = (MODE == MODE_A3) ? blk * NL : 0;
   int nunits = 8;  // 32-key units of this workgroup (wave w < nunits owns keys key0 + 32 w ..)
   if (MODE == MODE_A3 && a.q_total > 0) {
@@ -1751,6 +1754,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
     ddv = dd[qq] + (dd2 ? dd2[qq] : 0.f);
   }
   __builtin_amdgcn_sched_barrier(0);
+  stamp(1);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int c = tid + NT * j, row = c >> 3, d0 = (c & 7) * 8;
@@ -1770,6 +1774,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
     dd_s[tid] = ddv;
   }
   __syncthreads();
+  stamp(2);
 
   f32x16 dvt[2], dkt[2];  // [d tile], cols = this wave's 32 keys
 #pragma unroll
@@ -1781,6 +1786,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   for (int c0 = 0; c0 < q_count; c0 += 32) {
     // S = Q K^T, dP = dO V^T: rows = queries (registers), cols = this wave's keys (lanes)
     f32x16 s = (f32x16){}, dp = (f32x16){};
+    cstamp(c0, 0);
     if (active) {
 #pragma unroll
       for (int st = 0; st < 4; ++st) {
@@ -1810,10 +1816,13 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
         }
       }
     }
+    cstamp(c0, 1);
     __syncthreads();  // previous chunk's dQ reads of ds_s / xch are done
+    cstamp(c0, 2);
 #pragma unroll
     for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + r] = from_f<bf16>(dp[i]);  // 0: idle wave
     __syncthreads();
+    cstamp(c0, 3);
     // dQ chunk [32 q x 64 d] = dS [32 x NK] . K [NK x 64]: this wave: d tile dt_q, keys 16 KQS kq ..
     {
       f32x16 acc = (f32x16){};
@@ -1828,7 +1837,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
           for (int i = 0; i < 16; ++i) xch[((kq - 1) * 2 + dt_q) * 1024 + i * 64 + lane] = acc[i];
         }
       }
+      cstamp(c0, 4);
       __syncthreads();
+      cstamp(c0, 5);
       if (kq == 0) {
         float* dst;
         if (MODE == MODE_A1) dst = a.dq + bh * a.dq_bh;
@@ -1842,10 +1853,65 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
           dst[(size_t)qq * DH + dt_q * 32 + r] = v;
         }
       }
+      cstamp(c0, 6);
     }
+    if (c0 == 0) stamp(3);
+    if (c0 == 96) stamp(4);
   }
+  stamp(5);
   // ---- key-side epilogue through LDS (transpose to [key][d]) ----
   __syncthreads();
+  if (MODE == MODE_A3 && a.dqkv) {
+    // fused: the final bf16 k / v rows of dqkv (no fp32 key-side slabs, no assemble pass for them):
+    // every addend load (the conv backward's dv window, dk~ / l) issued first, dV and dK staged
+    // side by side (one barrier), then 16-B bf16 stores of 8 columns per item
+    constexpr int IT = (LY::NK * DH / 8 + NT - 1) / NT;
+    static_assert(2 * LY::NK * 68 * 4 <= LY::BYTES, "fused A3 epilogue: two staged tiles exceed the layout");
+    const int bag = bh / nh, hh = bh % nh, inner = nh * DH;
+    bf16* outk = (bf16*)a.dqkv + ((size_t)bag * a.n_key_rows + key0) * 3 * inner + inner + hh * DH;
+    bf16* outv = outk + inner;
+    const float* dvc = a.dv + bh * a.dv_bh + (size_t)key0 * DH;
+    const float* dkl = a.dkl + (size_t)bh * NL * DH;
+    f32x4 av[IT][2], ak[IT][2];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + NT * it, key = i >> 3, d8 = (i & 7) * 8;
+      const bool valid = key < nk;
+      const bool vw = valid && key0 + key >= a.dv_lo && key0 + key < a.dv_hi;
+      const float* pv = dvc + (size_t)min(key, nk - 1) * DH + d8;
+      const float* pk = dkl + (size_t)((key0 + min(key, nk - 1)) / a.l) * DH + d8;
+      av[it][0] = vw ? *(const f32x4*)pv : (f32x4){0.f, 0.f, 0.f, 0.f};
+      av[it][1] = vw ? *(const f32x4*)(pv + 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      ak[it][0] = *(const f32x4*)pk;
+      ak[it][1] = *(const f32x4*)(pk + 4);
+    }
+    float* stage_k = stage + LY::NK * 68;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int o = (mykey + r) * 68 + dt * 32 + 8 * g4 + 4 * h;
+        *(f32x4*)(stage + o) = (f32x4){dvt[dt][4 * g4], dvt[dt][4 * g4 + 1], dvt[dt][4 * g4 + 2], dvt[dt][4 * g4 + 3]};
+        *(f32x4*)(stage_k + o) = (f32x4){dkt[dt][4 * g4], dkt[dt][4 * g4 + 1], dkt[dt][4 * g4 + 2], dkt[dt][4 * g4 + 3]};
+      }
+    __syncthreads();
+    const float il = a.inv_l;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + NT * it, key = i >> 3, d8 = (i & 7) * 8;
+      if (key >= nk) continue;
+      const float* sv = stage + key * 68 + d8;
+      const float* sk = stage_k + key * 68 + d8;
+      const f32x4 v0 = *(const f32x4*)sv + av[it][0], v1 = *(const f32x4*)(sv + 4) + av[it][1];
+      const f32x4 k0 = *(const f32x4*)sk + ak[it][0] * il, k1 = *(const f32x4*)(sk + 4) + ak[it][1] * il;
+      *(bf16x8*)(outv + (size_t)key * 3 * inner + d8) =
+          (bf16x8){(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3], (bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+      *(bf16x8*)(outk + (size_t)key * 3 * inner + d8) =
+          (bf16x8){(bf16)k0[0], (bf16)k0[1], (bf16)k0[2], (bf16)k0[3], (bf16)k1[0], (bf16)k1[1], (bf16)k1[2], (bf16)k1[3]};
+    }
+    stamp(6);
+    return;
+  }
 #pragma unroll
   for (int which = 0; which < 2; ++which) {
 #pragma unroll
@@ -1857,25 +1923,6 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
             (f32x4){accv[4 * g4], accv[4 * g4 + 1], accv[4 * g4 + 2], accv[4 * g4 + 3]};
     }
     __syncthreads();
-    if (MODE == MODE_A3 && a.dqkv) {
-      // fused: the final bf16 k / v rows of dqkv (no fp32 key-side slabs, no assemble pass for them)
-      const int bag = bh / nh, hh = bh % nh, inner = nh * DH;
-      bf16* out = (bf16*)a.dqkv + ((size_t)bag * a.n_key_rows + key0) * 3 * inner + (which == 0 ? 2 : 1) * inner + hh * DH;
-      const float* dvc = a.dv + bh * a.dv_bh + (size_t)key0 * DH;
-      const float* dkl = a.dkl + (size_t)bh * NL * DH;
-      for (int i = tid; i < nk * DH / 4; i += NT) {
-        const int key = i >> 4, d4 = (i & 15) * 4;
-        f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
-        if (which == 0) {
-          if (key0 + key >= a.dv_lo && key0 + key < a.dv_hi) val += *(const f32x4*)(dvc + (size_t)key * DH + d4);
-        }
-        else val += *(const f32x4*)(dkl + (size_t)((key0 + key) / a.l) * DH + d4) * a.inv_l;
-        *(bf16x4*)(out + (size_t)key * 3 * inner + d4) =
-            (bf16x4){(bf16)val[0], (bf16)val[1], (bf16)val[2], (bf16)val[3]};
-      }
-      __syncthreads();
-      continue;
-    }
     float* dst;
     bool add = false;
     if (MODE == MODE_A3) {
@@ -1893,6 +1940,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
     }
     __syncthreads();
   }
+  stamp(6);
 }
 
 template <typename T>
@@ -2214,6 +2262,18 @@ void launch_a3_bwd_bf16(BwdArgs& a, int nbh, int n, hipStream_t st, int& slabs) 
   a.q_total = n;  // even split on
   slabs = sp.wpg;
   if (sp.nw == 9) {
+#ifdef TM_DIAG
+    if (NYS_VARIANT == 30) {   // diagnostic: s_memtime stamps per wave (tm_debug_a1_stamps)
+      tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9, 1>, BwdLay9::BYTES);
+      attn_bwd_bf16_kernel<MODE_A3, 9, 1><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
+      return;
+    }
+    if (NYS_VARIANT == 31) {   // diagnostic: stamps inside query chunk 2
+      tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9, 2>, BwdLay9::BYTES);
+      attn_bwd_bf16_kernel<MODE_A3, 9, 2><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
+      return;
+    }
+#endif
     tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9>, BwdLay9::BYTES);
     attn_bwd_bf16_kernel<MODE_A3, 9><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
   } else {
