@@ -1646,7 +1646,7 @@ struct BwdLayT {
   static constexpr size_t DS_OFF = KT_OFF + DH * KT_ROW * 2;
   static constexpr size_t QS_OFF = DS_OFF + 32 * DS_ROW * 2;
   static constexpr size_t OS_OFF = QS_OFF + MAXQ * QROW * 2;
-  static constexpr size_t XC_OFF = OS_OFF + MAXQ * QROW * 2;  // fp32 [3][2][1024]
+  static constexpr size_t XC_OFF = OS_OFF + MAXQ * QROW * 2;  // fp32 [3][32 q][64 d] key-group dq partials
   static constexpr size_t LS_OFF = XC_OFF + 6 * 1024 * 4;     // fp32 lse[MAXQ], D[MAXQ]
   static constexpr size_t MAIN = LS_OFF + 2 * MAXQ * 4;       // 160512 B (<8, 288>), 157184 B (<9, 256>)
   static constexpr size_t EPI = (size_t)NK * 68 * 4;
@@ -1654,12 +1654,12 @@ struct BwdLayT {
 };
 using BwdLay16 = BwdLayT<8, 288>;
 using BwdLay9 = BwdLayT<9, 256>;
-static_assert(BwdLay9::BYTES <= 160 * 1024, "A3 even-split layout exceeds the CU's LDS");
+static_assert(BwdLay9::BYTES <= 160 * 1024 && BwdLay16::BYTES <= 160 * 1024, "bf16 backward layout exceeds the CU's LDS");
 
 // A-operand fragment (rows m = mb + l32, 8 k in acc_as_operand order) of a row-major
 // [k][QROW] bf16 image: element j of lane half h <-> k = kb + 8 (j >> 2) + 4 h + (j & 3)
-TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) {
-  constexpr int R = BwdLay16::QROW;
+template <int R>
+TM_DEV bf16x8 frag_tr_rows(const bf16* S, int mb, int kb, int lane) {
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int m = mb + (g & 1) * 16 + 4 * p;
   const int k = kb + 4 * (g >> 1) + q;
@@ -1668,6 +1668,7 @@ TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) {
   const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4*)(S + (k + 8) * R + m));
   return (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
+TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) { return frag_tr_rows<BwdLay16::QROW>(S, mb, kb, lane); }
 
 template <int MODE, int NW = 8, int ST = 0>   // ST: diagnostic s_memtime stamps (g_a1_stamps): 1 phases, 2 one chunk
 __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
@@ -1826,31 +1827,39 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
     // dQ chunk [32 q x 64 d] = dS [32 x NK] . K [NK x 64]: this wave: d tile dt_q, keys 16 KQS kq ..
     {
       f32x16 acc = (f32x16){};
+      float* dst = MODE == MODE_A1 ? a.dq + bh * a.dq_bh : a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;
+      dst += (size_t)(q_begin + c0) * DH;
       if (dq_role) {
 #pragma unroll
         for (int st = 0; st < KQS; ++st) {
           const int kk = kq * 16 * KQS + st * 16 + 8 * h;
           mma16(acc, load8(ds_s + r * DS_ROW + kk), load8(kt_s + (dt_q * 32 + r) * KT_ROW + kk));
         }
-        if (kq > 0) {
+        // [32 q][64 d] partials of key group kq (9 waves: every group, 3 x 8 KB; 8 waves: groups 1-3)
+        if (NW == 9 || kq > 0) {
+          float* xs = xch + (NW == 9 ? kq : kq - 1) * 2048;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) xch[((kq - 1) * 2 + dt_q) * 1024 + i * 64 + lane] = acc[i];
+          for (int i = 0; i < 16; ++i) xs[acc_row(i, h) * 64 + dt_q * 32 + r] = acc[i];
         }
       }
       cstamp(c0, 4);
       __syncthreads();
       cstamp(c0, 5);
-      if (kq == 0) {
-        float* dst;
-        if (MODE == MODE_A1) dst = a.dq + bh * a.dq_bh;
-        else dst = a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;
+      if constexpr (NW == 9) {
+        // every thread: one 4-column piece of the chunk's dq, the key groups summed in a fixed order
+        if (tid < 512) {
+          const int q = tid >> 4, d4 = (tid & 15) * 4;
+          const f32x4 v = (*(const f32x4*)(xch + q * 64 + d4) + *(const f32x4*)(xch + 2048 + q * 64 + d4)) +
+                          *(const f32x4*)(xch + 4096 + q * 64 + d4);
+          *(f32x4*)(dst + (size_t)q * DH + d4) = v;
+        }
+      } else if (kq == 0) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const int qq = q_begin + c0 + acc_row(i, h);
           float v = acc[i];
 #pragma unroll
-          for (int g = 0; g < NKQ - 1; ++g) v += xch[(g * 2 + dt_q) * 1024 + i * 64 + lane];
-          dst[(size_t)qq * DH + dt_q * 32 + r] = v;
+          for (int g = 0; g < NKQ - 1; ++g) v += xch[g * 2048 + acc_row(i, h) * 64 + dt_q * 32 + r];
+          dst[(size_t)acc_row(i, h) * DH + dt_q * 32 + r] = v;
         }
       }
       cstamp(c0, 6);
@@ -1863,8 +1872,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   __syncthreads();
   if (MODE == MODE_A3 && a.dqkv) {
     // fused: the final bf16 k / v rows of dqkv (no fp32 key-side slabs, no assemble pass for them):
-    // every addend load (the conv backward's dv window, dk~ / l) issued first, dV and dK staged
-    // side by side (one barrier), then 16-B bf16 stores of 8 columns per item
+    // the conv backward's dv window loads issued first, dV and dK staged side by side, the dk~ / l
+    // loads, one barrier, then 16-B bf16 stores of 8 columns per item
     constexpr int IT = (LY::NK * DH / 8 + NT - 1) / NT;
     static_assert(2 * LY::NK * 68 * 4 <= LY::BYTES, "fused A3 epilogue: two staged tiles exceed the layout");
     const int bag = bh / nh, hh = bh % nh, inner = nh * DH;
@@ -1879,11 +1888,8 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
       const bool valid = key < nk;
       const bool vw = valid && key0 + key >= a.dv_lo && key0 + key < a.dv_hi;
       const float* pv = dvc + (size_t)min(key, nk - 1) * DH + d8;
-      const float* pk = dkl + (size_t)((key0 + min(key, nk - 1)) / a.l) * DH + d8;
       av[it][0] = vw ? *(const f32x4*)pv : (f32x4){0.f, 0.f, 0.f, 0.f};
       av[it][1] = vw ? *(const f32x4*)(pv + 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-      ak[it][0] = *(const f32x4*)pk;
-      ak[it][1] = *(const f32x4*)(pk + 4);
     }
     float* stage_k = stage + LY::NK * 68;
 #pragma unroll
@@ -1894,6 +1900,14 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
         *(f32x4*)(stage + o) = (f32x4){dvt[dt][4 * g4], dvt[dt][4 * g4 + 1], dvt[dt][4 * g4 + 2], dvt[dt][4 * g4 + 3]};
         *(f32x4*)(stage_k + o) = (f32x4){dkt[dt][4 * g4], dkt[dt][4 * g4 + 1], dkt[dt][4 * g4 + 2], dkt[dt][4 * g4 + 3]};
       }
+    // dk~ / l rows (L2-resident: 256 x 64 per head) once dV / dK have left the registers
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + NT * it, key = min(i >> 3, nk - 1), d8 = (i & 7) * 8;
+      const float* pk = dkl + (size_t)((key0 + key) / a.l) * DH + d8;
+      ak[it][0] = *(const f32x4*)pk;
+      ak[it][1] = *(const f32x4*)(pk + 4);
+    }
     __syncthreads();
     const float il = a.inv_l;
 #pragma unroll
