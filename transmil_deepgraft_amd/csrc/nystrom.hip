@@ -870,6 +870,7 @@ constexpr int A3V_PIECES = (A3V_KEYS * 8 + 511) / 512;             // 16-B piece
 // partials per head of the v2 kernel
 inline int a3v_splits(int nbh, int n) { return std::max(1, std::min(n / 32, 256 / std::max(nbh, 1))); }
 
+template <int ST = 0>   // ST: diagnostic s_memtime stamps (g_a1_stamps)
 __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict__ ql, const bf16* __restrict__ k,
                                                         const bf16* __restrict__ v, int n, int P,
                                                         float* __restrict__ part_o, float* __restrict__ part_m,
@@ -878,6 +879,8 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int p = blockIdx.x, bh = blockIdx.y, nbh = gridDim.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  auto stamp = [&](int slot) { if (ST) a1p_stamp<ST ? 9 : 0>(slot, wave); };
+  stamp(0);
   const int S32 = n / 32;
   const int sb0 = (int)((long long)p * S32 / P), sb1 = (int)((long long)(p + 1) * S32 / P);
   const int qi = wave * 32 + r;
@@ -912,8 +915,10 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
   bf16x8 qf[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st) qf[st] = cvt8<bf16>(ql + ((size_t)bh * NL + qi) * DH + st * 16 + 8 * h);
+  stamp(1);
   stage(sb0, 0);
   __syncthreads();
+  stamp(2);
   float m_run = -INFINITY, l_run = 0.f;
   f32x16 o[2];
   o[0] = (f32x16){};
@@ -965,12 +970,15 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
             mma16(o[dt], value_frag<bf16>(vs, dt, kt * 32 + 16 * sp, lane), acc_as_operand<bf16>(s[kt], sp));
         }
     }
+    if (c0 == sb0) stamp(3);
     if (more) {
       stage(c0 + A3V_G, buf ^ 1);   // the other buffer: last read two chunks ago, before the barrier below
       __syncthreads();
       buf ^= 1;
     }
+    if (c0 == sb0) stamp(4);
   }
+  stamp(5);
   const size_t pidx = ((size_t)p * nbh + bh) * NL + qi;
   if (h == 0) { part_m[pidx] = m_run; part_l[pidx] = l_run; }
   float* po = part_o + pidx * DH;
@@ -982,6 +990,10 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
       val[0] = o[dt][4 * g4]; val[1] = o[dt][4 * g4 + 1]; val[2] = o[dt][4 * g4 + 2]; val[3] = o[dt][4 * g4 + 3];
       *(f32x4*)(po + dt * 32 + 8 * g4 + 4 * h) = val;
     }
+  if (ST) {
+    __builtin_amdgcn_s_waitcnt(0);
+    stamp(6);
+  }
 }
 
 // combine of the v2 partials: grid (nbh, 32), block 256 (a3_combine.h; the bench step runs the same
@@ -2099,8 +2111,16 @@ extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const vo
     float* po = work;
     float* pm = po + (size_t)P * nbh * NL * DH;
     float* pl = pm + (size_t)P * nbh * NL;
-    tm_allow_smem(a3_fwd_v2_kernel, A3V_BYTES);
-    a3_fwd_v2_kernel<<<dim3(P, nbh), 512, A3V_BYTES, st>>>(ql, (const bf16*)k, (const bf16*)v, n, P, po, pm, pl);
+#ifdef TM_DIAG
+    if (NYS_VARIANT == 32) {   // diagnostic: s_memtime stamps per wave (tm_debug_a1_stamps)
+      tm_allow_smem(a3_fwd_v2_kernel<1>, A3V_BYTES);
+      a3_fwd_v2_kernel<1><<<dim3(P, nbh), 512, A3V_BYTES, st>>>(ql, (const bf16*)k, (const bf16*)v, n, P, po, pm, pl);
+    } else
+#endif
+    {
+      tm_allow_smem(a3_fwd_v2_kernel<0>, A3V_BYTES);
+      a3_fwd_v2_kernel<0><<<dim3(P, nbh), 512, A3V_BYTES, st>>>(ql, (const bf16*)k, (const bf16*)v, n, P, po, pm, pl);
+    }
     TM_CHECK_LAUNCH();
     if (!w) return 0;   // deferred: the combine runs in the pseudo-inverse chain (tm_pinv_fwd_split_a3)
     a3_combine_v2_kernel<<<dim3(nbh, NL / 8), 256, 0, st>>>(A3Combine{po, pm, pl, P, nbh, w, lse3});
