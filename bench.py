@@ -118,6 +118,8 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
     ln = S * d * f4 + n * d * t + 2 * S * f4         # H (fp32) in, xn (T, pad rows included) out, mean / rstd
     landmarks = 2 * n * d * t + 2 * lm * (f4 + t)    # q, k in; q~, k~ out (fp32 + T copies)
     a3f = 2 * n * d * t + lm * f4 + lm * f4 + heads * m * f4   # k, v, q~ in; W, lse3 out
+    if t == 2:   # bf16: the same launch writes A2 (fp32 + split bf16 planes) from q~, k~ (tm_nys_a3_fwd_sim2)
+        a3f += lm * f4 + heads * m * m * (f4 + 2 * t)
     a1f = 2 * n * d * t + 2 * lm * t + n * d * t + heads * n * f4   # q, v, k~, Y in; merged, lse1 out
     ppf = 2 * S * d * f4                             # H1 in, H2 out (fp32 residual stream)
     ppb = 3 * S * d * f4 + n * d * t                 # H1, dH in; dH1 out; layer 1's padded dropout gradient out
@@ -129,8 +131,8 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
         ("ln_fwd", 1): ("ln_fwd_kernel", ln), ("ln_fwd", 2): ("ln_fwd_kernel", ln),
         ("landmarks", 1): ("landmarks_kernel", landmarks), ("landmarks", 2): ("landmarks_kernel", landmarks),
         # the key-split kernel; its partials' combine runs inside the pseudo-inverse chain's last launch
-        ("a3_fwd", 1): ("a3_fwd_v2_kernel (combine inside pinv F launch)", a3f),
-        ("a3_fwd", 2): ("a3_fwd_v2_kernel (combine inside pinv F launch)", a3f),
+        ("a3_fwd", 1): ("a3_fwd_v2_kernel<0, 4> (+ A2 rows; combine inside pinv F launch)", a3f),
+        ("a3_fwd", 2): ("a3_fwd_v2_kernel<0, 4> (+ A2 rows; combine inside pinv F launch)", a3f),
         ("a1_fwd", 1): ("a1_fwd_bf16_kernel", a1f),
         ("ppeg_fwd", 0): ("ppeg_stencil_kernel<false>", ppf),
         ("ppeg_bwd", 0): ("ppeg_stencil_kernel<true> + ppeg_wgrad_kernel + ppeg_wgrad_reduce_kernel", ppb),
@@ -173,14 +175,16 @@ def hbm_roofline(engine, run_step, steps, n_patches, dtype_bytes):
             ms = sorted(xs[k::len(layers)])[len(xs[k::len(layers)]) // 2]   # median over the probe steps
             kname, byts = model[(site, layer)]
             gbs = byts / (ms / 1e3) / 1e9
+            tr = measured_traffic(f"{site}:{layer}" if len(layers) > 1 else site, n_patches,
+                                  "bf16" if dtype_bytes == 2 else "fp32")
             out.append(dict(site=site, layer=layer, kernel=kname, algorithmic_bytes=byts, us=round(ms * 1e3, 2),
-                            achieved_gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4)))
+                            achieved_gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4), traffic=tr))
     return out
 
 
 def measured_traffic(site, n_patches, dtype):
     """HBM bytes per launch of `site` from the committed rocprofv3 PMC passes
-    (profiles/traffic.json, written by scripts/gpu_traffic.sh + scripts/traffic_summary.py):
+    (profiles/traffic.json, written by scripts/gpu_pmc_bench.sh + scripts/traffic_json.py):
     FETCH_SIZE (doubled for the gfx950 half-count) + WRITE_SIZE.  None when that file does not
     hold a measurement of this call site at this workload."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
@@ -428,7 +432,7 @@ def main():
         if overhead_samples:
             roof.update(event_span_ms=round(sum(span_samples) / len(span_samples), 5),
                         event_pair_overhead_ms=round(sum(overhead_samples) / len(overhead_samples), 5))
-        kname = {"pinv_fwd": "pinv_stage_kernel x14 (tm_pinv_fwd_split)"}.get(args.probe, args.probe)
+        kname = {"pinv_fwd": "pinv_stage_kernel x14 (tm_pinv_fwd_split_a3)"}.get(args.probe, args.probe)
         roof.update(kernel=kname, kernel_ms=round(kernel_ms, 5), samples=len(kernel_ms_samples),
                     algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])
         if "units" in rm:

@@ -127,6 +127,12 @@ long long tm_nys_a3_workspace(int nbh, int n);
 long long tm_nys_a3_partials(int nbh, int n);
 int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
                   float* w, float* lse3, void* stream);
+/* bf16 only: tm_nys_a3_fwd(TM_BF16, ..., w = NULL, lse3 = NULL) and tm_nys_sim2_softmax_split(ql, kl,
+ * nbh, a2, a2s) in ONE launch (the A3 workgroups also write the A2 rows, bit-identical to the
+ * separate kernel; two launches where the key split does not tile the 256 rows).  Both replace
+ * NystromAttention.forward's attn2 / attn3 softmaxes (code/models/TransMIL.py:47; App. A eq. 5-6). */
+int tm_nys_a3_fwd_sim2(const float* ql, const float* kl, const void* k, const void* v, int nbh, int n,
+                       float* work, float* a2, void* a2s, void* stream);
 /* merged[b][t][head*64+d] = softmax(q kl^T) y + conv33(v); lse1 [B*h, n]; kl_t, y_t: T copies */
 int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void* kl_t, const void* y_t,
                   const float* wconv, int nbh, int nh, int n, void* merged, float* lse1, void* stream);

@@ -160,3 +160,35 @@ def test_pinv_fwd_with_a3_combine_equals_separate_launches(nbh, n):
     assert torch.equal(w, w_ref) and torch.equal(lse, lse_ref)
     zn = nbh * 65536
     assert torch.equal(saved[:zn], saved_ref[:zn])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nbh,n", [(8, 8448), (16, 1280), (8, 256), (2, 4096)])
+def test_a3_fwd_with_sim2_equals_separate_launches(nbh, n):
+    """tm_nys_a3_fwd_sim2 (the A2 rows written by the A3 forward's workgroups) = tm_nys_a3_fwd
+    (deferred combine) + tm_nys_sim2_softmax_split, bit for bit: same partials, same A2 and planes
+    (the split tiles the 256 rows at (8, 8448) and (16, 1280); the others take the two-launch path)."""
+    from transmil_deepgraft_amd import _lib
+    from transmil_deepgraft_amd._lib import BF16
+    from transmil_deepgraft_amd.engine import _p, _stream
+    g = torch.Generator().manual_seed(7 * n + nbh)
+    ql = (torch.randn(nbh, 256, 64, generator=g) * 0.4).to(DEV)
+    kl = (torch.randn(nbh, 256, 64, generator=g) * 0.4).to(DEV)
+    k = (torch.randn(nbh, n, 64, generator=g) * 0.4).to(torch.bfloat16).to(DEV)
+    v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16).to(DEV)
+    nw = _lib.query("tm_nys_a3_workspace", nbh, n) // 4
+    work_ref = torch.full((nw,), float("nan"), device=DEV)
+    a2_ref = torch.full((nbh, 256, 256), float("nan"), device=DEV)
+    a2s_ref = torch.full((2 * nbh * 65536,), float("nan"), device=DEV).to(torch.bfloat16)
+    _lib.call("tm_nys_a3_fwd", BF16, _p(ql), _p(k), _p(v), nbh, n, _p(work_ref), _p(None), _p(None), _stream())
+    _lib.call("tm_nys_sim2_softmax_split", _p(ql), _p(kl), nbh, _p(a2_ref), _p(a2s_ref), _stream())
+    work = torch.full_like(work_ref, float("nan"))
+    a2 = torch.full_like(a2_ref, float("nan"))
+    a2s = torch.full_like(a2s_ref, float("nan"))
+    _lib.call("tm_nys_a3_fwd_sim2", _p(ql), _p(kl), _p(k), _p(v), nbh, n, _p(work), _p(a2), _p(a2s), _stream())
+    torch.cuda.synchronize()
+    P = _lib.query("tm_nys_a3_partials", nbh, n)
+    used = P * nbh * 256 * 66
+    assert torch.equal(work[:used], work_ref[:used])
+    assert torch.equal(a2, a2_ref) and torch.equal(a2s, a2s_ref)
+    assert torch.allclose(a2.sum(-1), torch.ones(nbh, 256, device=DEV), atol=1e-5)

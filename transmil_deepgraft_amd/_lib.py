@@ -83,6 +83,7 @@ _SIGS = {
     "tm_nys_a3_workspace": (L, [I, I]),
     "tm_nys_a3_partials": (L, [I, I]),
     "tm_nys_a3_fwd": (I, [I, P, P, P, I, I, P, P, P, P]),
+    "tm_nys_a3_fwd_sim2": (I, [P, P, P, P, I, I, P, P, P, P]),
     "tm_nys_a1_fwd": (I, [I, P, P, P, P, P, I, I, I, P, P, P]),
     "tm_nys_rowdot_cast": (I, [I, P, P, I, P, P, P]),
     "tm_cast_f32": (I, [I, P, P, L, P]),

@@ -112,12 +112,64 @@ __global__ __launch_bounds__(256) void landmarks_kernel(const T* __restrict__ q,
 // a2s (optional): the same values as bf16 hi / lo planes (hi = bf16(a), lo = bf16(a - hi); lo plane at
 // a2s + nbh * 256 * 256), the operand format of the split pseudo-inverse chain (pinv_split.hip).
 constexpr int S2_ROWS = 8, S2_KT = NL + 4;
+
+// A2 rows o0 / NL .. + ROWS - 1 by one 256-thread group (thread j = column j), shared by
+// sim2_softmax_kernel and the fused A3 forward (a3_fwd_v2_kernel<.., S2R>): kt = k~^T [64][S2_KT]
+// and qs = the group's q~ rows [ROWS][64] in LDS, red = [4][ROWS] LDS scratch.  Every thread of the
+// workgroup calls it (its barriers are workgroup-wide); the arithmetic of a row does not depend on
+// ROWS, so both callers write the same bits.
+template <int ROWS>
+TM_DEV void sim2_rows(const float* kt, const float* qs, float* red, int j, float* __restrict__ a2,
+                      bf16* __restrict__ a2s, size_t o0, size_t plane) {
+  const int lane = j & 63, wave = j >> 6;
+  float s[ROWS];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) s[r] = 0.f;
+#pragma unroll 8
+  for (int c = 0; c < DH; ++c) {
+    const float kv = kt[c * S2_KT + j];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) s[r] = fmaf(qs[r * DH + c], kv, s[r]);
+  }
+  // row max
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    const float m = wave_max(s[r]);
+    if (lane == 0) red[wave * ROWS + r] = m;
+  }
+  __syncthreads();
+  float mx[ROWS];
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r)
+    mx[r] = fmaxf(fmaxf(red[0 * ROWS + r], red[1 * ROWS + r]), fmaxf(red[2 * ROWS + r], red[3 * ROWS + r]));
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    s[r] = __expf(s[r] - mx[r]);
+    const float t = wave_sum(s[r]);
+    if (lane == 0) red[wave * ROWS + r] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    const float tot = (red[0 * ROWS + r] + red[1 * ROWS + r]) + (red[2 * ROWS + r] + red[3 * ROWS + r]);
+    const size_t o = o0 + (size_t)r * NL + j;
+    const float v = s[r] / tot;
+    a2[o] = v;
+    if (a2s) {
+      const bf16 hi = (bf16)v;
+      a2s[o] = hi;
+      a2s[o + plane] = (bf16)(v - (float)hi);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restrict__ ql, const float* __restrict__ kl,
                                                            float* __restrict__ a2, bf16* __restrict__ a2s) {
-  const int bh = blockIdx.x, i0 = blockIdx.y * S2_ROWS, j = threadIdx.x, lane = j & 63, wave = j >> 6;
+  const int bh = blockIdx.x, i0 = blockIdx.y * S2_ROWS, j = threadIdx.x;
   __shared__ float kt[DH * S2_KT];   // k~^T
-  __shared__ float qs[S2_ROWS][DH];
-  __shared__ float red[4][S2_ROWS];
+  __shared__ float qs[S2_ROWS * DH];
+  __shared__ float red[4 * S2_ROWS];
   {
     // the q~ rows go out with the k~ loads (one memory round trip before the LDS writes)
     static_assert(S2_ROWS * DH % 256 == 0, "sim2: q~ rows per thread");
@@ -130,7 +182,7 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
 #pragma unroll
     for (int u = 0; u < 16; ++u) v[u] = *(const f32x4*)(kb + (size_t)(u * 256 + j) * 4);  // piece p: row p/16, d 4 (p%16)
 #pragma unroll
-    for (int u = 0; u < QE; ++u) qs[(u * 256 + j) / DH][(u * 256 + j) % DH] = qv[u];
+    for (int u = 0; u < QE; ++u) qs[u * 256 + j] = qv[u];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int p = u * 256 + j, row = p >> 4, d0 = (p & 15) * 4;
@@ -139,45 +191,7 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
     }
   }
   __syncthreads();
-  float s[S2_ROWS];
-#pragma unroll
-  for (int r = 0; r < S2_ROWS; ++r) s[r] = 0.f;
-#pragma unroll 8
-  for (int c = 0; c < DH; ++c) {
-    const float kv = kt[c * S2_KT + j];
-#pragma unroll
-    for (int r = 0; r < S2_ROWS; ++r) s[r] = fmaf(qs[r][c], kv, s[r]);
-  }
-  // row max
-#pragma unroll
-  for (int r = 0; r < S2_ROWS; ++r) {
-    const float m = wave_max(s[r]);
-    if (lane == 0) red[wave][r] = m;
-  }
-  __syncthreads();
-  float mx[S2_ROWS];
-#pragma unroll
-  for (int r = 0; r < S2_ROWS; ++r) mx[r] = fmaxf(fmaxf(red[0][r], red[1][r]), fmaxf(red[2][r], red[3][r]));
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < S2_ROWS; ++r) {
-    s[r] = __expf(s[r] - mx[r]);
-    const float t = wave_sum(s[r]);
-    if (lane == 0) red[wave][r] = t;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < S2_ROWS; ++r) {
-    const float tot = (red[0][r] + red[1][r]) + (red[2][r] + red[3][r]);
-    const size_t o = ((size_t)bh * NL + i0 + r) * NL + j;
-    const float v = s[r] / tot;
-    a2[o] = v;
-    if (a2s) {
-      const bf16 hi = (bf16)v;
-      a2s[o] = hi;
-      a2s[o + (size_t)gridDim.x * NL * NL] = (bf16)(v - (float)hi);
-    }
-  }
+  sim2_rows<S2_ROWS>(kt, qs, red, j, a2, a2s, ((size_t)bh * NL + i0) * NL, (size_t)gridDim.x * NL * NL);
 }
 
 // bench-mode A2 = softmax_j(ql_i . kl_j) on the MFMA: the logits as bf16x3 products (x = hi + lo,
@@ -298,6 +312,7 @@ template <> TM_DEV f32x8 value_frag<float>(const float* vt, int dt, int kb, int 
   const f32x4 lo = *(const f32x4*)row, hi = *(const f32x4*)(row + 8);
   return (f32x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
+
 
 // ---------------------------------------------------------------------------
 // Shared forward block: one wave, 32 queries (B-operand fragments qf), 256 keys in
@@ -870,11 +885,16 @@ constexpr int A3V_PIECES = (A3V_KEYS * 8 + 511) / 512;             // 16-B piece
 // partials per head of the v2 kernel
 inline int a3v_splits(int nbh, int n) { return std::max(1, std::min(n / 32, 256 / std::max(nbh, 1))); }
 
-template <int ST = 0>   // ST: diagnostic s_memtime stamps (g_a1_stamps)
+// S2R > 0: the workgroup also writes A2 = softmax(q~ k~^T) rows p * 2 S2R .. + 2 S2R - 1 of its head
+// (sim2_rows, two 256-thread groups of S2R rows; host-checked 2 S2R P == 256) before its first key
+// chunk is staged: the k~ / q~ loads go out ahead of the chunk's, so the rows are computed while the
+// chunk is in flight, and the separate sim2 launch disappears from the step.
+struct Sim2Out { const float* kl; float* a2; bf16* a2s; };
+template <int ST = 0, int S2R = 0>   // ST: diagnostic s_memtime stamps (g_a1_stamps)
 __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict__ ql, const bf16* __restrict__ k,
                                                         const bf16* __restrict__ v, int n, int P,
                                                         float* __restrict__ part_o, float* __restrict__ part_m,
-                                                        float* __restrict__ part_l) {
+                                                        float* __restrict__ part_l, Sim2Out s2) {
   constexpr int KROW = Lay<bf16>::KROW, VROW = Lay<bf16>::VROW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int p = blockIdx.x, bh = blockIdx.y, nbh = gridDim.y;
@@ -911,11 +931,40 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
       }
     }
   };
+  // fused A2 rows: k~ of the head (16-B pieces, p = u 512 + tid: row p / 16, d 4 (p % 16)) and the
+  // group's q~ rows requested first
+  constexpr int S2Q = S2R > 0 ? S2R * DH / 256 : 1;
+  f32x4 k2[S2R > 0 ? 8 : 1];
+  float q2[S2Q];
+  const int g2 = tid >> 8, j2 = tid & 255, r2 = p * 2 * S2R + g2 * S2R;
+  if constexpr (S2R > 0) {
+    const float* kb = s2.kl + (size_t)bh * NL * DH;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) k2[u] = *(const f32x4*)(kb + (size_t)(u * 512 + tid) * 4);
+#pragma unroll
+    for (int u = 0; u < S2Q; ++u) q2[u] = ql[((size_t)bh * NL + r2) * DH + u * 256 + j2];
+  }
   fetch(sb0);
   bf16x8 qf[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st) qf[st] = cvt8<bf16>(ql + ((size_t)bh * NL + qi) * DH + st * 16 + 8 * h);
   stamp(1);
+  if constexpr (S2R > 0) {
+    float* kt = (float*)smem;                          // k~^T [64][S2_KT]; the chunk buffers come after
+    float* qs = kt + DH * S2_KT + g2 * S2R * DH;
+    float* red = kt + DH * S2_KT + 2 * S2R * DH + g2 * 4 * S2R;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int pc = u * 512 + tid, row = pc >> 4, d0 = (pc & 15) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kt[(d0 + e) * S2_KT + row] = k2[u][e];
+    }
+#pragma unroll
+    for (int u = 0; u < S2Q; ++u) qs[u * 256 + j2] = q2[u];
+    __syncthreads();
+    sim2_rows<S2R>(kt, qs, red, j2, s2.a2, s2.a2s, ((size_t)bh * NL + r2) * NL, (size_t)nbh * NL * NL);
+    __syncthreads();   // the LDS goes to the key chunks
+  }
   stage(sb0, 0);
   __syncthreads();
   stamp(2);
@@ -2101,28 +2150,52 @@ extern "C" long long tm_nys_a3_workspace(int nbh, int n) {
   return parts * nbh * NL * (DH + 2) * (long long)sizeof(float);
 }
 
+namespace {
+// the bf16 key-split launch (+ the fused A2 rows when s2.a2 is set and the split allows it)
+void launch_a3_fwd_v2(const float* ql, const void* k, const void* v, int nbh, int n, float* work, Sim2Out s2,
+                      hipStream_t st) {
+  const int P = a3v_splits(nbh, n);
+  float* po = work;
+  float* pm = po + (size_t)P * nbh * NL * DH;
+  float* pl = pm + (size_t)P * nbh * NL;
+  const dim3 grid(P, nbh);
+  const bf16* kb = (const bf16*)k;
+  const bf16* vb = (const bf16*)v;
+#ifdef TM_DIAG
+  if (NYS_VARIANT == 32 && !s2.a2) {   // diagnostic: s_memtime stamps per wave (tm_debug_a1_stamps)
+    tm_allow_smem(a3_fwd_v2_kernel<1>, A3V_BYTES);
+    a3_fwd_v2_kernel<1><<<grid, 512, A3V_BYTES, st>>>(ql, kb, vb, n, P, po, pm, pl, s2);
+    return;
+  }
+#endif
+  if (s2.a2 && P * 8 == NL) {
+    tm_allow_smem(a3_fwd_v2_kernel<0, 4>, A3V_BYTES);
+    a3_fwd_v2_kernel<0, 4><<<grid, 512, A3V_BYTES, st>>>(ql, kb, vb, n, P, po, pm, pl, s2);
+  } else if (s2.a2 && P * 16 == NL) {
+    tm_allow_smem(a3_fwd_v2_kernel<0, 8>, A3V_BYTES);
+    a3_fwd_v2_kernel<0, 8><<<grid, 512, A3V_BYTES, st>>>(ql, kb, vb, n, P, po, pm, pl, s2);
+  } else {
+    tm_allow_smem(a3_fwd_v2_kernel<0>, A3V_BYTES);
+    a3_fwd_v2_kernel<0><<<grid, 512, A3V_BYTES, st>>>(ql, kb, vb, n, P, po, pm, pl, s2);
+    if (s2.a2)   // a split the fused rows do not tile: the separate launch
+      sim2_softmax_kernel<<<dim3(nbh, NL / S2_ROWS), 256, 0, st>>>(ql, s2.kl, s2.a2, s2.a2s);
+  }
+}
+}  // namespace
+
 extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const void* v, int nbh, int n, float* work,
                              float* w, float* lse3, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0, "a3_fwd: n must be a positive multiple of 256");
   TM_REQUIRE((w && lse3) || dtype == TM_BF16, "a3_fwd: w / lse3 may be null (deferred combine) in bf16 mode only");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TM_BF16) {
+    launch_a3_fwd_v2(ql, k, v, nbh, n, work, Sim2Out{nullptr, nullptr, nullptr}, st);
+    TM_CHECK_LAUNCH();
+    if (!w) return 0;   // deferred: the combine runs in the pseudo-inverse chain (tm_pinv_fwd_split_a3)
     const int P = a3v_splits(nbh, n);
     float* po = work;
     float* pm = po + (size_t)P * nbh * NL * DH;
     float* pl = pm + (size_t)P * nbh * NL;
-#ifdef TM_DIAG
-    if (NYS_VARIANT == 32) {   // diagnostic: s_memtime stamps per wave (tm_debug_a1_stamps)
-      tm_allow_smem(a3_fwd_v2_kernel<1>, A3V_BYTES);
-      a3_fwd_v2_kernel<1><<<dim3(P, nbh), 512, A3V_BYTES, st>>>(ql, (const bf16*)k, (const bf16*)v, n, P, po, pm, pl);
-    } else
-#endif
-    {
-      tm_allow_smem(a3_fwd_v2_kernel<0>, A3V_BYTES);
-      a3_fwd_v2_kernel<0><<<dim3(P, nbh), 512, A3V_BYTES, st>>>(ql, (const bf16*)k, (const bf16*)v, n, P, po, pm, pl);
-    }
-    TM_CHECK_LAUNCH();
-    if (!w) return 0;   // deferred: the combine runs in the pseudo-inverse chain (tm_pinv_fwd_split_a3)
     a3_combine_v2_kernel<<<dim3(nbh, NL / 8), 256, 0, st>>>(A3Combine{po, pm, pl, P, nbh, w, lse3});
     TM_CHECK_LAUNCH();
     return 0;
@@ -2138,6 +2211,15 @@ extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const vo
   }));
   TM_CHECK_LAUNCH();
   a3_combine_kernel<<<dim3(nbh, NL / 16), 256, 0, st>>>(po, pm, pl, nkb, nbh, w, lse3);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_nys_a3_fwd_sim2(const float* ql, const float* kl, const void* k, const void* v, int nbh, int n,
+                                  float* work, float* a2, void* a2s, void* stream) {
+  TM_REQUIRE(n > 0 && n % NL == 0, "a3_fwd_sim2: n must be a positive multiple of 256");
+  TM_REQUIRE(ql && kl && k && v && work && a2 && a2s, "a3_fwd_sim2: null operand");
+  launch_a3_fwd_v2(ql, k, v, nbh, n, work, Sim2Out{kl, a2, (bf16*)a2s}, (hipStream_t)stream);
   TM_CHECK_LAUNCH();
   return 0;
 }

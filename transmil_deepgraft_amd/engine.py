@@ -266,17 +266,19 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool, cls_r
     #  the step -- the chain's launches then wait for CUs -- so the path stays serial; in bench
     #  mode the partials' combine runs inside the chain's last launch, on the CUs it leaves idle)
     prec = 1 if dt_code == BF16 else 0
-    with probe("a3_fwd"):
-        if prec:
-            _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(None), _p(None), st)
-        else:
-            _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
     a2s = None
     if prec:
-        # bench mode: the pseudo-inverse chain on split bf16 hi/lo operands (pinv_split.hip)
+        # bench mode: the key-split A3 forward also writes A2 (+ its split bf16 hi/lo planes, the
+        # operands of the pseudo-inverse chain, pinv_split.hip); the partials' combine runs in the
+        # chain's last launch
         a2s = pool(nbh * NL * NL)   # hi + lo bf16 planes = one fp32 matrix's bytes
+        with probe("a3_fwd"):
+            _lib.call("tm_nys_a3_fwd_sim2", _p(ql), _p(kl), _p(k), _p(v), nbh, n, _p(work), _p(a2), _p(a2s), st)
+    else:
+        with probe("a3_fwd"):
+            _lib.call("tm_nys_a3_fwd", dt_code, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(w), _p(lse3), st)
+    if prec:
         saved = pool(_lib.query("tm_pinv_split_saved_floats", nbh, PINV_ITERS))
-        _lib.call("tm_nys_sim2_softmax_split", _p(ql), _p(kl), nbh, _p(a2), _p(a2s), st)
         with probe("pinv_fwd"):
             _lib.call("tm_pinv_fwd_split_a3", _p(a2), _p(a2s), nbh, PINV_ITERS, _p(saved), _p(work),
                       _lib.query("tm_nys_a3_partials", nbh, n), _p(w), _p(lse3), st)
