@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void landmarks_kernel(const T* __restrict__ q,
 // the q~ rows are LDS broadcasts.
 // a2s (optional): the same values as bf16 hi / lo planes (hi = bf16(a), lo = bf16(a - hi); lo plane at
 // a2s + nbh * 256 * 256), the operand format of the split pseudo-inverse chain (pinv_split.hip).
-constexpr int S2_ROWS = 8, S2_KT = NL + 4;
+constexpr int S2_ROWS = 8, S2_KT = NL + 1;   // k~^T rows of 257: the transposing writes spread over the banks
 
 // A2 rows o0 / NL .. + ROWS - 1 by one 256-thread group (thread j = column j), shared by
 // sim2_softmax_kernel and the fused A3 forward (a3_fwd_v2_kernel<.., S2R>): kt = k~^T [64][S2_KT]
@@ -125,11 +125,18 @@ TM_DEV void sim2_rows(const float* kt, const float* qs, float* red, int j, float
   float s[ROWS];
 #pragma unroll
   for (int r = 0; r < ROWS; ++r) s[r] = 0.f;
-#pragma unroll 8
-  for (int c = 0; c < DH; ++c) {
-    const float kv = kt[c * S2_KT + j];
+#pragma unroll 2
+  for (int c = 0; c < DH; c += 4) {   // the q~ values as 16-B broadcasts; FMA order over c unchanged
+    const float kv0 = kt[c * S2_KT + j], kv1 = kt[(c + 1) * S2_KT + j];
+    const float kv2 = kt[(c + 2) * S2_KT + j], kv3 = kt[(c + 3) * S2_KT + j];
 #pragma unroll
-    for (int r = 0; r < ROWS; ++r) s[r] = fmaf(qs[r * DH + c], kv, s[r]);
+    for (int r = 0; r < ROWS; ++r) {
+      const f32x4 q4 = *(const f32x4*)(qs + r * DH + c);
+      s[r] = fmaf(q4[0], kv0, s[r]);
+      s[r] = fmaf(q4[1], kv1, s[r]);
+      s[r] = fmaf(q4[2], kv2, s[r]);
+      s[r] = fmaf(q4[3], kv3, s[r]);
+    }
   }
   // row max
 #pragma unroll
@@ -168,7 +175,7 @@ __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restri
                                                            float* __restrict__ a2, bf16* __restrict__ a2s) {
   const int bh = blockIdx.x, i0 = blockIdx.y * S2_ROWS, j = threadIdx.x;
   __shared__ float kt[DH * S2_KT];   // k~^T
-  __shared__ float qs[S2_ROWS * DH];
+  __shared__ __attribute__((aligned(16))) float qs[S2_ROWS * DH];
   __shared__ float red[4 * S2_ROWS];
   {
     // the q~ rows go out with the k~ loads (one memory round trip before the LDS writes)
