@@ -7,7 +7,7 @@ chain (the bench `roofline` kernel): FETCH_SIZE doubled for the gfx950 half-coun
 reads (MI355X_MICROARCH.md, HBM) + WRITE_SIZE, per dispatch, mean over the run's dispatches.
 Sites with two layers on one kernel are split by dispatch order (forward: layer 1 then 2;
 backward: 2 then 1); the pinv forward chain is the 14 pinv_stage dispatches after each
-sim2_softmax dispatch.  Algorithmic bytes from bench.hbm_model / bench.roofline_model.
+A3 forward dispatch (which also writes A2, the chain's input).  Algorithmic bytes from bench.hbm_model / bench.roofline_model.
 """
 import argparse
 import csv
@@ -80,7 +80,7 @@ def main():
             if (site, layer) not in model:
                 continue
             kname, byts = model[(site, layer)]
-            pats = {"ln_fwd": [r"^ln_fwd_kernel"], "landmarks": [r"^landmarks_kernel"],
+            pats = {"ln_fwd": [r"ln_fwd_kernel"], "landmarks": [r"landmarks_kernel"],
                     "a3_fwd": [r"^a3_fwd_v2_kernel"], "a1_fwd": [r"^a1_fwd_bf16_kernel"],
                     "ppeg_fwd": [r"^ppeg_stencil_kernel<false>"],
                     "ppeg_bwd": [r"^ppeg_stencil_kernel<true>", r"^ppeg_wgrad_kernel", r"^ppeg_wgrad_reduce_kernel"],
@@ -88,11 +88,11 @@ def main():
             key = site if len(layers) == 1 else f"{site}:{layer}"
             put(key, pats, layer_of=k if len(layers) > 1 else None, nlayers=len(layers), algo=byts, kernel=kname)
 
-    # pinv forward chain: the 14 pinv_stage dispatches after each sim2_softmax dispatch
+    # pinv forward chain: the 14 pinv_stage dispatches after each A3 forward (+ A2 rows) dispatch
     def chains(rows):
         out, i = [], 0
         while i < len(rows):
-            if rows[i][1].startswith("sim2_softmax"):
+            if rows[i][1].startswith("a3_fwd_v2_kernel") or rows[i][1].startswith("sim2_softmax"):
                 seq = [b for _, k, b in rows[i + 1:i + 40] if k.startswith("pinv_stage_kernel")][:14]
                 if len(seq) == 14:
                     out.append(sum(seq))
