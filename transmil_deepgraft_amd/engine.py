@@ -152,7 +152,7 @@ def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c
 def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool):
     """out[M,N] (fp32) = sum_k dY[k, m] X[k, n]  (split-K, deterministic)."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
-    splits = max(1, min(16, 320 // max(tiles, 1), (K + 255) // 256))
+    splits = max(1, min(16, 256 // max(tiles, 1), (K + 255) // 256))   # <= one workgroup per CU
     if splits == 1:
         gemm(dY, X, out, M, N, K, lda=ldy, ldb=ldx, ldc=N, a_trans=1, b_kn=1, dtype=dtype, c_dtype=F32)
         return
