@@ -617,3 +617,22 @@ def test_bmm_rowdot_partials():
         prod = dw.double() * w.double()
         exp = torch.stack([prod[..., :32].sum(-1), prod[..., 32:].sum(-1)])
         assert torch.allclose(rd.double(), exp, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("rows,cols,ld,acc", [(8448, 512, 512, 0), (1000, 1024, 1536, 1), (300, 520, 520, 0),
+                                              (77, 512, 512, 1)])
+def test_colsum_bf16_matches_fp64(rows, cols, ld, acc):
+    """tm_colsum (the bias gradients' deterministic two-level column sum) against an fp64 sum of the
+    same bf16 values, with and without accumulate, ragged row chunks and a row stride > cols."""
+    from transmil_deepgraft_amd import _lib
+    from transmil_deepgraft_amd._lib import BF16
+    from transmil_deepgraft_amd.engine import _p, _stream
+    g = torch.Generator().manual_seed(rows + cols)
+    X = torch.randn(rows, ld, generator=g).to(torch.bfloat16).to("cuda")
+    out = torch.randn(cols, generator=g).to("cuda")
+    base = out.clone()
+    work = torch.empty(_lib.query("tm_colsum_workspace", rows, cols, 64) // 4 + 4, device="cuda")
+    _lib.call("tm_colsum", _p(X), BF16, rows, cols, ld, 64, _p(work), _p(out), acc, _stream())
+    torch.cuda.synchronize()
+    ref = X[:, :cols].double().sum(0).cpu() + (base.double().cpu() if acc else 0)
+    assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=1e-4)
