@@ -635,4 +635,4 @@ def test_colsum_bf16_matches_fp64(rows, cols, ld, acc):
     _lib.call("tm_colsum", _p(X), BF16, rows, cols, ld, 64, _p(work), _p(out), acc, _stream())
     torch.cuda.synchronize()
     ref = X[:, :cols].double().sum(0).cpu() + (base.double().cpu() if acc else 0)
-    assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=2e-3)   # fp32 sums of ~8 K terms of size ~1
