@@ -66,18 +66,25 @@ typedef struct tm_gemm_args {
 } tm_gemm_args;
 
 int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* args, void* stream);
+/* Deferred parameter-gradient reductions.  A tm_reduce_queue is a caller-owned host object
+ * (no device memory, no stream): every entry point below that ends in a split-K / slab sum takes
+ * `tm_reduce_queue* rq`.  rq == NULL launches the sum now on `stream`; otherwise the (slab, out)
+ * pair is only appended to *rq, and tm_reduce_flush(rq, stream) sums every queued pair in ONE
+ * launch (same fixed split order, so bit-identical to the immediate form).  The library keeps no
+ * deferral state of its own: two engines on two streams, or two threads, each pass their own
+ * queue.  A queue must not be used by two threads at once; nothing may read a queued output (or
+ * free its slab) before the flush.  A full queue (48 entries) is flushed on the appending call's
+ * stream.  Replaces the DDP-reducer-era fixed-bucket gradient pass (code/train.py:184). */
+typedef struct tm_reduce_queue tm_reduce_queue;
+tm_reduce_queue* tm_reduce_queue_create(void);          /* NULL + tm_last_error() on failure */
+void tm_reduce_queue_destroy(tm_reduce_queue* rq);      /* entries still queued are dropped */
+int tm_reduce_queue_pending(const tm_reduce_queue* rq); /* queued entries, -1 if rq is invalid */
+int tm_reduce_flush(tm_reduce_queue* rq, void* stream);
 int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
-                     int accumulate, void* stream);
-/* Deferred parameter-gradient reductions: while deferral is on, tm_splitk_reduce (and the
- * reductions inside tm_colsum / tm_layernorm_bwd / tm_nys_conv_bwd) only queue their
- * (slab, out) pairs; tm_reduce_flush sums every queued pair in ONE launch on `stream`.  The
- * queue is per process (one engine per process); nothing may read a queued output before the
- * flush. */
-int tm_reduce_defer(int on);
-int tm_reduce_flush(void* stream);
+                     int accumulate, tm_reduce_queue* rq, void* stream);
 long long tm_colsum_workspace(int rows, int cols, int rows_per_chunk);
 int tm_colsum(const void* X, int dtype, int rows, int cols, int ld, int rows_per_chunk,
-              float* work, float* out, int accumulate, void* stream);
+              float* work, float* out, int accumulate, tm_reduce_queue* rq, void* stream);
 
 /* ---- LayerNorm / head (layernorm.hip) ----------------------------------
  * TransLayer.norm (code/models/TransMIL.py:23,47) and the final norm + _fc
@@ -91,7 +98,8 @@ long long tm_layernorm_bwd_workspace(int rows, int D, int rows_per_block);
  * the other rows are written (=) without being read (the last layer's dL/dH, clsrow.hip) */
 int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const float* gamma, const float* mean,
                      const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
-                     int resid_cls_only, float* dx_accum, float* work, float* dgamma, float* dbeta, void* stream);
+                     int resid_cls_only, float* dx_accum, float* work, float* dgamma, float* dbeta,
+                     tm_reduce_queue* rq, void* stream);
 int tm_head_fwd(const float* h, int B, int S, int D, const float* gamma, const float* beta, float eps,
                 const float* W, const float* bias, int C, float* logits, float* xhat, float* rstd,
                 void* stream);
@@ -140,17 +148,19 @@ int tm_nys_rowdot_cast(int dtype, const float* dw, const float* w, int rows, flo
 int tm_cast_f32(int dtype, const float* x, void* y, long long count, void* stream);
 long long tm_nys_conv_bwd_workspace(int nbags, int nh, int n);
 int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merged, const void* v, const float* wconv,
-                    int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv, void* stream);
+                    int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv,
+                    tm_reduce_queue* rq, void* stream);
 long long tm_nys_a1_bwd_workspace(int nbh, int n, int queries_per_wg);
 int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t,
                   const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
-                  float* dq, float* work, float* dkl, float* dy, int accumulate, void* stream);
+                  float* dq, float* work, float* dkl, float* dy, int accumulate, tm_reduce_queue* rq,
+                  void* stream);
 long long tm_nys_a3_bwd_workspace(int nbh, int n);
 /* d3 (here and in tm_nys_a3_bwd_fused): D = rowsum(dW o W) as [2][B*h][256] partials, the two
  * 32-column halves of dW (tm_bmm_job.Rd of the dW = Z^T dY product); the kernels sum them */
 int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
                   const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
-                  float* work, float* dql, int accumulate, void* stream);
+                  float* work, float* dql, int accumulate, tm_reduce_queue* rq, void* stream);
 /* Row `row` of the return_attn product attn1 Z attn3 (App. A eq. 11; read by
  * code/visualize_mil.py:580-581 as cls_attention[0,:,padding+1,...]) for every bag and
  * head, without the [n, n] matrix: out [B*h, n] fp32 from the forward's q, k (T, q
@@ -165,7 +175,8 @@ int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const flo
  * [dv_lo, dv_hi) (zero elsewhere; 0, n = dense); dq_row >= 0: dq is zero outside that row. */
 int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v, const float* lse3,
                         const float* d3, int nbh, int nh, int n, const float* dv_conv, int dv_lo, int dv_hi,
-                        const float* dkl, float* work, float* dql, void* dqkv, void* stream);
+                        const float* dkl, float* work, float* dql, void* dqkv, tm_reduce_queue* rq,
+                        void* stream);
 int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a, const float* dql_b, int nbags,
                       int nh, int n, float scale, void* dqkv, void* stream);
 
@@ -265,7 +276,8 @@ int tm_gather_rows(int dtype, const void* src, int F, const long long* i0, const
 int tm_put_cls(const float* cls, int B, int S, int D, float* H, void* stream);
 /* CrossEntropyLoss(logits, one_hot(label).float()) mean over B rows + softmax + argmax in one
  * launch (code/models/model_interface.py:339-347); backward dlogits = g[0] (prob - one_hot) / B.
- * label int64 [B] on the device, values in [0, C) (not checked on the device).  class_stats
+ * label int64 [B] on the device, values in [0, C); an out-of-range label makes the loss NaN and is
+ * left out of class_stats (no out-of-bounds access).  class_stats
  * (nullable, int32 [C][2]) accumulates per-class count / correct (:350-356). */
 int tm_ce_fwd(const float* logits, const long long* label, int B, int C, float* loss, float* prob,
               long long* yhat, int* class_stats, void* stream);

@@ -28,10 +28,10 @@ dkl = torch.randn(nbh, 256, 64, device=dev) * 0.01
 dqkv = torch.empty(1, n, 3 * 512, dtype=torch.bfloat16, device=dev)
 if os.environ.get("A3_FUSED", "1") == "1":   # the bench's form: bf16 k / v rows of dqkv straight from the kernel
     f = lambda: _lib.call("tm_nys_a3_bwd_fused", _p(ql), _p(dw), _p(k), _p(v), _p(lse), _p(d), nbh, 8, n, _p(dvc),
-                          0, n, _p(dkl), _p(work), _p(dql), _p(dqkv), _stream())
+                          0, n, _p(dkl), _p(work), _p(dql), _p(dqkv), None, _stream())
 else:
     f = lambda: _lib.call("tm_nys_a3_bwd", BF16, _p(ql), _p(dw), _p(k), _p(v), _p(lse), _p(d), nbh, 8, n, _p(dk),
-                          _p(dv), _p(work), _p(dql), 0, _stream())
+                          _p(dv), _p(work), _p(dql), 0, None, _stream())
 STV = int(os.environ.get("A3_STAMPS", "30"))   # 30: phases; 31: inside query chunk 2
 for var in (0, STV):
     _lib.lib().tm_debug_set_variant(1, var)

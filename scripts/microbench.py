@@ -232,14 +232,14 @@ def main():
                                                                      dtype=BF16, work_pool=pool), 2 * n * 1536 * 512)
         slab = torch.randn(8, 1536 * 512, device=dev)
         case("splitk_reduce 8 x 786K", lambda: _lib.call("tm_splitk_reduce", E._p(slab), E._p(dW), 8, 1536 * 512,
-                                                         C.c_float(1.0), 0, st()), byts=9 * 1536 * 512 * 4)
+                                                         C.c_float(1.0), 0, None, st()), byts=9 * 1536 * 512 * 4)
         slab2 = torch.randn(33, 512, device=dev)
         ob = torch.empty(512, device=dev)
         nf = torch.empty(n * 1536, device=dev)
     case("torch fill 52 MB fp32", lambda: nf.fill_(1.0), byts=n * 1536 * 4)
     case("torch copy 52 MB fp32", lambda: slabq.view(-1).copy_(nf), byts=2 * n * 1536 * 4)
     case("splitk_reduce 33 x 512", lambda: _lib.call("tm_splitk_reduce", E._p(slab2), E._p(ob), 33, 512,
-                                                         C.c_float(1.0), 0, st()))
+                                                         C.c_float(1.0), 0, None, st()))
     _lib.lib().tm_debug_set_variant(2, 0)
     tag[0] = ""
 
@@ -298,7 +298,7 @@ def main():
     cw = torch.empty(_lib.query("tm_nys_conv_bwd_workspace", 1, 8, n) // 4, device=dev)
     dwc = torch.empty(8, 33, device=dev)
     case("conv_bwd", lambda: _lib.call("tm_nys_conv_bwd", BF16, E._p(dmerged), E._p(merged), E._p(v), E._p(wconv),
-                                       nbh, 8, n, E._p(dv), E._p(d1), E._p(cw), E._p(dwc), st()),
+                                       nbh, 8, n, E._p(dv), E._p(d1), E._p(cw), E._p(dwc), None, st()),
          byts=4 * n * 512 * 2)
     dqf = torch.empty(nbh, n, 64, device=dev)
     a1w = torch.empty(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, 256) // 4, device=dev)
@@ -307,7 +307,7 @@ def main():
     lse1.uniform_(3, 4)
     case("a1_bwd (+2 reduces)", lambda: _lib.call("tm_nys_a1_bwd", BF16, E._p(q), E._p(dmerged), E._p(kl_t),
                                                   E._p(y_t), E._p(lse1), E._p(d1), nbh, 8, n, 256, E._p(dqf),
-                                                  E._p(a1w), E._p(dkl), E._p(dy), 0, st()), 10 * nbh * n * 256 * 64)
+                                                  E._p(a1w), E._p(dkl), E._p(dy), 0, None, st()), 10 * nbh * n * 256 * 64)
     a3bw = torch.empty(_lib.query("tm_nys_a3_bwd_workspace", nbh, n) // 4, device=dev)
     d3 = torch.randn(2, nbh, 256, device=dev)   # [2][nbh][256] partials
     dw_t = torch.randn(nbh, 256, 64, device=dev).to(bf)
@@ -316,7 +316,7 @@ def main():
     lse3.uniform_(8, 9)
     case("a3_bwd (+reduce)", lambda: _lib.call("tm_nys_a3_bwd", BF16, E._p(ql_t), E._p(dw_t), E._p(k), E._p(v),
                                                E._p(lse3), E._p(d3), nbh, 8, n, E._p(dk), E._p(dv), E._p(a3bw),
-                                               E._p(dql), 1, st()), 10 * nbh * n * 256 * 64)
+                                               E._p(dql), 1, None, st()), 10 * nbh * n * 256 * 64)
     zz = torch.randn(nbh, 256, 256, device=dev) * 1e-2
     arow = torch.empty(nbh, n, device=dev)
     case("attn_row (return_attn row)", lambda: _lib.call("tm_nys_attn_row", BF16, E._p(q), E._p(k), E._p(ql), E._p(kl),
@@ -337,7 +337,7 @@ def main():
 
         def a3():
             _lib.call("tm_nys_a3_bwd", BF16, E._p(ql_t), E._p(dw_t), E._p(k), E._p(v), E._p(lse3), E._p(d3), nbh, 8,
-                      n, E._p(dk), E._p(dv), E._p(a3bw), E._p(dql), 1, st())
+                      n, E._p(dk), E._p(dv), E._p(a3bw), E._p(dql), 1, None, st())
 
         def both():
             side.wait_stream(torch.cuda.current_stream())

@@ -3,7 +3,8 @@
 Launched twice by the test with RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the
 environment; both ranks share the one leased GPU, so the process group is gloo (RCCL refuses
 two ranks on one device; gloo all-reduces CUDA tensors through host staging).  Each rank runs
-the fused HIP TransMIL step (bf16 mode, train mode) on its own bags through
+the fused HIP TransMIL step (bf16 mode, train mode) on its own bags (argv[4] patches, default
+700; 8192 = BASELINE config C4's per-rank workload) through
 ``TransMILTask.optimization_step`` with ``GradAllReduce(model=..., overlap=True)``: the part-0
 all_reduce is issued by the fused backward's mid-backward ``ready(0)`` hook, and with
 ``accumulate_grad_batches = K`` only every K-th micro-batch reduces (Lightning's DDP no-sync,
@@ -29,13 +30,13 @@ def build_model():
     return TransMIL(2, 512, 512).cuda().train().set_compute_dtype(torch.bfloat16)
 
 
-def bag(rank, micro):
+def bag(rank, micro, n=N_PATCHES):
     g = torch.Generator(device="cuda").manual_seed(1000 * rank + micro)
-    x = torch.rand(1, N_PATCHES, 512, device="cuda", generator=g)
+    x = torch.rand(1, n, 512, device="cuda", generator=g)
     return x, torch.tensor([(rank + micro) % 2], device="cuda"), None   # (bags, labels, names)
 
 
-def main(out_path, k, steps):
+def main(out_path, k, steps, n=N_PATCHES):
     import torch.distributed as dist
     from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
     torch.cuda.set_device(0)
@@ -54,7 +55,7 @@ def main(out_path, k, steps):
     task = TransMILTask(model, accumulate_grad_batches=k)
     opt = task.configure_optimizers()[0][0]
     for micro in range(steps * k):
-        task.optimization_step(bag(rank, micro), opt, allreduce=ar)
+        task.optimization_step(bag(rank, micro, n), opt, allreduce=ar)
     torch.cuda.synchronize()
     owned = all(ar.bucket.owns(p) for p in model.parameters()) or all(p.grad is None for p in model.parameters())
     torch.save({"params": {n: p.detach().cpu() for n, p in model.named_parameters()},
@@ -64,4 +65,4 @@ def main(out_path, k, steps):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]))
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else N_PATCHES)

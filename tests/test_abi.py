@@ -91,3 +91,77 @@ def test_product_library_has_no_diagnostic_switches():
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True)
     if nm.returncode == 0:
         assert "tm_debug" not in nm.stdout
+
+
+def _prototypes():
+    """name -> parameter count of every prototype in the header (comments stripped)."""
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(tm_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_ctypes_arity_matches_header():
+    """Every ctypes argtypes list has exactly as many entries as the C prototype has parameters
+    (a signature change in the header without the binding would pass garbage for the stream)."""
+    from transmil_deepgraft_amd import _lib
+    protos = _prototypes()
+    bad = {n: (len(args), protos.get(n)) for n, (_, args) in _lib._SIGS.items() if protos.get(n) != len(args)}
+    assert not bad, bad
+
+
+def test_reduce_queue_is_caller_owned():
+    """The deferral queue is a caller-owned host object: two queues are independent, appending
+    needs no GPU (no launch happens until tm_reduce_flush), an invalid handle is refused, and the
+    reduction entry points take the queue explicitly (reentrant across streams)."""
+    import ctypes as C
+    from transmil_deepgraft_amd import _lib
+    lib = _lib.lib()
+    assert not hasattr(lib, "tm_reduce_defer")        # the old process-global switch is gone
+    qa, qb = C.c_void_p(lib.tm_reduce_queue_create()), C.c_void_p(lib.tm_reduce_queue_create())
+    assert qa.value and qb.value and qa.value != qb.value
+    try:
+        assert lib.tm_reduce_queue_pending(qa) == 0 and lib.tm_reduce_queue_pending(qb) == 0
+        slab, out = C.c_void_p(0x10000), C.c_void_p(0x20000)      # never dereferenced on the host
+        for i in range(3):
+            _lib.call("tm_splitk_reduce", slab, out, 4, 1024, C.c_float(1.0), 0, qa, None)
+        _lib.call("tm_splitk_reduce", slab, out, 4, 0, C.c_float(1.0), 0, qb, None)   # empty: not queued
+        assert lib.tm_reduce_queue_pending(qa) == 3
+        assert lib.tm_reduce_queue_pending(qb) == 0
+        _lib.call("tm_reduce_flush", qb, None)              # nothing queued: no launch
+        with pytest.raises(RuntimeError, match="not a tm_reduce_queue"):
+            _lib.call("tm_reduce_flush", None, None)
+        assert lib.tm_reduce_queue_pending(None) == -1
+    finally:
+        lib.tm_reduce_queue_destroy(qa)
+        lib.tm_reduce_queue_destroy(qb)
+
+
+def test_engine_binds_one_queue_per_backward_call_and_thread():
+    """engine.reduce_scope binds a fresh queue per call on the calling thread only; the call
+    sites pass it only inside defer_reductions()."""
+    import threading
+    from transmil_deepgraft_amd import engine as E
+    assert E._rq().value is None
+    seen = {}
+
+    def worker(i):
+        with E.reduce_scope() as q:
+            with E.defer_reductions():
+                seen[i] = (q.handle.value, E._rq().value)
+            seen[(i, "after")] = E._rq().value
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    with E.reduce_scope() as outer:
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert E._rq().value is None                  # bound but not deferring here
+        with E.defer_reductions():
+            assert E._rq().value == outer.handle.value
+    assert seen[0][0] == seen[0][1] and seen[1][0] == seen[1][1]
+    assert seen[(0, "after")] is None and seen[(1, "after")] is None
+    assert E._rq().value is None

@@ -125,8 +125,8 @@ def test_rccl_allreduce_inside_captured_graph(overlap):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [1, 3])
-def test_two_ranks_average_through_the_hip_engine(k, tmp_path):
+@pytest.mark.parametrize("k,n", [(1, 700), (3, 700), (1, 8192)])
+def test_two_ranks_average_through_the_hip_engine(k, n, tmp_path):
     """Two processes on the one leased GPU (gloo: RCCL refuses two ranks on one device), each
     running the fused HIP TransMIL step (bf16 mode, train mode) on its own bags with
     ``GradAllReduce(model=..., overlap=True)`` and ``accumulate_grad_batches = k``
@@ -134,7 +134,8 @@ def test_two_ranks_average_through_the_hip_engine(k, tmp_path):
     :199).  After 2 optimizer steps both ranks hold the same parameters, equal (rtol 1e-5) to one
     process that accumulates both ranks' bags with loss / (2k) -- the gradient average DDP
     computes -- through the same kernels and optimizer, with the dropout stream replayed.  The
-    part-0 all_reduce is issued by the fused backward's ready() hook."""
+    part-0 all_reduce is issued by the fused backward's ready() hook.  n = 8192 is BASELINE config
+    C4's per-rank workload (C2: 2-class, N=8192x512, bf16, train mode, one slide per rank)."""
     import os
     import subprocess
     import sys
@@ -149,7 +150,7 @@ def test_two_ranks_average_through_the_hip_engine(k, tmp_path):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(here, "ddp_two_rank_worker.py"),
-                                       str(tmp_path / f"rank{r}.pt"), str(k), str(steps)],
+                                       str(tmp_path / f"rank{r}.pt"), str(k), str(steps), str(n)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     try:
@@ -177,7 +178,7 @@ def test_two_ranks_average_through_the_hip_engine(k, tmp_path):
         for micro in range(s * k, (s + 1) * k):
             for r in range(world):
                 model._dropout_counter.copy_(c0 + micro)     # each rank's stream at this micro-batch
-                task.backward(task.training_step(W.bag(r, micro)) / (world * k))
+                task.backward(task.training_step(W.bag(r, micro, n)) / (world * k))
         opt.step()
         opt.zero_grad(set_to_none=True)
     torch.cuda.synchronize()

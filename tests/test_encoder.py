@@ -102,3 +102,85 @@ def test_folded_weights_follow_parent_loads_and_inplace_edits():
         enc.bn1.running_mean.sub_(0.5)          # in place: back to the first statistics for bn1
         other.bn1.running_mean.sub_(0.5)
         torch.testing.assert_close(enc(x), other(x), rtol=1e-5, atol=1e-5)
+
+
+def test_encoder_oracle_pinned_by_reference_fixture():
+    """oracle/encoder_ref.py (functional ResNet-50, eval BN) reproduces the features the reference's
+    own ResNet.py computed for the fixture's 4 tiles (fp64: to rounding; fp32: 1e-5)."""
+    from oracle.encoder_ref import features
+    fx = load("retccl_r50_tiles4")
+    sd = _encoder().state_dict()
+    x = torch.from_numpy(encoder_tiles(4))
+    np.testing.assert_allclose(features(x, sd).numpy(), fx["feats.f64"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(features(x, sd, torch.float32).numpy(), fx["feats"], rtol=1e-5, atol=1e-5)
+
+
+C5_TILES = 4096     # BASELINE config C5: one slide of 4096 224x224 tiles
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("enc_dtype,mil_dtype,rtol,ltol,gtol", [
+    (torch.float32, torch.float32, 2e-3, 1e-4, 2e-3),       # parity mode end to end
+    (torch.bfloat16, torch.bfloat16, 6e-2, 5e-2, 6e-2),     # the bench mode (C2 bf16 tolerances)
+])
+def test_c5_full_bag_4096_tiles(enc_dtype, mil_dtype, rtol, ltol, gtol):
+    """Config C5 at its own size on one GPU (code/models/model_interface.py:237-247,297-316;
+    code/models/ResNet.py:130-277): a 4096-tile bag [1, 4096, 3, 224, 224] through ImageBagModel ->
+    RetCCL ResNet-50 (eval, BN folded) -> TransMIL(2, 2048) (RCC _fc1 branch).
+      * 16 tiles spread over the bag: encoder features against the fixture-pinned fp64 oracle
+        (oracle/encoder_ref.py), per-tile relative L2 error < rtol;
+      * the whole-bag features (the encoder's internal 512-tile chunks) bit-identical to running
+        the 8 chunks of 512 tiles one by one, and within rtol of one 4096-tile pass;
+      * TransMIL logits / every parameter gradient on the GPU-computed features against the fp64
+        TransMIL oracle on the same features (C2 tolerances for the mode);
+      * one train step of the image model (dropout on, Lookahead(RAdam)) finite and moving."""
+    from oracle.encoder_ref import features
+    from test_parity_gpu import _pair, _ref_forward_backward, _ours_forward_backward
+    from transmil_deepgraft_amd.encoder import ImageBagModel
+    from transmil_deepgraft_amd.interface import TransMILTask
+    torch.backends.cudnn.allow_tf32 = False
+    enc = _encoder(enc_dtype).cuda()
+    g = torch.Generator(device="cuda").manual_seed(4096)
+    tiles = torch.randn(1, C5_TILES, 3, 224, 224, device="cuda", generator=g)
+    with torch.no_grad():
+        whole = enc(tiles[0])
+        chunks = torch.cat([enc(tiles[0, s:s + 512]) for s in range(0, C5_TILES, 512)])
+        enc.chunk = C5_TILES
+        one_pass = enc(tiles[0])
+        enc.chunk = 512
+    torch.cuda.synchronize()
+    assert torch.isfinite(whole).all()
+    assert torch.equal(whole, chunks)
+    err1 = ((one_pass - whole).norm(dim=1) / whole.norm(dim=1)).max().item()
+    assert err1 < rtol, err1
+    idx = torch.linspace(0, C5_TILES - 1, 16).round().long()
+    ref = features(tiles[0, idx.cuda()].float().cpu(), enc.state_dict())
+    got = whole[idx.cuda()].double().cpu()
+    err = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert err < rtol, err
+
+    # TransMIL(2, 2048) on the GPU features against the fp64 oracle on the same features
+    refm, ours = _pair(2, feat=2048, dtype=mil_dtype)
+    feats = whole.view(1, C5_TILES, 2048).cpu()
+    lo, go = _ours_forward_backward(ours, feats, 1, 2)
+    lr, gr = _ref_forward_backward(refm, feats, 1, 2)
+    np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=ltol)
+    bad = [(n, e) for n, e in (((n, ((go[n].double() - g_).abs().max() / g_.abs().max().clamp_min(1e-12)).item())
+                                for n, g_ in gr.items())) if e > gtol]
+    assert not bad, bad
+
+    # one train step of the image model
+    ours.train().zero_grad(set_to_none=True)
+    model = ImageBagModel(enc, ours)
+    task = TransMILTask(ours)
+    opt = task.configure_optimizers()[0][0]
+    before = {n: p.detach().clone() for n, p in ours.named_parameters()}
+    logits = model(tiles)
+    loss = task.loss(logits, torch.nn.functional.one_hot(torch.tensor([1], device="cuda"), 2).float())
+    loss.backward()
+    opt.step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all() and loss.item() > 0
+    assert all(p.grad is None for p in enc.parameters())
+    moved = max((p.detach() - before[n]).abs().max().item() for n, p in ours.named_parameters())
+    assert 0 < moved < 1 and all(torch.isfinite(p).all() for p in ours.parameters())

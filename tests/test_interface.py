@@ -343,3 +343,80 @@ def test_head_fused_cross_entropy_matches_separate_launches(B, C, train):
     assert torch.equal(h1, h2) and torch.equal(s1, s2)
     for n in g2:
         torch.testing.assert_close(g1[n], g2[n], rtol=1e-5, atol=1e-7, msg=n)
+
+
+@pytest.mark.gpu
+def test_training_step_runs_hooks_on_the_model_and_the_task():
+    """A forward hook / pre-hook registered on the TransMIL module itself or on the task fires in
+    training_step (the fused forward_ce path steps aside for self(x)), with the same loss as the
+    unhooked fused step."""
+    from transmil_deepgraft_amd.models import TransMIL
+    from transmil_deepgraft_amd.interface import TransMILTask
+    torch.manual_seed(0)
+    model = TransMIL(2, 512, 512).cuda().set_compute_dtype(torch.float32).eval()
+    x = torch.rand(1, 200, 512, generator=torch.Generator().manual_seed(3)).cuda()
+    label = torch.tensor([1], device="cuda")
+    task = TransMILTask(model)
+    base = task.training_step((x, label, None)).detach().clone()
+    fired = []
+    for target in (model, task):
+        h1 = target.register_forward_hook(lambda m, i, o: fired.append(("fwd", type(m).__name__)))
+        h2 = target.register_forward_pre_hook(lambda m, i: fired.append(("pre", type(m).__name__)))
+        loss = task.training_step((x, label, None))
+        h1.remove()
+        h2.remove()
+        torch.testing.assert_close(loss.detach(), base, rtol=1e-6, atol=1e-6)
+    assert ("fwd", "TransMIL") in fired and ("pre", "TransMIL") in fired
+    assert ("fwd", "TransMILTask") in fired and ("pre", "TransMILTask") in fired
+
+
+@pytest.mark.gpu
+def test_out_of_range_label_never_indexes_out_of_bounds():
+    """F.one_hot raises on a label >= n_classes; the fused CE cannot raise on the device, so the
+    loss is NaN and the class statistics are untouched (no out-of-bounds write); a CPU label is
+    checked on the host and raises."""
+    from transmil_deepgraft_amd.models import TransMIL
+    torch.manual_seed(0)
+    model = TransMIL(2, 512, 512).cuda().set_compute_dtype(torch.float32).eval()
+    x = torch.rand(1, 100, 512).cuda()
+    stats = torch.zeros(2, 2, dtype=torch.int32, device="cuda")
+    with torch.no_grad():
+        _, loss, _, _ = model.forward_ce(x, torch.tensor([5], device="cuda"), stats)
+    assert torch.isnan(loss).item()
+    assert int(stats.abs().sum()) == 0
+    with pytest.raises(IndexError):
+        model.forward_ce(x, torch.tensor([2]), stats)
+
+
+def _unused_worker(rank, world, port, out):
+    """Rank 0 leaves parameter 1 without a gradient, rank 1 gives it one; parameter 2 is unused
+    on both ranks."""
+    import torch.distributed as dist
+    from transmil_deepgraft_amd.interface import GradAllReduce
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ps = [torch.nn.Parameter(torch.ones(5)) for _ in range(3)]
+    ar = GradAllReduce(ps)
+    ps[0].grad = torch.full((5,), float(rank + 1))
+    if rank == 1:
+        ps[1].grad = torch.full((5,), 4.0)
+    ar()
+    out[rank] = [None if p.grad is None else p.grad.clone() for p in ps]
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_param_unused_on_one_rank():
+    """DDP find_unused_parameters semantics (code/train.py:184): a parameter used on another rank
+    receives the averaged gradient on every rank (the optimizer steps stay identical); one unused
+    on every rank keeps grad None."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_unused_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    for r in range(2):
+        torch.testing.assert_close(res[r][0], torch.full((5,), 1.5))
+        torch.testing.assert_close(res[r][1], torch.full((5,), 2.0))
+        assert res[r][2] is None

@@ -490,7 +490,7 @@ def test_conv_bwd_bf16_mfma(nbags, n):
     work = torch.empty(L.query("tm_nys_conv_bwd_workspace", nbags, nh, n) // 4 + 16, device=DEV)
     dOd, Od, vd, wd = (t.to(DEV).contiguous() for t in (dO, O, v, wconv))
     L.call("tm_nys_conv_bwd", BF16, _p(dOd), _p(Od), _p(vd), _p(wd), nbh, nh, n, _p(dv), _p(d1), _p(work),
-           _p(dw), _stream())
+           _p(dw), None, _stream())
     torch.cuda.synchronize()
     assert torch.isfinite(dv).all() and torch.isfinite(d1).all() and torch.isfinite(dw).all()
     assert _rel(dv.cpu(), ref_dv) < 1e-5
@@ -562,7 +562,7 @@ def test_a3_bwd_bf16_even_split(nbh, n):
     assert torch.allclose(dparts.sum(0), d)
     lsed, dd = lse.float().to(DEV).contiguous(), dparts.float().to(DEV).contiguous()
     L.call("tm_nys_a3_bwd", BF16, _p(qd), _p(wd), _p(kd), _p(vd), _p(lsed), _p(dd), nbh, 8, n,
-           _p(dk), _p(dv), _p(work), _p(dql), 0, _stream())
+           _p(dk), _p(dv), _p(work), _p(dql), 0, None, _stream())
     torch.cuda.synchronize()
     assert torch.isfinite(dk).all() and torch.isfinite(dv).all() and torch.isfinite(dql).all()
     assert _rel(dk.cpu(), ref_dk) < 2e-2
@@ -632,7 +632,7 @@ def test_colsum_bf16_matches_fp64(rows, cols, ld, acc):
     out = torch.randn(cols, generator=g).to("cuda")
     base = out.clone()
     work = torch.empty(_lib.query("tm_colsum_workspace", rows, cols, 64) // 4 + 4, device="cuda")
-    _lib.call("tm_colsum", _p(X), BF16, rows, cols, ld, 64, _p(work), _p(out), acc, _stream())
+    _lib.call("tm_colsum", _p(X), BF16, rows, cols, ld, 64, _p(work), _p(out), acc, None, _stream())
     torch.cuda.synchronize()
     ref = X[:, :cols].double().sum(0).cpu() + (base.double().cpu() if acc else 0)
     assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=2e-3)   # fp32 sums of ~8 K terms of size ~1

@@ -67,12 +67,12 @@ _SIGS = {
     "tm_last_error": (C.c_char_p, []),
     "tm_build_info": (C.c_char_p, []),
     "tm_gemm": (I, [P, P, P, C.POINTER(GemmArgs), P]),
-    "tm_splitk_reduce": (I, [P, P, I, L, Fl, I, P]),
+    "tm_splitk_reduce": (I, [P, P, I, L, Fl, I, P, P]),
     "tm_colsum_workspace": (L, [I, I, I]),
-    "tm_colsum": (I, [P, I, I, I, I, I, P, P, I, P]),
+    "tm_colsum": (I, [P, I, I, I, I, I, P, P, I, P, P]),
     "tm_layernorm_fwd": (I, [P, P, P, Fl, I, I, I, I, I, I, P, P, P, P]),
     "tm_layernorm_bwd_workspace": (L, [I, I, I]),
-    "tm_layernorm_bwd": (I, [P, I, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P]),
+    "tm_layernorm_bwd": (I, [P, I, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P]),
     "tm_head_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P]),
     "tm_head_bwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "tm_head_ce_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P, P, P, P, P, P]),
@@ -88,13 +88,13 @@ _SIGS = {
     "tm_nys_rowdot_cast": (I, [I, P, P, I, P, P, P]),
     "tm_cast_f32": (I, [I, P, P, L, P]),
     "tm_nys_conv_bwd_workspace": (L, [I, I, I]),
-    "tm_nys_conv_bwd": (I, [I, P, P, P, P, I, I, I, P, P, P, P, P]),
+    "tm_nys_conv_bwd": (I, [I, P, P, P, P, I, I, I, P, P, P, P, P, P]),
     "tm_nys_a1_bwd_workspace": (L, [I, I, I]),
-    "tm_nys_a1_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P, P, P, P, I, P]),
+    "tm_nys_a1_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P, P, P, P, I, P, P]),
     "tm_nys_a3_bwd_workspace": (L, [I, I]),
-    "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, I, P]),
+    "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, I, P, P]),
     "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
-    "tm_nys_a3_bwd_fused": (I, [P, P, P, P, P, P, I, I, I, P, I, I, P, P, P, P, P]),
+    "tm_nys_a3_bwd_fused": (I, [P, P, P, P, P, P, I, I, I, P, I, I, P, P, P, P, P, P]),
     "tm_nys_assemble_q": (I, [I, P, I, P, P, I, I, I, Fl, P, P]),
     "tm_nys_attn_row": (I, [I, P, P, P, P, P, P, I, I, I, P, P]),
     "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
@@ -120,8 +120,10 @@ _SIGS = {
     "tm_attmil_bwd": (I, [P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P, P]),
     "tm_put_cls": (I, [P, I, I, I, P, P]),
     "tm_step_prepare": (I, [I, C.POINTER(CastTable), P, P, P, P, P, P, I, P, P, P, P, P, P, I, I, P]),
-    "tm_reduce_defer": (I, [I]),
-    "tm_reduce_flush": (I, [P]),
+    "tm_reduce_queue_create": (P, []),
+    "tm_reduce_queue_destroy": (None, [P]),
+    "tm_reduce_queue_pending": (I, [P]),
+    "tm_reduce_flush": (I, [P, P]),
     "tm_ce_fwd": (I, [P, P, I, I, P, P, P, P, P]),
     "tm_ce_bwd": (I, [P, P, I, I, P, P, P]),
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),

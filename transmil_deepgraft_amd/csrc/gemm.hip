@@ -21,6 +21,8 @@
 //     transposes anywhere.  (fp32 parity mode transposes on the LDS write.)
 // Split-K writes fp32 slabs that tm_splitk_reduce sums in a fixed order
 // (bitwise reproducible; no float atomics).
+#include <new>
+
 #include "common.h"
 #include "../../include/transmil_hip.h"
 
@@ -1414,10 +1416,13 @@ extern "C" int tm_debug_gemm_stamps(unsigned long long* host, int count) {
 }
 #endif
 
-// ---- deferred reductions: the parameter-gradient slab sums of a backward, queued while the
-// engine has deferral on and summed by ONE launch at tm_reduce_flush (a kernel boundary costs
-// ~4.5 us in graph replay on gfx950; a backward has ~15 such sums that nothing reads before the
-// optimizer).  Same fixed split order as splitk_reduce_kernel, so results are bit-identical.
+// ---- deferred reductions: the parameter-gradient slab sums of a backward, queued in a
+// CALLER-OWNED tm_reduce_queue and summed by ONE launch at tm_reduce_flush (a kernel boundary
+// costs ~4.5 us in graph replay on gfx950; a backward has ~15 such sums that nothing reads before
+// the optimizer).  Same fixed split order as splitk_reduce_kernel, so results are bit-identical.
+// The library keeps no deferral state of its own: every engine / thread / stream passes its own
+// queue (or NULL = launch now), so concurrent callers never see each other's entries.
+namespace {
 constexpr int DEFER_MAX = 48;
 struct ReduceEntry {
   const float* slab;
@@ -1437,8 +1442,17 @@ struct ReduceTable {
   int boff[DEFER_MAX + 1];        // prefix sums of the entries' workgroup counts (256 threads each)
   int n;
 };
-static ReduceTable g_defer{};
-static int g_defer_on = 0;
+static_assert(sizeof(ReduceTable) <= 4096, "multi_reduce_kernel's table must fit the kernel-argument segment");
+
+}  // namespace
+
+struct tm_reduce_queue {
+  unsigned magic;
+  ReduceTable t;
+};
+
+namespace {
+constexpr unsigned RQ_MAGIC = 0x52514D54u;   // "TMQR"
 
 // one thread = one 16-B unit (4 floats; entries whose count is not a multiple of 4 or whose
 // pointers are not 16-B aligned go element by element); every workgroup lies inside one entry
@@ -1486,41 +1500,62 @@ __global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
   if (r.accumulate) s += r.out[u];
   r.out[u] = s;
 }
+}  // namespace
 
-extern "C" int tm_reduce_defer(int on) {
-  g_defer_on = on;
-  return 0;
+extern "C" tm_reduce_queue* tm_reduce_queue_create(void) {
+  tm_reduce_queue* q = new (std::nothrow) tm_reduce_queue{};
+  if (!q) {
+    tm_set_error("reduce_queue_create: out of host memory");
+    return nullptr;
+  }
+  q->magic = RQ_MAGIC;
+  return q;
 }
 
-extern "C" int tm_reduce_flush(void* stream) {
-  if (g_defer.n == 0) return 0;
-  g_defer.boff[0] = 0;
-  for (int i = 0; i < g_defer.n; ++i)
-    g_defer.boff[i + 1] = g_defer.boff[i] + (int)((g_defer.off[i + 1] - g_defer.off[i] + 255) / 256);
-  multi_reduce_kernel<<<(unsigned)g_defer.boff[g_defer.n], 256, 0, (hipStream_t)stream>>>(g_defer);
-  g_defer.n = 0;
-  g_defer.off[0] = 0;
+extern "C" void tm_reduce_queue_destroy(tm_reduce_queue* q) {
+  if (q && q->magic == RQ_MAGIC) {
+    q->magic = 0;
+    delete q;
+  }
+}
+
+extern "C" int tm_reduce_queue_pending(const tm_reduce_queue* q) {
+  return (q && q->magic == RQ_MAGIC) ? q->t.n : -1;
+}
+
+extern "C" int tm_reduce_flush(tm_reduce_queue* q, void* stream) {
+  TM_REQUIRE(q && q->magic == RQ_MAGIC, "reduce_flush: not a tm_reduce_queue");
+  ReduceTable& t = q->t;
+  if (t.n == 0) return 0;
+  t.boff[0] = 0;
+  for (int i = 0; i < t.n; ++i)
+    t.boff[i + 1] = t.boff[i] + (int)((t.off[i + 1] - t.off[i] + 255) / 256);
+  multi_reduce_kernel<<<(unsigned)t.boff[t.n], 256, 0, (hipStream_t)stream>>>(t);
+  t.n = 0;
+  t.off[0] = 0;
   TM_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
-                                int accumulate, void* stream) {
+                                int accumulate, tm_reduce_queue* q, void* stream) {
   TM_REQUIRE(slab && out && splits >= 1 && count >= 0, "splitk_reduce: bad args");
+  TM_REQUIRE(!q || q->magic == RQ_MAGIC, "splitk_reduce: not a tm_reduce_queue");
   if (count == 0) return 0;
-  if (g_defer_on) {
-    if (g_defer.n == DEFER_MAX)
-      if (int rc = tm_reduce_flush(stream)) return rc;
+  if (q) {
+    ReduceTable& t = q->t;
+    if (t.n == DEFER_MAX)
+      if (int rc = tm_reduce_flush(q, stream)) return rc;
     const int vec = count % 4 == 0 && ((uintptr_t)slab % 16) == 0 && ((uintptr_t)out % 16) == 0;
     const long long units = vec ? count / 4 : count;
     // threads per unit: enough that each sums <= 2 bursts of 12 splits, while the entry keeps
     // to <= ~64 K threads
     int par = 1;
     while (par < 64 && (splits + par - 1) / par > 24 && units * par * 2 <= 65536) par <<= 1;
-    g_defer.e[g_defer.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha, vec, par};
+    t.e[t.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha, vec, par};
     // offsets count threads: par per 16-B unit (or element)
-    g_defer.off[g_defer.n + 1] = g_defer.off[g_defer.n] + units * par;
-    ++g_defer.n;
+    t.off[t.n + 1] = t.off[t.n] + units * par;
+    ++t.n;
     return 0;
   }
   hipStream_t st = (hipStream_t)stream;
@@ -1549,7 +1584,7 @@ extern "C" long long tm_colsum_workspace(int rows, int cols, int rows_per_chunk)
 
 // out[c] (+)= sum_r X[r, c]; deterministic two-level sum through `work`
 extern "C" int tm_colsum(const void* X, int dtype, int rows, int cols, int ld, int rows_per_chunk, float* work,
-                         float* out, int accumulate, void* stream) {
+                         float* out, int accumulate, tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(X && work && out && rows_per_chunk > 0, "colsum: bad args");
   const int nchunk = (rows + rows_per_chunk - 1) / rows_per_chunk;
   dim3 grid((cols + 63) / 64, nchunk);
@@ -1559,5 +1594,5 @@ extern "C" int tm_colsum(const void* X, int dtype, int rows, int cols, int ld, i
   else
     colsum_partial_kernel<float><<<grid, 256, 0, st>>>((const float*)X, rows, cols, ld, rows_per_chunk, work);
   TM_CHECK_LAUNCH();
-  return tm_splitk_reduce(work, out, nchunk, cols, 1.0f, accumulate, stream);
+  return tm_splitk_reduce(work, out, nchunk, cols, 1.0f, accumulate, rq, stream);
 }

@@ -212,7 +212,8 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const float* __restrict__ l
     for (int c = 0; c < C; ++c) s += expf(l[c] - m);
     const float inv = 1.f / s, lse = m + logf(s);
     for (int c = 0; c < C; ++c) prob[(size_t)b * C + c] = expf(l[c] - m) * inv;
-    acc += lse - l[label[b]];
+    const long long y = label[b];      // out of range: NaN loss, no out-of-bounds read
+    acc += (y >= 0 && y < C) ? lse - l[y] : __builtin_nanf("");
     yhat[b] = am;
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
@@ -224,7 +225,9 @@ __global__ void __launch_bounds__(256) ce_fwd_kernel(const float* __restrict__ l
     // the device instead of one host sync per step
     if (stats)
       for (int b = 0; b < B; ++b) {
-        const int y = (int)label[b];
+        const long long yl = label[b];
+        if (yl < 0 || yl >= C) continue;
+        const int y = (int)yl;
         stats[2 * y] += 1;
         stats[2 * y + 1] += yhat[b] == y;
       }

@@ -339,7 +339,10 @@ __global__ __launch_bounds__(64 * HEAD_CE_WAVES) void head_ce_fwd_kernel(
     for (int c = 0; c < C; ++c) s += expf(l[c] - m);
     const float inv = 1.f / s, lse = m + logf(s);
     for (int c = 0; c < C; ++c) prob[(size_t)b * C + c] = expf(l[c] - m) * inv;
-    acc += lse - l[label[b]];
+    // an out-of-range label (F.one_hot raises in the reference) poisons the loss with NaN instead
+    // of reading past the logits row
+    const long long y = label[b];
+    acc += (y >= 0 && y < C) ? lse - l[y] : __builtin_nanf("");
     yhat[b] = am;
   }
   acc = wave_sum(acc);
@@ -352,7 +355,9 @@ __global__ __launch_bounds__(64 * HEAD_CE_WAVES) void head_ce_fwd_kernel(
     loss[0] = t / (float)B;
     if (stats)
       for (int b = 0; b < B; ++b) {
-        const int yv = (int)label[b];
+        const long long y = label[b];
+        if (y < 0 || y >= C) continue;     // never index class_stats out of bounds
+        const int yv = (int)y;
         stats[2 * yv] += 1;
         stats[2 * yv + 1] += yhat[b] == yv;
       }
@@ -498,7 +503,7 @@ extern "C" long long tm_layernorm_bwd_workspace(int rows, int D, int rows_per_bl
 extern "C" int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const float* gamma, const float* mean,
                                 const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
                                 int resid_cls_only, float* dx_accum, float* work, float* dgamma, float* dbeta,
-                                void* stream) {
+                                tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(dy && x && gamma && mean && rstd && dx_accum && work && dgamma && dbeta, "layernorm_bwd: null arg");
   TM_REQUIRE(rows_per_block > 0 && S > 0, "layernorm_bwd: bad args");
   const int nb = (rows + rows_per_block - 1) / rows_per_block;
@@ -511,9 +516,9 @@ extern "C" int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const
                                                                       S, n_pad, pad, rows_per_block, resid_cls_only, dx_accum, work)));
   }
   TM_CHECK_LAUNCH();
-  int rc = tm_splitk_reduce(work, dgamma, nb, D, 1.0f, 0, stream);
+  int rc = tm_splitk_reduce(work, dgamma, nb, D, 1.0f, 0, rq, stream);
   if (rc) return rc;
-  return tm_splitk_reduce(work + (size_t)nb * D, dbeta, nb, D, 1.0f, 0, stream);
+  return tm_splitk_reduce(work + (size_t)nb * D, dbeta, nb, D, 1.0f, 0, rq, stream);
 }
 
 extern "C" int tm_head_fwd(const float* h, int B, int S, int D, const float* gamma, const float* beta, float eps,

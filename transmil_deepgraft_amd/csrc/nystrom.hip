@@ -2295,7 +2295,7 @@ extern "C" long long tm_nys_conv_bwd_workspace(int nbags, int nh, int n) {
 
 extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merged, const void* v, const float* wconv,
                                int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv,
-                               void* stream) {
+                               tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(nbh % nh == 0 && n > 0, "conv_bwd: bad shape");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TM_BF16 && NYS_VARIANT != 7) {
@@ -2304,13 +2304,13 @@ extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merge
     conv_bwd_mfma_kernel<<<dim3(nblk, nbh), 512, CbLay::BYTES, st>>>(
         (const bf16*)dmerged, (const bf16*)merged, (const bf16*)v, wconv, n, nh, r, dv, d1, work);
     TM_CHECK_LAUNCH();
-    return tm_splitk_reduce(work, dwconv, (nbh / nh) * nblk, (long long)nh * TAPS, 1.0f, 0, stream);
+    return tm_splitk_reduce(work, dwconv, (nbh / nh) * nblk, (long long)nh * TAPS, 1.0f, 0, rq, stream);
   }
   const int ntb = (n + 63) / 64;
   TM_DTYPE_DISPATCH(dtype, (conv_bwd_kernel<T><<<dim3(ntb, nbh), 256, 0, st>>>(
                                (const T*)dmerged, (const T*)merged, (const T*)v, wconv, n, nh, dv, d1, work)));
   TM_CHECK_LAUNCH();
-  return tm_splitk_reduce(work, dwconv, (nbh / nh) * ntb, (long long)nh * TAPS, 1.0f, 0, stream);
+  return tm_splitk_reduce(work, dwconv, (nbh / nh) * ntb, (long long)nh * TAPS, 1.0f, 0, rq, stream);
 }
 
 // A1 backward: keys = landmarks kl_t [bh][256][64], values = y_t, queries = q rows, dO = dmerged.
@@ -2331,7 +2331,8 @@ extern "C" long long tm_nys_a1_bwd_workspace(int nbh, int n, int queries_per_wg)
 
 extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t,
                              const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
-                             float* dq, float* work, float* dkl, float* dy, int accumulate, void* stream) {
+                             float* dq, float* work, float* dkl, float* dy, int accumulate, tm_reduce_queue* rq,
+                             void* stream) {
   TM_REQUIRE(queries_per_wg % 32 == 0 && n % queries_per_wg == 0, "a1_bwd: queries_per_wg must divide n, x32");
   const bool split = dtype == TM_BF16 && queries_per_wg <= NL && NYS_VARIANT != 3;
   const int nqc = split ? a1_bwd_split(nbh, n) : n / queries_per_wg;
@@ -2359,9 +2360,9 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
   }
   TM_CHECK_LAUNCH();
   const long long cnt = (long long)nbh * NL * DH;
-  int rc = tm_splitk_reduce(slab_k, dkl, nqc, cnt, 1.0f, accumulate, stream);
+  int rc = tm_splitk_reduce(slab_k, dkl, nqc, cnt, 1.0f, accumulate, rq, stream);
   if (rc) return rc;
-  return tm_splitk_reduce(slab_v, dy, nqc, cnt, 1.0f, 0, stream);
+  return tm_splitk_reduce(slab_v, dy, nqc, cnt, 1.0f, 0, rq, stream);
 }
 
 // A3 backward: keys = k rows, values = v rows, queries = ql_t (256 landmarks), dO = dw_t.
@@ -2413,7 +2414,7 @@ extern "C" long long tm_nys_a3_bwd_workspace(int nbh, int n) {
 
 extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, const void* k, const void* v,
                              const float* lse3, const float* d3, int nbh, int nh, int n, float* dk, float* dv,
-                             float* work, float* dql, int accumulate, void* stream) {
+                             float* work, float* dql, int accumulate, tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(n % NL == 0, "a3_bwd: n must be a multiple of 256");
   const int nkb = n / NL;
   BwdArgs a{};
@@ -2436,7 +2437,7 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
                               attn_bwd_kernel<T, MODE_A3><<<dim3(nkb, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
   }
   TM_CHECK_LAUNCH();
-  return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, accumulate, stream);
+  return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, accumulate, rq, stream);
 }
 
 // bf16 A3 backward with the fused key-side epilogue: the final k / v parts of dqkv from dK, dV,
@@ -2445,7 +2446,7 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
 extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v,
                                    const float* lse3, const float* d3, int nbh, int nh, int n, const float* dv_conv,
                                    int dv_lo, int dv_hi, const float* dkl, float* work, float* dql, void* dqkv,
-                                   void* stream) {
+                                   tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(n % NL == 0 && nbh % nh == 0, "a3_bwd_fused: n must be a multiple of 256");
   TM_REQUIRE(dv_conv && dkl && dqkv, "a3_bwd_fused: null operand");
   const int nkb = n / NL;
@@ -2465,7 +2466,7 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   int slabs = nkb;
   launch_a3_bwd_bf16(a, nbh, n, st, slabs);
   TM_CHECK_LAUNCH();
-  return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, 0, stream);
+  return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, 0, rq, stream);
 }
 
 extern "C" int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a, const float* dql_b,

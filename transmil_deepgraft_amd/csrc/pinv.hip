@@ -564,7 +564,7 @@ extern "C" int tm_pinv_bwd(const float* X, int nbh, int iters, int prec, const f
   // init: Z0 = X^T / (maxc * maxr)
   dot_partial_kernel<<<dim3(nbh, 16), 256, 0, st>>>(G, Zs, part);
   TM_CHECK_LAUNCH();
-  if (int rc = tm_splitk_reduce(part, gz, nbh * 16, 1, 1.0f, 0, stream)) return rc;
+  if (int rc = tm_splitk_reduce(part, gz, nbh * 16, 1, 1.0f, 0, nullptr, stream)) return rc;   // read below
   pinv_init_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, sums, G, gz, nbh, dX);
   TM_CHECK_LAUNCH();
   return 0;

@@ -169,14 +169,14 @@ def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool):
     g.mode = EPI_SPLITK
     g.alpha = 1.0
     _lib.call("tm_gemm", _p(dY), _p(X), _p(slab), C.byref(g), _stream())
-    _lib.call("tm_splitk_reduce", _p(slab), _p(out), splits, M * N, C.c_float(1.0), 0, _stream())
+    _lib.call("tm_splitk_reduce", _p(slab), _p(out), splits, M * N, C.c_float(1.0), 0, _rq(), _stream())
 
 
 def colsum(X, rows, cols, ld, dtype, out, work_pool, accumulate=False):
     rpc = 256
     nchunk = (rows + rpc - 1) // rpc
     work = work_pool(nchunk * cols)
-    _lib.call("tm_colsum", _p(X), dtype, rows, cols, ld, rpc, _p(work), _p(out), int(accumulate), _stream())
+    _lib.call("tm_colsum", _p(X), dtype, rows, cols, ld, rpc, _p(work), _p(out), int(accumulate), _rq(), _stream())
 
 
 def bmm_job(A, ta, B, tb, Cout, M, N, K, alpha=1.0, diag=0.0, E1=None, e1=0.0, E2=None, e2=0.0, Ct=None,
@@ -218,31 +218,94 @@ class Pool:
 
     def __call__(self, numel, dtype=torch.float32):
         t = torch.empty(int(numel), dtype=dtype, device=self.device)
-        if _DEFER[0]:
+        if getattr(_TLS, "deferring", False):
             self.hold.append(t)
         return t
 
 
-_DEFER = [False]
+class ReduceQueue:
+    """A caller-owned ``tm_reduce_queue`` (include/transmil_hip.h): the host-side list of
+    parameter-gradient slab sums a backward defers to one ``tm_reduce_flush`` launch.  The library
+    keeps no deferral state; each backward call owns one of these, so engines on different
+    threads / streams never share entries."""
+
+    def __init__(self):
+        h = _lib.lib().tm_reduce_queue_create()
+        if not h:
+            raise RuntimeError(f"tm_reduce_queue_create failed: {_lib.last_error()}")
+        self.handle = C.c_void_p(h)
+
+    def pending(self) -> int:
+        return int(_lib.lib().tm_reduce_queue_pending(self.handle))
+
+    def flush(self):
+        _lib.call("tm_reduce_flush", self.handle, _stream())
+
+    def close(self):
+        if self.handle is not None:
+            _lib.lib().tm_reduce_queue_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# per-thread binding of the queue the current backward call owns (reduce_scope) and whether the
+# call sites inside a ``defer_reductions`` block pass it (else NULL: reduce now)
+import threading as _threading  # noqa: E402
+_TLS = _threading.local()
+
+
+class reduce_scope:
+    """Bind a fresh ReduceQueue to this thread for one backward call; anything still queued at
+    exit is flushed on the current stream, then the queue is destroyed."""
+
+    def __enter__(self):
+        self.prev = getattr(_TLS, "queue", None)
+        self.q = ReduceQueue()
+        _TLS.queue = self.q
+        return self.q
+
+    def __exit__(self, *exc):
+        try:
+            if exc[0] is None and self.q.pending() > 0:
+                self.q.flush()
+        finally:
+            _TLS.queue = self.prev
+            self.q.close()
+        return False
+
+
+def _rq():
+    """The tm_reduce_queue* argument of a call site: the bound queue inside defer_reductions()."""
+    q = getattr(_TLS, "queue", None)
+    if q is not None and getattr(_TLS, "deferring", False):
+        return q.handle
+    return C.c_void_p(0)
 
 
 class defer_reductions:
-    """Queue the parameter-gradient slab sums issued inside the block (tm_reduce_defer); they
-    run as ONE launch at the next ``flush_reductions()``."""
+    """Queue the parameter-gradient slab sums issued inside the block in the thread's bound
+    ReduceQueue; they run as ONE launch at the next ``flush_reductions()``.  Outside a
+    ``reduce_scope`` the sums run immediately (nothing to defer into)."""
 
     def __enter__(self):
-        _lib.call("tm_reduce_defer", 1)
-        _DEFER[0] = True
+        self.prev = getattr(_TLS, "deferring", False)
+        _TLS.deferring = getattr(_TLS, "queue", None) is not None
         return self
 
     def __exit__(self, *exc):
-        _lib.call("tm_reduce_defer", 0)
-        _DEFER[0] = False
+        _TLS.deferring = self.prev
         return False
 
 
 def flush_reductions():
-    _lib.call("tm_reduce_flush", _stream())
+    q = getattr(_TLS, "queue", None)
+    if q is not None:
+        q.flush()
 
 
 # ----------------------------------------------------------------------------- NystromAttention core
@@ -340,14 +403,14 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         with defer_reductions(), probe("conv_bwd"):
             work = pool(_lib.query("tm_nys_conv_bwd_workspace", geo.B, nh, n) // 4)
             _lib.call("tm_nys_conv_bwd", dt_code, _p(dmerged), _p(merged), _p(v), _p(wconv), nbh, nh, n, _p(dv),
-                      _p(d1), _p(work), _p(dwconv_out), st)
+                      _p(d1), _p(work), _p(dwconv_out), _rq(), st)
         # A1 product backward: dq (complete), dkl, dY
         qpw = 256 if n % 256 == 0 else 32
         work = pool(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, qpw) // 4)
         with probe("a1_bwd"):
             with defer_reductions():     # its dk~ and dY slab sums as one launch
                 _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t),
-                          _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, st)
+                          _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, _rq(), st)
             flush_reductions()
     # Y = Z W
     dz = pool(mat).view(nbh, NL, NL)
@@ -376,7 +439,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         # A3 product backward: dk (=), dv (+=), dql3 (=)
         with probe("a3_bwd"):
             _lib.call("tm_nys_a3_bwd", dt_code, _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]),
-                      _p(d3), nbh, nh, n, _p(dk), _p(dv), _p(work3), _p(dql3), 0, st)
+                      _p(d3), nbh, nh, n, _p(dk), _p(dv), _p(work3), _p(dql3), 0, _rq(), st)
     # pseudo-inverse backward -> dA2, then softmax backward
     ds2 = pool(mat).view(nbh, NL, NL)
     if state["a2s"] is not None:
@@ -400,7 +463,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         with probe("a3_bwd"):
             lo, hi = (0, n) if cls_row is None else (max(cls_row - 16, 0), min(cls_row + 17, n))
             _lib.call("tm_nys_a3_bwd_fused", _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]), _p(d3),
-                      nbh, nh, n, _p(dv), lo, hi, _p(dkl), _p(work3), _p(dql3), _p(dqkv), st)
+                      nbh, nh, n, _p(dv), lo, hi, _p(dkl), _p(work3), _p(dql3), _p(dqkv), _rq(), st)
         _lib.call("tm_nys_assemble_q", dt_code, _p(dq), -1 if cls_row is None else cls_row, _p(dql), _p(dql3),
                   geo.B, nh, n, C.c_float(scale), _p(dqkv), st)
         return dqkv
@@ -484,7 +547,7 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
         _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
                   _p(saved["rstd"]), B * S, D, S, n, pad, rpb, int(saved["cls_only"]), _p(dH), _p(work),
                   _p(grads["norm_w"]),
-                  _p(grads["norm_b"]), st)
+                  _p(grads["norm_b"]), _rq(), st)
 
 
 # ----------------------------------------------------------------------------- whole model
@@ -691,7 +754,14 @@ class TransMILEngine:
         return logits, ctx
 
     def backward(self, dlogits, ctx, params, out=None, ready=None, gloss=None):
-        """Returns a dict name -> fp32 gradient with the reference parameter names.
+        """Returns a dict name -> fp32 gradient with the reference parameter names.  The deferred
+        parameter-gradient sums go into a ReduceQueue owned by this call (reentrant across
+        threads / streams)."""
+        with reduce_scope():
+            return self._backward(dlogits, ctx, params, out, ready, gloss)
+
+    def _backward(self, dlogits, ctx, params, out=None, ready=None, gloss=None):
+        """Body of ``backward``.
 
         ``gloss``: the gradient of the forward's fused loss (``ce``; a 0-d device tensor); then
         ``dlogits`` is the gradient reaching the logits from other uses, or None.
@@ -781,7 +851,7 @@ class TransMILEngine:
             work = pool(_lib.query("tm_layernorm_bwd_workspace", B * N, Fm, rpb) // 4)
             _lib.call("tm_layernorm_bwd", _p(dxln), F32, _p(inner["y0"]), _p(prm["ln0_w"]), _p(inner["mean0"]),
                       _p(inner["rstd0"]), B * N, Fm, N, N, 0, rpb, 0, _p(dy0), _p(work), _p(g[lnn + ".weight"]),
-                      _p(g[lnn + ".bias"]), st)
+                      _p(g[lnn + ".bias"]), _rq(), st)
             dpre0 = pool(B * N * Fm, self.tdtype).view(B * N, Fm)
             _lib.call("tm_gelu_bwd", self.dt_code, _p(dy0), _p(inner["pre0"]), B * N * Fm, _p(dpre0), st)
             weight_grad(dpre0, inner["xt"], g[w0n + ".weight"], Fm, Fin, B * N, ldy=Fm, ldx=Fin, dtype=self.dt_code,
@@ -835,6 +905,10 @@ class NystromEngine:
         return out, ctx
 
     def backward(self, dout, ctx):
+        with reduce_scope():
+            return self._backward(dout, ctx)
+
+    def _backward(self, dout, ctx):
         geo = ctx["geo"]
         B, S, D, n, pad = geo.B, geo.S, geo.D, geo.n, geo.pad
         pool = Pool(dout.device)

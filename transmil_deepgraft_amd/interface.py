@@ -357,8 +357,9 @@ class GradAllReduce:
     """Average gradients over ranks: the DDP gradient all-reduce on a ``GradBucket``.
 
     Replaces the Lightning DDP reducer (``strategy='ddp_find_unused_parameters_true'``,
-    code/train.py:184).  Every TransMIL parameter receives a gradient each step, so the
-    unused-parameter search is unnecessary.  With ``model=`` (a TransMIL with
+    code/train.py:184).  On the fused path every TransMIL parameter receives a gradient each step,
+    so no unused-parameter search runs; on the module-by-module path a has-gradient mask is
+    all-reduced first and parameters used on another rank adopt the averaged gradient.  With ``model=`` (a TransMIL with
     ``grad_bucket_parts``) the bucket has two parts: part 0 (head, norm, layer2, PPEG; 4.4 MB
     fp32) is final before layer1's backward is enqueued and, with ``overlap``, its RCCL
     all_reduce is issued right then on RCCL's stream, overlapping layer1 + _fc1 backward on
@@ -406,10 +407,18 @@ class GradAllReduce:
             self._works.clear()
             return
         owned = all(self.bucket.owns(p) for p in self.params if p.grad is not None)
+        adopt = []
         if not owned:
-            # gradients produced outside the fused backward (module-by-module path): bind them
+            # gradients produced outside the fused backward (module-by-module path): bind them.
+            # As DDP's find_unused_parameters: a parameter without a gradient HERE but with one on
+            # another rank receives the averaged gradient (its zeroed slice summed with theirs), so
+            # the ranks' optimizer steps stay identical; one used on no rank keeps grad None.
             self._works.clear()
+            local = [p.grad is not None for p in self.params]
             self.bucket.bind()
+            used = torch.tensor(local, dtype=torch.int32, device=self.flat.device)
+            dist.all_reduce(used, op=dist.ReduceOp.MAX, group=self.group)
+            adopt = [p for p, here, anywhere in zip(self.params, local, used.tolist()) if anywhere and not here]
         for i in range(len(self.bucket.ranges)):
             if i not in self._works:
                 self._works[i] = dist.all_reduce(self.bucket.part(i), op=dist.ReduceOp.SUM, group=self.group,
@@ -418,6 +427,8 @@ class GradAllReduce:
             self._works[i].wait()       # the compute stream waits on RCCL's stream
         self._works.clear()
         self.flat.mul_(1.0 / self._world())
+        for p in adopt:
+            p.grad = self.bucket.view(p)
 
 
 class _CrossEntropyOneHot(torch.autograd.Function):
@@ -488,6 +499,8 @@ class TransMILTask(nn.Module):
             if self.class_stats is None or self.class_stats.device != x.device:
                 self.class_stats = torch.zeros(self.n_classes, 2, dtype=torch.int32, device=x.device)
             fused = getattr(self.model, "forward_ce", None)
+            if self._forward_hooks or self._forward_pre_hooks:
+                fused = None            # hooks on the task run only through self(x)
             out = fused(x, label, self.class_stats) if fused is not None else None
             if out is not None:
                 logits, loss, y_prob, y_hat = out

@@ -274,10 +274,13 @@ class TransMIL(nn.Module):
             raise RuntimeError("TransMIL (HIP) needs a GPU tensor: there is no CPU path")
         layout = self._fc1_layout()
         x = x.float().contiguous()
-        if not self.fused or self._hooked() or x.requires_grad:
+        if not self.fused or self._hooked() or x.requires_grad or self._forward_hooks or self._forward_pre_hooks:
+            # hooks on this module itself run only through __call__: the caller's self(x) path
             return None
         if layout is FC1_EMBED:
             x = self._pre_embed(x).contiguous()
+        if not label.is_cuda and label.numel() and not (0 <= int(label.min()) and int(label.max()) < self.n_classes):
+            raise IndexError(f"forward_ce: labels must lie in [0, {self.n_classes})")   # as F.one_hot
         lab = label.reshape(-1).to(device=x.device, dtype=torch.int64).contiguous()
         if lab.numel() != x.shape[0]:
             raise ValueError(f"forward_ce: {lab.numel()} labels for {x.shape[0]} bags")

@@ -43,7 +43,7 @@ class _LayerNormFn(torch.autograd.Function):
         rpb = 64
         work = torch.empty(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4, device=x.device)
         _lib.call("tm_layernorm_bwd", _p(dy.float().contiguous()), F32, _p(x), _p(w), _p(mean), _p(rstd),
-                  B * S, D, S, S, 0, rpb, 0, _p(dx), _p(work), _p(dw), _p(db), _stream())
+                  B * S, D, S, S, 0, rpb, 0, _p(dx), _p(work), _p(dw), _p(db), C.c_void_p(0), _stream())
         return dx, dw, db, None
 
 
