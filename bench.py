@@ -86,6 +86,19 @@ def roofline_model(site, n_patches, dtype_bytes):
         byts = mat * (1 + 1 + 3 + 6 * 5 + 5 * 5 + 4)   # X; S; A_0 out; B_k/A_k in+out; F
         return dict(bytes=byts, flops=flops, peak_tfs=F32_MATRIX_PEAK_TFS, units=14,
                     note="fp32-class products as bf16 hi/lo x3 on the bf16 MFMA; units = launches per call")
+    if site == "pinv_bwd":
+        # the adjoint of the chain (pinv_split.hip bwd_level_job), per iteration 8 products of 256^3 per
+        # head in 4 launches (dT5, dZa | dP, dT3 | dP += dT3 P^T + P^T dT3 | dX, G), then the c-gradient
+        # dot and the apply launch (Z_0 = X^T / c terms + the A2 softmax backward);
+        # bytes: every operand / addend read and every output written once per level as split bf16
+        # planes (4 B per element; dX fp32): 14 matrices read + 7 written per iteration, then G, X
+        # (c-dot) and X, G, dX in + out (apply)
+        mat = heads * m * m * 4
+        flops = 6 * 8 * heads * 2 * m ** 3
+        byts = mat * (6 * (14 + 7) + 2 + 4)
+        return dict(bytes=byts, flops=flops, peak_tfs=F32_MATRIX_PEAK_TFS, units=26,
+                    note="fp32-class products as bf16 hi/lo x3 on the bf16 MFMA; 24 pinv_stage_kernel launches "
+                         "+ pinv_c_dot_kernel + pinv_apply_bwd_kernel per call; units = launches per call")
     if site == "a1_fwd":
         # read q, v (conv) [n, 512] T; write merged [n, 512] T + lse [8, n] fp32; landmarks/Y fp32
         byts = 3 * n * 512 * t + heads * n * 4 + 2 * heads * m * dh * 4
@@ -326,9 +339,12 @@ def main():
         def step(i):
             graphs[i % len(graphs)].replay()
 
+    # the roofline call site, and the pseudo-inverse backward beside the forward chain
+    probe_sites = {args.probe, "pinv_bwd"} if args.probe == "pinv_fwd" else {args.probe}
     if args.eager:
-        engine.probe.target = args.probe
+        engine.probe.target = probe_sites
         engine.probe.events.clear()
+        engine.probe.names.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -355,7 +371,7 @@ def main():
         # three times; the events hold each replay's timestamps.  The timed graph has no probes.
         try:
             pgraph = torch.cuda.CUDAGraph()
-            engine.probe.target, engine.probe.external = args.probe, True
+            engine.probe.target, engine.probe.external = probe_sites, True
             engine.probe.events.clear()
             with torch.cuda.graph(pgraph):
                 body()
@@ -364,7 +380,8 @@ def main():
                 load(i)
                 pgraph.replay()
                 torch.cuda.synchronize()
-                kernel_ms_samples += [s.elapsed_time(e) for s, e in engine.probe.events]
+                kernel_ms_samples += [(nm, s.elapsed_time(e)) for nm, (s, e) in zip(engine.probe.names, engine.probe.events)]
+                engine.probe.names.clear()
         except Exception as exc:  # noqa: BLE001 - event timing inside graphs unsupported: probe eagerly
             print(f"# graph event probe unavailable ({exc}); eager probe", file=sys.stderr)
             engine.probe.target, engine.probe.external = None, False
@@ -372,9 +389,10 @@ def main():
         if not kernel_ms_samples:
             # after the timed region: three eager steps with the probed launch queued behind
             # a GPU spin (engine._Probe.spin_cycles), so its events bracket the kernel itself
-            engine.probe.target = args.probe
+            engine.probe.target = probe_sites
             engine.probe.spin_cycles = 2_000_000
             engine.probe.events.clear()
+            engine.probe.names.clear()
             for i in range(3):
                 load(i)
                 body()
@@ -382,12 +400,16 @@ def main():
             engine.probe.target = None
             engine.probe.spin_cycles = 0
             # launch span minus the span of an empty event pair recorded just before it
-            kernel_ms_samples = [s.elapsed_time(e) - zs.elapsed_time(ze) for s, e, zs, ze in engine.probe.events]
-            overhead_samples = [zs.elapsed_time(ze) for _, _, zs, ze in engine.probe.events]
-            span_samples = [s.elapsed_time(e) for s, e, _, _ in engine.probe.events]
+            evs = list(zip(engine.probe.names, engine.probe.events))
+            kernel_ms_samples = [(nm, s.elapsed_time(e) - zs.elapsed_time(ze)) for nm, (s, e, zs, ze) in evs]
+            overhead_samples = [(nm, zs.elapsed_time(ze)) for nm, (_, _, zs, ze) in evs]
+            span_samples = [(nm, s.elapsed_time(e)) for nm, (s, e, _, _) in evs]
     if graph is None:
-        kernel_ms_samples = [s.elapsed_time(e) for s, e in engine.probe.events]
-    kernel_ms = sum(kernel_ms_samples) / max(len(kernel_ms_samples), 1)
+        kernel_ms_samples = [(nm, s.elapsed_time(e)) for nm, (s, e) in zip(engine.probe.names, engine.probe.events)]
+
+    def site_mean(samples, site):
+        xs = [v for nm, v in samples if nm == site]
+        return sum(xs) / len(xs) if xs else None
 
     hbm = None
     if rank == 0 and not args.no_hbm_probe and args.features == 512:
@@ -415,29 +437,39 @@ def main():
         except Exception as exc:  # noqa: BLE001
             print(f"# optimizer timing unavailable ({exc})", file=sys.stderr)
 
-    if rank == 0:
-        slides = args.steps * world
+    def roofline_obj(site):
+        kernel_ms = site_mean(kernel_ms_samples, site)
+        if kernel_ms is None:
+            return None
         tb = 2 if args.dtype == "bf16" else 4
-        rm = roofline_model(args.probe, args.n, tb)
+        rm = roofline_model(site, args.n, tb)
         sec = kernel_ms / 1e3
         ach_bw = rm["bytes"] / sec / 1e9
         ach_fl = rm["flops"] / sec / 1e12
         peak_fl = rm.get("peak_tfs", BF16_PEAK_TFS if args.dtype == "bf16" else F32_MATRIX_PEAK_TFS)
         hbm_bound = rm["flops"] / rm["bytes"] < peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
         roof = (dict(bound="hbm", achieved=round(ach_bw, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                     frac=round(ach_bw / HBM_PEAK_GBS, 4), traffic=measured_traffic(args.probe, args.n, args.dtype))
+                     frac=round(ach_bw / HBM_PEAK_GBS, 4), traffic=measured_traffic(site, args.n, args.dtype))
                 if hbm_bound else
                 dict(bound="mfma", achieved=round(ach_fl, 2), peak=peak_fl, unit="TFLOP/s",
-                     frac=round(ach_fl / peak_fl, 4), traffic=measured_traffic(args.probe, args.n, args.dtype)))
+                     frac=round(ach_fl / peak_fl, 4), traffic=measured_traffic(site, args.n, args.dtype)))
         if overhead_samples:
-            roof.update(event_span_ms=round(sum(span_samples) / len(span_samples), 5),
-                        event_pair_overhead_ms=round(sum(overhead_samples) / len(overhead_samples), 5))
-        kname = {"pinv_fwd": "pinv_stage_kernel x14 (tm_pinv_fwd_split_a3)"}.get(args.probe, args.probe)
-        roof.update(kernel=kname, kernel_ms=round(kernel_ms, 5), samples=len(kernel_ms_samples),
+            roof.update(event_span_ms=round(site_mean(span_samples, site), 5),
+                        event_pair_overhead_ms=round(site_mean(overhead_samples, site), 5))
+        kname = {"pinv_fwd": "pinv_stage_kernel x14 (tm_pinv_fwd_split_a3)",
+                 "pinv_bwd": "pinv_stage_kernel x24 + pinv_c_dot_kernel + pinv_apply_bwd_kernel "
+                             "(tm_pinv_bwd_split)"}.get(site, site)
+        roof.update(kernel=kname, kernel_ms=round(kernel_ms, 5),
+                    samples=sum(1 for nm, _ in kernel_ms_samples if nm == site),
                     algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])
         if "units" in rm:
             roof.update(launches_per_call=rm["units"], ms_per_launch=round(kernel_ms / rm["units"], 5),
                         note=rm["note"])
+        return roof
+
+    if rank == 0:
+        slides = args.steps * world
+        roof = roofline_obj(args.probe)
         base_metric = "slides/sec (fwd+bwd) at N=8192 patches, d=512"
         if args.features == 512:
             metric = base_metric if args.n == 8192 else f"slides/sec (fwd+bwd) at N={args.n} patches, d=512"
@@ -461,6 +493,7 @@ def main():
                        "execution": "eager" if args.eager else "hipGraph replay of the whole step (one graph per resident bag)",
                        "global_batch": world, "seq_len": args.n, "parallelism": f"dp{world}"},
             "roofline": roof,
+            "roofline_pinv_bwd": roofline_obj("pinv_bwd") if args.probe == "pinv_fwd" else None,
             "hbm_roofline": hbm,
             "optimizer_ms": round(opt_ms, 5) if opt_ms is not None else None,
         }

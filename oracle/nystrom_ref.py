@@ -12,10 +12,17 @@ does not vendor it.  The variant is pinned by its consumers: a 4-D
 ``[B, h, n', n']`` attention return and FRONT padding to a multiple of the
 landmark count (``code/visualize_mil.py:580-581``,
 ``code/models/TransMIL.py:190-193``) -- the 0.0.11-era API restated in
-SURVEY.md section 8 Appendix A (eq. 1-11).  Parity of the arithmetic inside
-this class is therefore **unpinned** by reference-held fixtures; it is
-cross-checked against HF ``NystromformerSelfAttention.iterative_inv`` for the
-pseudo-inverse (eq. 7) in ``tests/test_oracle.py``.
+SURVEY.md section 8 Appendix A (eq. 1-11).  The package itself is absent (no
+lock file, not installable offline), so no reference-held fixture pins this
+class directly.  Its arithmetic is pinned against an independent
+implementation of the same algorithm: ``tests/test_oracle.py::
+test_nystrom_eq2_to_9_match_hf_nystromformer`` compares eq. 2-9 (segment-mean
+landmarks, the three softmaxes, the Moore-Penrose iteration, the aggregation
+and the 33-tap residual conv) with HF ``NystromformerSelfAttention.forward``
+in fp64 to 1e-9 at n' in {512 (B=2), 1280, 8448}; the front pad and the
+``out[:, -n:]`` slice (eq. 1, 10), which HF does not do, are pinned by the
+fixtures generated from the reference's own ``code/models/TransMIL.py``
+(tests/golden/make_golden*.py).
 
 Everything is plain torch on the CPU, in the dtype of the input (fp32 or fp64).
 """
