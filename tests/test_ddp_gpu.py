@@ -125,8 +125,8 @@ def test_rccl_allreduce_inside_captured_graph(overlap):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k,n", [(1, 700), (3, 700), (1, 8192)])
-def test_two_ranks_average_through_the_hip_engine(k, n, tmp_path):
+@pytest.mark.parametrize("k,npatch", [(1, 700), (3, 700), (1, 8192)])
+def test_two_ranks_average_through_the_hip_engine(k, npatch, tmp_path):
     """Two processes on the one leased GPU (gloo: RCCL refuses two ranks on one device), each
     running the fused HIP TransMIL step (bf16 mode, train mode) on its own bags with
     ``GradAllReduce(model=..., overlap=True)`` and ``accumulate_grad_batches = k``
@@ -150,7 +150,7 @@ def test_two_ranks_average_through_the_hip_engine(k, n, tmp_path):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(here, "ddp_two_rank_worker.py"),
-                                       str(tmp_path / f"rank{r}.pt"), str(k), str(steps), str(n)],
+                                       str(tmp_path / f"rank{r}.pt"), str(k), str(steps), str(npatch)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     try:
@@ -178,7 +178,7 @@ def test_two_ranks_average_through_the_hip_engine(k, n, tmp_path):
         for micro in range(s * k, (s + 1) * k):
             for r in range(world):
                 model._dropout_counter.copy_(c0 + micro)     # each rank's stream at this micro-batch
-                task.backward(task.training_step(W.bag(r, micro, n)) / (world * k))
+                task.backward(task.training_step(W.bag(r, micro, npatch)) / (world * k))
         opt.step()
         opt.zero_grad(set_to_none=True)
     torch.cuda.synchronize()

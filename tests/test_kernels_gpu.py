@@ -223,15 +223,17 @@ def test_layernorm_fwd_bwd():
 
 
 # ----------------------------------------------------------------------------- PPEG
-@pytest.mark.parametrize("G", [1, 5, 32])
-def test_ppeg_fwd_bwd(G):
+@pytest.mark.parametrize("G,D,B", [(1, 64, 2), (5, 64, 2), (32, 64, 2), (13, 128, 3), (91, 512, 1)])
+def test_ppeg_fwd_bwd(G, D, B):
+    """The persistent PPEG walker (tile teams per 64-channel chunk, fused weight gradient) against the
+    fp64 oracle PPEG (code/models/TransMIL.py:60-75); G = 91, D = 512 is the bench shape."""
     from oracle.transmil_ref import PPEG as RefPPEG
     from transmil_deepgraft_amd.models.TransMIL import PPEG
     torch.manual_seed(G)
-    ref = RefPPEG(64).double()
-    ours = PPEG(64).to(DEV)
+    ref = RefPPEG(D).double()
+    ours = PPEG(D).to(DEV)
     ours.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
-    x = torch.randn(2, 1 + G * G, 64, dtype=torch.float64)
+    x = torch.randn(B, 1 + G * G, D, dtype=torch.float64)
     y_ref = ref(x.clone().requires_grad_(), G, G)
     xr = x.clone().requires_grad_()
     y_ref = ref(xr, G, G)

@@ -148,6 +148,23 @@ const char* tm_set_error(const char* msg);
 
 enum { TM_F32 = 0, TM_BF16 = 1 };
 
+// Compute units of the current device (hipDeviceAttributeMultiprocessorCount), for grid sizing
+// only (never for results' layout): a read-only per-device cache, so schedules follow the part
+// the library runs on instead of assuming 256 CUs.
+inline int tm_cu_count() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  static int cache[64];   // benign race: every writer stores the same device constant
+  int v = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+  if (v <= 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) c = 256;
+    __atomic_store_n(&cache[dev], c, __ATOMIC_RELAXED);
+    v = c;
+  }
+  return v;
+}
+
 // Opt a kernel into > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
 template <typename K>
 inline void tm_allow_smem(K kernel, size_t bytes) {

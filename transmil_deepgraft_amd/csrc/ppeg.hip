@@ -7,8 +7,8 @@
 // ONE 7x7 depthwise stencil (w = w7 + pad(w5) + pad(w3) + delta, b = b7+b5+b3),
 // applied channel-last directly on the [B, S, D] fp32 residual stream: token
 // t = 1 + r*G + c (row-major, :71).  No transpose to NCHW, no padded copy.
-// Blocks own a tile of grid cells x 64 channels staged through LDS (one burst of coalesced
-// 256-B channel-row loads per window); HBM-bound.
+// Persistent workgroups walk tiles of grid cells x 64 channels staged through LDS (coalesced
+// 256-B channel-row loads, the next tile's window in flight during the current tile); HBM-bound.
 #include "common.h"
 #include "../../include/transmil_hip.h"
 
@@ -34,35 +34,12 @@ __global__ void ppeg_fold_kernel(const float* __restrict__ w7, const float* __re
   bf[ch] = b7[ch] + b5[ch] + b3[ch];
 }
 
-// LDS-tiled stencil: a 256-thread block owns a TR x TC tile of grid cells x 64 channels.  The
-// (TR + 6) x (TC + 6) input window (zero outside the grid) is requested in one burst of 16-B
-// loads (a wave covers 4 cells x 64 channels: four 256-B segments) into LDS [cell][64]; then
-// thread (channel, g) computes output rows 2g, 2g + 1 of the tile (16 cells x 49 taps) from LDS
-// (consecutive channels in consecutive banks) and stores 256-B channel rows.
-// grid (ceil(G / TC) * D / 64, ceil(G / TR), B), block 256.
+// Tiles: TR x TC grid cells x 64 channels; the (TR + 6) x (TC + 6) input window (zero outside
+// the grid) sits in LDS as [cell][64] fp32 (consecutive channels in consecutive banks), requested
+// as 16-B pieces (a wave covers 4 cells x 64 channels: four 256-B segments).
 constexpr int TR = 8, TC = 8, WR = TR + KS - 1, WC = TC + KS - 1;  // 14 x 14 window
 constexpr int WIN = WR * WC;                                       // 196 cells
 constexpr int TILE_LDS = WIN * 64 * 4;                             // 50 KB
-
-// the block's input window into LDS (zero outside the G x G grid)
-TM_DEV void load_window(float* win, const float* __restrict__ xb, int G, int D, int r0, int c0) {
-  const int tid = threadIdx.x;
-  constexpr int PIECES = WIN * 16;              // 16-B pieces (4 channels each)
-  constexpr int PER = (PIECES + 255) / 256;     // 13: every load in flight before the first LDS write
-  f32x4 v[PER];
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int i = u * 256 + tid, cell = i >> 4, c4 = (i & 15) * 4;
-    const int rr = r0 - R + cell / WC, cc = c0 - R + cell % WC;
-    v[u] = (i < PIECES && rr >= 0 && rr < G && cc >= 0 && cc < G)
-               ? *(const f32x4*)(xb + (size_t)(rr * G + cc) * D + c4) : (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int i = u * 256 + tid;
-    if (i < PIECES) *(f32x4*)(win + (i >> 4) * 64 + (i & 15) * 4) = v[u];
-  }
-}
 
 // Backward only, optional: the next layer-backward's first step fused into the stencil's stores --
 // dout[b][pad + t][c] = T(keep(b*S + t, c) * scale * dx[b*S + t][c]) and zero pad rows, the
@@ -82,136 +59,164 @@ TM_DEV void droppad_store(const DropPad& dp, uint64_t seed, int b, int S, int D,
   else ((float*)dp.out)[o] = v;
 }
 
-template <bool BWD_DATA>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void ppeg_stencil_kernel(const float* __restrict__ x, int S, int G, int D,
-                                                           const float* __restrict__ wf, const float* __restrict__ bf,
-                                                           float* __restrict__ y, DropPad dp) {
-  extern __shared__ __attribute__((aligned(16))) float win[];
+// ---------------------------------------------------------------------------
+// Persistent tile walker (the step's PPEG launches).  The tiles of one 64-channel chunk belong to a
+// team of workgroups launched as blockIdx.x = chunk + nchunk * team, so with the round-robin
+// dispatch a chunk's team sits on ONE XCD (nchunk = 8): the 3-cell halo every 8 x 8 tile re-reads is
+// served by that XCD's L2 (the chunk's x / dy slices are 2.1 MB each).  A team member walks tiles
+// team, team + nteam, ... (row-major: the team works on neighbouring tiles at the same time), and
+// the next tile's window is requested into registers before the current tile is computed, so its
+// HBM / L2 round trip overlaps the stencil arithmetic.  512 threads: wave w computes row w of the
+// tile (8 cells x 49 taps per lane = channel), in a fixed tap order (window rows, then
+// columns).  BWD: the window of dy gives dx (flipped taps, + the fused dropout-pad store of the layer
+// below) and, with the x window beside it, the 49 tap + bias gradient partials of the tile's cells
+// (dW[tap] += dy[cell] x[cell + tap - 3]), kept in registers over the member's tiles and summed over
+// its 8 waves in a fixed order into ONE [D][50] partial slab per member (the x / dy windows are read
+// once; the separate weight-gradient pass and its second read of dy / x are gone).
+constexpr int WALK_THREADS = 512;
+constexpr int WALK_PER = (WIN * 16 + WALK_THREADS - 1) / WALK_THREADS;   // 16-B window pieces per thread: 7
+constexpr int WALK_RED = 8 * 64 * (NT + 1) * 4;                          // 102 KB: the 8 waves' partials
+
+constexpr int WALK_W = NT * 64 * 4;                                      // the chunk's folded taps: 12.25 KB
+template <bool BWD>
+constexpr int walk_lds() { return (BWD ? (2 * TILE_LDS > WALK_RED ? 2 * TILE_LDS : WALK_RED) : TILE_LDS) + WALK_W; }
+
+// tiles per team member for a chunk of `ntiles` tiles and at most `cap` members: the balanced team size
+inline int walk_team(int ntiles, int cap) {
+  cap = cap < 1 ? 1 : cap;
+  const int per = (ntiles + cap - 1) / cap;
+  return (ntiles + per - 1) / per;
+}
+
+template <bool BWD>
+__global__ __launch_bounds__(WALK_THREADS) void ppeg_walk_kernel(const float* __restrict__ src,
+                                                                 const float* __restrict__ xw, int S, int G, int D,
+                                                                 int nteam, const float* __restrict__ wf,
+                                                                 const float* __restrict__ bf, float* __restrict__ y,
+                                                                 DropPad dp, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* win = lds;                        // [WIN][64]: x (forward) / dy (backward)
+  float* winx = lds + WIN * 64;            // backward: the x window
+  float* wl = lds + (walk_lds<BWD>() - WALK_W) / 4;   // [49][64] taps (flipped for the backward)
   const int nchunk = D / 64;
-  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
-  const int chunk = blockIdx.x % nchunk, ch = chunk * 64 + lane;
-  const int r0 = blockIdx.y * TR, c0 = (blockIdx.x / nchunk) * TC, b = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int chunk = blockIdx.x % nchunk, team = blockIdx.x / nchunk, b = blockIdx.y;
+  const int ch = chunk * 64 + lane;
+  const int ntc = (G + TC - 1) / TC, ntiles = ((G + TR - 1) / TR) * ntc;
+  const float* sb = src + (size_t)b * S * D + D + chunk * 64;
+  const float* xb = BWD ? xw + (size_t)b * S * D + D + chunk * 64 : nullptr;
   float* yb = y + (size_t)b * S * D;
-  const bool fuse = BWD_DATA && dp.out != nullptr;
+  const bool fuse = BWD && dp.out != nullptr;
   const uint64_t seed = fuse && dp.p > 0.f ? effective_seed(dp.seed0, dp.seed_ptr) : 0;
-  if (blockIdx.x < (unsigned)nchunk && blockIdx.y == 0) {
-    if (g == 0) {  // class token passes through
-      const float v = x[(size_t)b * S * D + ch];
+  if (team == 0) {
+    if (w == 0) {  // the class token passes through
+      const float v = src[(size_t)b * S * D + ch];
       yb[ch] = v;
       if (fuse) droppad_store(dp, seed, b, S, D, 0, ch, v);
     }
-    if (fuse)  // the front pad rows of dout are zero
-      for (int t = g; t < dp.pad; t += 4) {
+    if (fuse)      // the front pad rows of dout are zero
+      for (int t = w; t < dp.pad; t += WALK_THREADS / 64) {
         const size_t o = ((size_t)b * dp.n_pad + t) * D + ch;
         if (dp.dtype == TM_BF16) ((bf16*)dp.out)[o] = (bf16)0.f;
         else ((float*)dp.out)[o] = 0.f;
       }
   }
-  load_window(win, x + (size_t)b * S * D + D + chunk * 64, G, D, r0, c0);
-  float w[NT];
+  for (int t = w; t < NT; t += WALK_THREADS / 64) wl[t * 64 + lane] = wf[(size_t)(BWD ? NT - 1 - t : t) * D + ch];
+  const float bias = BWD ? 0.f : bf[ch];
+  float accw[BWD ? NT + 1 : 1];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) w[t] = wf[(size_t)(BWD_DATA ? NT - 1 - t : t) * D + ch];
-  const float bias = BWD_DATA ? 0.f : bf[ch];
-  __syncthreads();
-  float acc[2][TC];
+  for (int t = 0; t < (BWD ? NT + 1 : 1); ++t) accw[t] = 0.f;
+
+  // window pieces of tile t (zero outside the grid): piece i = cell i / 16, channels 4 (i % 16)
+  f32x4 pa[WALK_PER], pb[BWD ? WALK_PER : 1];
+  auto fetch = [&](int t) {
+    const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int u = 0; u < WALK_PER; ++u) {
+      const int i = u * WALK_THREADS + tid, cell = i >> 4, c4 = (i & 15) * 4;
+      const int rr = r0 - R + cell / WC, cc = c0 - R + cell % WC;
+      const bool in = i < WIN * 16 && rr >= 0 && rr < G && cc >= 0 && cc < G;
+      const size_t o = (size_t)(rr * G + cc) * D + c4;
+      pa[u] = in ? *(const f32x4*)(sb + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (BWD) pb[u] = in ? *(const f32x4*)(xb + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto stage = [&]() {
 #pragma unroll
-    for (int j = 0; j < TC; ++j) acc[i][j] = bias;
+    for (int u = 0; u < WALK_PER; ++u) {
+      const int i = u * WALK_THREADS + tid;
+      if (i < WIN * 16) {
+        *(f32x4*)(win + (i >> 4) * 64 + (i & 15) * 4) = pa[u];
+        if constexpr (BWD) *(f32x4*)(winx + (i >> 4) * 64 + (i & 15) * 4) = pb[u];
+      }
+    }
+  };
+  if (team < ntiles) fetch(team);
+  for (int t = team; t < ntiles; t += nteam) {
+    __syncthreads();   // the previous tile's LDS reads are done
+    stage();
+    __syncthreads();
+    if (t + nteam < ntiles) fetch(t + nteam);   // in flight through this tile's arithmetic
+    const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
+    float acc[TC];
 #pragma unroll
-  for (int ir = 0; ir < 2 + KS - 1; ++ir) {   // window rows 2g .. 2g + 7
-    float xv[WC];
+    for (int j = 0; j < TC; ++j) acc[j] = bias;
+#pragma unroll 1
+    for (int dy = 0; dy < KS; ++dy) {   // window row w + dy (rolled: the row's 14 + 7 values live at once)
+      float xv[WC], wt[KS];
 #pragma unroll
-    for (int ic = 0; ic < WC; ++ic) xv[ic] = win[((2 * g + ir) * WC + ic) * 64 + lane];
+      for (int ic = 0; ic < WC; ++ic) xv[ic] = win[((w + dy) * WC + ic) * 64 + lane];
 #pragma unroll
-    for (int orow = 0; orow < 2; ++orow) {
-      const int dy = ir - orow;
-      if (dy < 0 || dy >= KS) continue;
+      for (int dx = 0; dx < KS; ++dx) wt[dx] = wl[(dy * KS + dx) * 64 + lane];
 #pragma unroll
       for (int oc = 0; oc < TC; ++oc)
 #pragma unroll
-        for (int dx = 0; dx < KS; ++dx) acc[orow][oc] = fmaf(w[dy * KS + dx], xv[oc + dx], acc[orow][oc]);
+        for (int dx = 0; dx < KS; ++dx) acc[oc] = fmaf(wt[dx], xv[oc + dx], acc[oc]);
     }
-  }
-#pragma unroll
-  for (int orow = 0; orow < 2; ++orow)
+    const int r = r0 + w;
 #pragma unroll
     for (int oc = 0; oc < TC; ++oc) {
-      const int r = r0 + 2 * g + orow, c = c0 + oc;
+      const int c = c0 + oc;
       if (r < G && c < G) {
-        yb[(size_t)(1 + r * G + c) * D + ch] = acc[orow][oc];
-        if (fuse) droppad_store(dp, seed, b, S, D, 1 + r * G + c, ch, acc[orow][oc]);
+        yb[(size_t)(1 + r * G + c) * D + ch] = acc[oc];
+        if (fuse) droppad_store(dp, seed, b, S, D, 1 + r * G + c, ch, acc[oc]);
       }
     }
-}
-
-// weight / bias gradient partials: dW[ch][tap] = sum_cells dy[cell][ch] x[cell + tap][ch],
-// db[ch] = sum_cells dy[cell][ch].  A block walks WT tiles along a row of tiles (x window and dy
-// tile through LDS, as the stencil), thread (channel, g) accumulating its 16 cells x 49 taps;
-// the 4 g partials are summed in order through LDS.  grid (ceil(nTC / WT) * D / 64, nTR, B),
-// partial slab index = (b * gridDim.y + by) * gridDim.x/nchunk + bx/nchunk, layout [slab][ch][50].
-constexpr int WT_DEFAULT = 3;   // G = 91: 4 column groups x 12 row tiles x 8 channel chunks = 384 blocks (scripts/dev/ppeg_wt.py: 43.0 vs 48.3 us at 4)
-#ifdef TM_DIAG
-int g_ppeg_wt = 0;   // diagnostic build: tiles per wgrad block (0: WT_DEFAULT)
-#define PPEG_WT (g_ppeg_wt > 0 ? g_ppeg_wt : WT_DEFAULT)
-#else
-#define PPEG_WT WT_DEFAULT
-#endif
-constexpr int DY_LDS = TR * TC * 64 * 4;   // 16 KB
-__global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy_,
-                                                         int S, int G, int D, int WT, float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float win[];
-  float* dyt = win + WIN * 64;
-  const int nchunk = D / 64;
-  const int tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
-  const int chunk = blockIdx.x % nchunk;
-  const int r0 = blockIdx.y * TR, b = blockIdx.z;
-  const int ntc = (G + TC - 1) / TC;
-  const float* xb = x + (size_t)b * S * D + D + chunk * 64;
-  const float* gb = dy_ + (size_t)b * S * D + D + chunk * 64;
-  float acc[NT + 1];
-#pragma unroll
-  for (int t = 0; t <= NT; ++t) acc[t] = 0.f;
-  for (int tcol = (blockIdx.x / nchunk) * WT; tcol < min(ntc, (int)(blockIdx.x / nchunk) * WT + WT); ++tcol) {
-    const int c0 = tcol * TC;
-    __syncthreads();  // previous tile's LDS reads done
-    load_window(win, xb, G, D, r0, c0);
-    for (int i = tid; i < TR * TC * 16; i += 256) {
-      const int cell = i >> 4, c4 = (i & 15) * 4, rr = r0 + cell / TC, cc = c0 + cell % TC;
-      *(f32x4*)(dyt + cell * 64 + c4) = (rr < G && cc < G) ? *(const f32x4*)(gb + (size_t)(rr * G + cc) * D + c4)
-                                                            : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-    __syncthreads();
-#pragma unroll
-    for (int orow = 0; orow < 2; ++orow) {
-      const int tr = 2 * g + orow;
+    if constexpr (BWD) {
+      // dW[dy][dx] += dy(r, c) x(r + dy - 3, c + dx - 3): dy(r, c) = centre of the dy window
       float gv[TC];
 #pragma unroll
       for (int oc = 0; oc < TC; ++oc) {
-        gv[oc] = dyt[(tr * TC + oc) * 64 + lane];
-        acc[NT] += gv[oc];
+        gv[oc] = win[((w + R) * WC + oc + R) * 64 + lane];
+        accw[NT] += gv[oc];
       }
 #pragma unroll
-      for (int dy = 0; dy < KS; ++dy) {
+      for (int dy = 0; dy < KS; ++dy) {   // unrolled: accw is indexed by dy at compile time
         float xv[WC];
 #pragma unroll
-        for (int ic = 0; ic < WC; ++ic) xv[ic] = win[((tr + dy) * WC + ic) * 64 + lane];
+        for (int ic = 0; ic < WC; ++ic) xv[ic] = winx[((w + dy) * WC + ic) * 64 + lane];
 #pragma unroll
         for (int oc = 0; oc < TC; ++oc)
 #pragma unroll
-          for (int dx = 0; dx < KS; ++dx) acc[dy * KS + dx] = fmaf(gv[oc], xv[oc + dx], acc[dy * KS + dx]);
+          for (int dx = 0; dx < KS; ++dx) accw[dy * KS + dx] = fmaf(gv[oc], xv[oc + dx], accw[dy * KS + dx]);
       }
     }
   }
-  __syncthreads();
-  float* red = win;  // [4][64][NT + 1]
+  if constexpr (BWD) {
+    __syncthreads();   // the windows are no longer read: the LDS takes the 8 waves' partials
+    float* red = lds;  // [8][64][NT + 1]
 #pragma unroll
-  for (int t = 0; t <= NT; ++t) red[(g * 64 + lane) * (NT + 1) + t] = acc[t];
-  __syncthreads();
-  const int slab = (b * gridDim.y + blockIdx.y) * (gridDim.x / nchunk) + blockIdx.x / nchunk;
-  float* dst = part + (size_t)slab * D * (NT + 1) + (size_t)chunk * 64 * (NT + 1);
-  for (int e = tid; e < 64 * (NT + 1); e += 256)
-    dst[e] = (red[e] + red[64 * (NT + 1) + e]) + (red[2 * 64 * (NT + 1) + e] + red[3 * 64 * (NT + 1) + e]);
+    for (int t = 0; t <= NT; ++t) red[(w * 64 + lane) * (NT + 1) + t] = accw[t];
+    __syncthreads();
+    float* dst = part + ((size_t)b * nteam + team) * D * (NT + 1) + (size_t)chunk * 64 * (NT + 1);
+    constexpr int E = 64 * (NT + 1);
+    for (int e = tid; e < E; e += WALK_THREADS) {
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < 8; ++v) s += red[v * E + e];
+      dst[e] = s;
+    }
+  }
 }
 
 // unfold folded gradients: dw7 = dwf, dw5 = centre 5x5, dw3 = centre 3x3, db* = db
@@ -244,9 +249,6 @@ __global__ __launch_bounds__(256) void ppeg_wgrad_reduce_kernel(const float* __r
 
 }  // namespace
 
-#ifdef TM_DIAG
-extern "C" void tm_debug_set_ppeg_wt(int v) { g_ppeg_wt = v; }
-#endif
 
 extern "C" int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, const float* b5, const float* w3,
                             const float* b3, int D, float* wfold, float* bfold, void* stream) {
@@ -256,33 +258,28 @@ extern "C" int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, c
 }
 
 // x, y: [B, S, D] fp32 with S = 1 + G*G.  y must not alias x.
+// team members of the walker per chunk: the forward (50 KB of LDS) two workgroups per CU, the
+// backward (100 KB) one
+static int walk_nteam(int G, int D, bool bwd) {
+  const int ntiles = ((G + TR - 1) / TR) * ((G + TC - 1) / TC);
+  const int nchunk = D / 64;
+  return walk_team(ntiles, (bwd ? 1 : 2) * tm_cu_count() / nchunk);
+}
+
+// x, y: [B, S, D] fp32 with S = 1 + G*G.  y must not alias x.
 extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
                            void* stream) {
-  TM_REQUIRE(x && y && x != y && D % 64 == 0 && G > 0, "ppeg_fwd: bad args");
-  const dim3 grid(((G + TC - 1) / TC) * (D / 64), (G + TR - 1) / TR, B);
-  ppeg_stencil_kernel<false><<<grid, 256, TILE_LDS, (hipStream_t)stream>>>(x, 1 + G * G, G, D, wfold, bfold, y,
-                                                                          DropPad{});
+  TM_REQUIRE(x && y && x != y && D % 64 == 0 && G > 0 && B > 0, "ppeg_fwd: bad args");
+  const int nteam = walk_nteam(G, D, false);
+  tm_allow_smem(ppeg_walk_kernel<false>, walk_lds<false>());
+  ppeg_walk_kernel<false><<<dim3(nteam * (D / 64), B), WALK_THREADS, walk_lds<false>(), (hipStream_t)stream>>>(
+      x, nullptr, 1 + G * G, G, D, nteam, wfold, bfold, y, DropPad{}, nullptr);
   TM_CHECK_LAUNCH();
   return 0;
 }
 
-static dim3 wgrad_grid(int B, int G, int D, int wt) {
-  const int ntc = (G + TC - 1) / TC;
-  return dim3(((ntc + wt - 1) / wt) * (D / 64), (G + TR - 1) / TR, B);
-}
-
-static int ppeg_wgrad_slabs(int B, int G, int wt) {
-  const dim3 g = wgrad_grid(B, G, 64, wt);
-  return (int)(g.x * g.y * g.z);
-}
-
 extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
-#ifdef TM_DIAG
-  const int wt = 1;   // the largest slab count any diagnostic WT needs
-#else
-  const int wt = PPEG_WT;
-#endif
-  return (long long)ppeg_wgrad_slabs(B, G, wt) * D * 50 * (long long)sizeof(float);
+  return (long long)B * walk_nteam(G, D, true) * D * (NT + 1) * (long long)sizeof(float);
 }
 
 // dy: [B,S,D] upstream gradient; x: PPEG input.  dx written (=); weight grads written.
@@ -290,22 +287,20 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
                            float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
                            float* db3, int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
                            const uint64_t* seed_ptr, void* stream) {
-  TM_REQUIRE(x && dy && dx && dx != dy && D % 64 == 0, "ppeg_bwd: bad args");
+  TM_REQUIRE(x && dy && dx && dx != dy && D % 64 == 0 && G > 0 && B > 0, "ppeg_bwd: bad args");
   TM_REQUIRE(!dout || ((dtype == TM_BF16 || dtype == TM_F32) && n_pad >= pad + 1 + G * G && pad >= 0),
              "ppeg_bwd: bad dropout-pad output");
   hipStream_t st = (hipStream_t)stream;
   const int S = 1 + G * G;
   const DropPad dp{dout, dtype, n_pad, pad, p, p > 0.f ? 1.f / (1.f - p) : 1.f, seed, seed_ptr};
-  ppeg_stencil_kernel<true><<<dim3(((G + TC - 1) / TC) * (D / 64), (G + TR - 1) / TR, B), 256, TILE_LDS, st>>>(
-      dy, S, G, D, wfold, nullptr, dx, dp);
-  TM_CHECK_LAUNCH();
-  tm_allow_smem(ppeg_wgrad_kernel, TILE_LDS + DY_LDS);
-  const int wt = PPEG_WT;
-  ppeg_wgrad_kernel<<<wgrad_grid(B, G, D, wt), 256, TILE_LDS + DY_LDS, st>>>(x, dy, S, G, D, wt, work);
+  const int nteam = walk_nteam(G, D, true);
+  tm_allow_smem(ppeg_walk_kernel<true>, walk_lds<true>());
+  ppeg_walk_kernel<true><<<dim3(nteam * (D / 64), B), WALK_THREADS, walk_lds<true>(), st>>>(
+      dy, x, S, G, D, nteam, wfold, nullptr, dx, dp, work);
   TM_CHECK_LAUNCH();
   (void)dwsum;
-  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, ppeg_wgrad_slabs(B, G, wt), D, dw7, db7, dw5,
-                                                                     db5, dw3, db3);
+  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, B * nteam, D, dw7, db7, dw5, db5, dw3,
+                                                                     db3);
   TM_CHECK_LAUNCH();
   return 0;
 }
