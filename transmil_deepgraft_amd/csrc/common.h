@@ -103,6 +103,17 @@ TM_DEV int acc_k_index(int s, int h, int j) { return 16 * s + 8 * (j >> 2) + 4 *
 // row of a C/D register
 TM_DEV int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
+// Raw buffer loads with hardware bounds: an offset at or past `bytes` returns zeros, so a masked
+// (zero-padded) tile load is ONE unconditional instruction (no exec-mask branch around it, 32-bit
+// offsets).  Resource word 3 = 0x00020000 for gfx9 (raw, 32-bit data format).
+TM_DEV __amdgpu_buffer_rsrc_t tm_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+TM_DEV f32x4 tm_bload4(__amdgpu_buffer_rsrc_t r, unsigned off_bytes) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off_bytes, 0, 0));
+}
+constexpr unsigned TM_OOB = 0xFFFFFFF0u;   // an offset past every resource
+
 TM_DEV float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -60,26 +60,32 @@ TM_DEV void droppad_store(const DropPad& dp, uint64_t seed, int b, int S, int D,
 }
 
 // ---------------------------------------------------------------------------
-// Persistent tile walker (the step's PPEG launches).  The tiles of one 64-channel chunk belong to a
-// team of workgroups launched as blockIdx.x = chunk + nchunk * team, so with the round-robin
-// dispatch a chunk's team sits on ONE XCD (nchunk = 8): the 3-cell halo every 8 x 8 tile re-reads is
-// served by that XCD's L2 (the chunk's x / dy slices are 2.1 MB each).  A team member walks tiles
-// team, team + nteam, ... (row-major: the team works on neighbouring tiles at the same time), and
-// the next tile's window is requested into registers before the current tile is computed, so its
-// HBM / L2 round trip overlaps the stencil arithmetic.  512 threads: wave w computes row w of the
-// tile (8 cells x 49 taps per lane = channel), in a fixed tap order (window rows, then
-// columns).  BWD: the window of dy gives dx (flipped taps, + the fused dropout-pad store of the layer
-// below) and, with the x window beside it, the 49 tap + bias gradient partials of the tile's cells
-// (dW[tap] += dy[cell] x[cell + tap - 3]), kept in registers over the member's tiles and summed over
-// its 8 waves in a fixed order into ONE [D][50] partial slab per member (the x / dy windows are read
-// once; the separate weight-gradient pass and its second read of dy / x are gone).
-constexpr int WALK_THREADS = 512;
-constexpr int WALK_PER = (WIN * 16 + WALK_THREADS - 1) / WALK_THREADS;   // 16-B window pieces per thread: 7
-constexpr int WALK_RED = 8 * 64 * (NT + 1) * 4;                          // 102 KB: the 8 waves' partials
-
-constexpr int WALK_W = NT * 64 * 4;                                      // the chunk's folded taps: 12.25 KB
-template <bool BWD>
-constexpr int walk_lds() { return (BWD ? (2 * TILE_LDS > WALK_RED ? 2 * TILE_LDS : WALK_RED) : TILE_LDS) + WALK_W; }
+// Persistent tile walkers (the step's PPEG launches).  The tiles of one 64-channel chunk belong to
+// a team of workgroups launched as blockIdx.x = chunk + nchunk * team, so with the round-robin
+// dispatch a chunk's team sits on ONE XCD (nchunk = 8): the 3-cell halo each 8 x 8 tile re-reads is
+// served by that XCD's L2 (the chunk's slice of a [B, S, 512] tensor is 2.1 MB).  A member walks
+// tiles team, team + nteam, ... (row-major: the team works on neighbouring tiles at the same time)
+// and requests the next tile's operands into registers before it computes the current one, so the
+// HBM / L2 round trip overlaps the arithmetic.
+//
+// Register blocking: a thread owns 4 channels (one 16-B LDS piece) and 4 cells, so one ds_read_b128
+// feeds 4 FMAs per tap it meets (the one-channel-per-lane form was LDS-instruction bound:
+// 0.38 ds_read_b32 per FMA against the ~0.25 the VALU rate allows).
+//   stencil (forward y = conv(x) + b; backward dx = conv_flipped(dy) + the fused dropout-pad store):
+//     256 threads = 16 channel quads x 2 column halves x 8 tile rows; per window row dy: 10 x-pieces
+//     + 7 tap pieces -> 4 cells x 7 taps x 4 channels (the same tap order as before: window rows,
+//     then columns).
+//   weight gradient dW[tap] += dy(cell) x(cell + tap - 3), db += dy(cell): 224 threads = 16 channel
+//     quads x 7 tap rows x 2 tile-row halves (+ 32 threads for db): per tile row, the dy row (8
+//     pieces) and the x window row (14 pieces) -> 7 taps x 8 cells x 4 channels, accumulated in
+//     registers over the member's tiles, then ONE [D][50] partial slab per member.
+constexpr int ST_THREADS = 256;
+constexpr int ST_PER = (WIN * 16 + ST_THREADS - 1) / ST_THREADS;   // 16-B window pieces per thread: 13
+constexpr int TAPS_LDS = NT * 64 * 4;                               // the chunk's folded taps: 12.25 KB
+constexpr int ST_LDS = TILE_LDS + TAPS_LDS;                         // 61.25 KB: two workgroups per CU
+constexpr int DYT_LDS = TR * TC * 64 * 4;                           // dy tile: 16 KB
+constexpr int WG_LDS = TILE_LDS + DYT_LDS;                          // 65 KB
+constexpr int DYT_PER = TR * TC * 16 / ST_THREADS;                  // 4
 
 // tiles per team member for a chunk of `ntiles` tiles and at most `cap` members: the balanced team size
 inline int walk_team(int ntiles, int cap) {
@@ -88,134 +94,196 @@ inline int walk_team(int ntiles, int cap) {
   return (ntiles + per - 1) / per;
 }
 
+TM_DEV f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+
+// the window of tile t (zero outside the grid): piece i = cell i / 16, channel quad i % 16
+// (rsrc: the bag's G x G cells from `base`, bounds-checked: out-of-grid pieces read zeros)
+template <int PER>
+TM_DEV void fetch_window(f32x4 (&v)[PER], __amdgpu_buffer_rsrc_t rsrc, int t, int ntc, int G, int D, int tid) {
+  const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
+  const int c4 = (tid & 15) * 4;
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int cell = u * (ST_THREADS / 16) + (tid >> 4);
+    const int rr = r0 - R + cell / WC, cc = c0 - R + cell % WC;
+    const bool in = (cell < WIN) & ((unsigned)rr < (unsigned)G) & ((unsigned)cc < (unsigned)G);
+    v[u] = tm_bload4(rsrc, in ? (unsigned)((rr * G + cc) * D + c4) * 4u : TM_OOB);
+  }
+}
+template <int PER>
+TM_DEV void stage_window(float* win, const f32x4 (&v)[PER], int tid) {
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = u * ST_THREADS + tid;
+    if (i < WIN * 16) *(f32x4*)(win + (i >> 4) * 64 + (i & 15) * 4) = v[u];
+  }
+}
+
+// 4 consecutive channels of droppad_store as one 8-B (bf16) / 16-B (fp32) store
+TM_DEV void droppad_store4(const DropPad& dp, uint64_t seed, int b, int S, int D, int t, int ch0, f32x4 v) {
+  if (dp.p > 0.f) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      v[e] = dropout_u01(seed, (uint32_t)(b * S + t), (uint32_t)(ch0 + e)) >= dp.p ? v[e] * dp.scale : 0.f;
+  }
+  const size_t o = ((size_t)b * dp.n_pad + dp.pad + t) * D + ch0;
+  if (dp.dtype == TM_BF16) *(bf16x4*)((bf16*)dp.out + o) = (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  else *(f32x4*)((float*)dp.out + o) = v;
+}
+
 template <bool BWD>
-__global__ __launch_bounds__(WALK_THREADS) void ppeg_walk_kernel(const float* __restrict__ src,
-                                                                 const float* __restrict__ xw, int S, int G, int D,
-                                                                 int nteam, const float* __restrict__ wf,
-                                                                 const float* __restrict__ bf, float* __restrict__ y,
-                                                                 DropPad dp, float* __restrict__ part) {
+__global__ __launch_bounds__(ST_THREADS) void ppeg_stencil_walk_kernel(const float* __restrict__ src, int S, int G,
+                                                                      int D, int nteam, const float* __restrict__ wf,
+                                                                      const float* __restrict__ bf,
+                                                                      float* __restrict__ y, DropPad dp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* win = lds;                        // [WIN][64]: x (forward) / dy (backward)
-  float* winx = lds + WIN * 64;            // backward: the x window
-  float* wl = lds + (walk_lds<BWD>() - WALK_W) / 4;   // [49][64] taps (flipped for the backward)
+  float* win = lds;                  // [WIN][64]: x (forward) / dy (backward)
+  float* wl = lds + WIN * 64;        // [49][64] taps (flipped for the backward)
   const int nchunk = D / 64;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, cq = tid & 15, hf = (tid >> 4) & 1, orow = tid >> 5;
   const int chunk = blockIdx.x % nchunk, team = blockIdx.x / nchunk, b = blockIdx.y;
-  const int ch = chunk * 64 + lane;
+  const int ch0 = chunk * 64 + 4 * cq;
   const int ntc = (G + TC - 1) / TC, ntiles = ((G + TR - 1) / TR) * ntc;
   const float* sb = src + (size_t)b * S * D + D + chunk * 64;
-  const float* xb = BWD ? xw + (size_t)b * S * D + D + chunk * 64 : nullptr;
   float* yb = y + (size_t)b * S * D;
   const bool fuse = BWD && dp.out != nullptr;
   const uint64_t seed = fuse && dp.p > 0.f ? effective_seed(dp.seed0, dp.seed_ptr) : 0;
   if (team == 0) {
-    if (w == 0) {  // the class token passes through
+    const int lane = tid & 63, wv = tid >> 6, ch = chunk * 64 + lane;
+    if (wv == 0) {  // the class token passes through
       const float v = src[(size_t)b * S * D + ch];
       yb[ch] = v;
       if (fuse) droppad_store(dp, seed, b, S, D, 0, ch, v);
     }
     if (fuse)      // the front pad rows of dout are zero
-      for (int t = w; t < dp.pad; t += WALK_THREADS / 64) {
+      for (int t = wv; t < dp.pad; t += ST_THREADS / 64) {
         const size_t o = ((size_t)b * dp.n_pad + t) * D + ch;
         if (dp.dtype == TM_BF16) ((bf16*)dp.out)[o] = (bf16)0.f;
         else ((float*)dp.out)[o] = 0.f;
       }
   }
-  for (int t = w; t < NT; t += WALK_THREADS / 64) wl[t * 64 + lane] = wf[(size_t)(BWD ? NT - 1 - t : t) * D + ch];
-  const float bias = BWD ? 0.f : bf[ch];
-  float accw[BWD ? NT + 1 : 1];
+  for (int i = tid; i < NT * 16; i += ST_THREADS) {
+    const int t = i >> 4, q = (i & 15) * 4;
+    *(f32x4*)(wl + t * 64 + q) = ld4(wf + (size_t)(BWD ? NT - 1 - t : t) * D + chunk * 64 + q);
+  }
+  const f32x4 bias = BWD ? (f32x4){0.f, 0.f, 0.f, 0.f} : ld4(bf + ch0);
+  const __amdgpu_buffer_rsrc_t rs = tm_rsrc(sb, (unsigned)(G * G * D) * 4u);
+  f32x4 pa[ST_PER];
+  if (team < ntiles) fetch_window(pa, rs, team, ntc, G, D, tid);
+  for (int t = team; t < ntiles; t += nteam) {
+    __syncthreads();   // the previous tile's LDS reads are done (first pass: the taps are written)
+    stage_window(win, pa, tid);
+    __syncthreads();
+    if (t + nteam < ntiles) fetch_window(pa, rs, t + nteam, ntc, G, D, tid);   // in flight meanwhile
+    const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
+    f32x4 acc[4];
 #pragma unroll
-  for (int t = 0; t < (BWD ? NT + 1 : 1); ++t) accw[t] = 0.f;
+    for (int j = 0; j < 4; ++j) acc[j] = bias;
+#pragma unroll 1
+    for (int dy = 0; dy < KS; ++dy) {
+      const float* wr = win + ((orow + dy) * WC + 4 * hf) * 64 + 4 * cq;
+      f32x4 xv[4 + KS - 1], wt[KS];
+#pragma unroll
+      for (int ic = 0; ic < 4 + KS - 1; ++ic) xv[ic] = ld4(wr + ic * 64);
+#pragma unroll
+      for (int dx = 0; dx < KS; ++dx) wt[dx] = ld4(wl + (dy * KS + dx) * 64 + 4 * cq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int dx = 0; dx < KS; ++dx)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[j][e] = fmaf(wt[dx][e], xv[j + dx][e], acc[j][e]);
+    }
+    const int r = r0 + orow;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 4 * hf + j;
+      if (r < G && c < G) {
+        const int tok = 1 + r * G + c;
+        *(f32x4*)(yb + (size_t)tok * D + ch0) = acc[j];
+        if (fuse) droppad_store4(dp, seed, b, S, D, tok, ch0, acc[j]);
+      }
+    }
+  }
+}
 
-  // window pieces of tile t (zero outside the grid): piece i = cell i / 16, channels 4 (i % 16)
-  f32x4 pa[WALK_PER], pb[BWD ? WALK_PER : 1];
+__global__ __launch_bounds__(ST_THREADS) void ppeg_wgrad_walk_kernel(const float* __restrict__ x,
+                                                                    const float* __restrict__ dy_, int S, int G, int D,
+                                                                    int nteam, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* win = lds;                  // [WIN][64] x window
+  float* dyt = lds + WIN * 64;       // [TR * TC][64] dy tile
+  const int nchunk = D / 64;
+  const int tid = threadIdx.x, cq = tid & 15, g = tid >> 4;   // g < 14: tap row g >> 1, tile rows 4 (g & 1) ..
+  const int chunk = blockIdx.x % nchunk, team = blockIdx.x / nchunk, b = blockIdx.y;
+  const int ntc = (G + TC - 1) / TC, ntiles = ((G + TR - 1) / TR) * ntc;
+  const float* xb = x + (size_t)b * S * D + D + chunk * 64;
+  const float* gb = dy_ + (size_t)b * S * D + D + chunk * 64;
+  const int tdy = g >> 1, rs = g & 1;   // g = 14 / 15: the bias sums of tile rows 0-3 / 4-7
+  f32x4 accw[KS];
+#pragma unroll
+  for (int dx = 0; dx < KS; ++dx) accw[dx] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rx = tm_rsrc(xb, (unsigned)(G * G * D) * 4u), rg = tm_rsrc(gb, (unsigned)(G * G * D) * 4u);
+  f32x4 px[ST_PER], pg[DYT_PER];
   auto fetch = [&](int t) {
+    fetch_window(px, rx, t, ntc, G, D, tid);
     const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
 #pragma unroll
-    for (int u = 0; u < WALK_PER; ++u) {
-      const int i = u * WALK_THREADS + tid, cell = i >> 4, c4 = (i & 15) * 4;
-      const int rr = r0 - R + cell / WC, cc = c0 - R + cell % WC;
-      const bool in = i < WIN * 16 && rr >= 0 && rr < G && cc >= 0 && cc < G;
-      const size_t o = (size_t)(rr * G + cc) * D + c4;
-      pa[u] = in ? *(const f32x4*)(sb + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
-      if constexpr (BWD) pb[u] = in ? *(const f32x4*)(xb + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  auto stage = [&]() {
-#pragma unroll
-    for (int u = 0; u < WALK_PER; ++u) {
-      const int i = u * WALK_THREADS + tid;
-      if (i < WIN * 16) {
-        *(f32x4*)(win + (i >> 4) * 64 + (i & 15) * 4) = pa[u];
-        if constexpr (BWD) *(f32x4*)(winx + (i >> 4) * 64 + (i & 15) * 4) = pb[u];
-      }
+    for (int u = 0; u < DYT_PER; ++u) {
+      const int i = u * ST_THREADS + tid, cell = i >> 4, c4 = (i & 15) * 4;
+      const int rr = r0 + cell / TC, cc = c0 + cell % TC;
+      pg[u] = tm_bload4(rg, ((rr < G) & (cc < G)) ? (unsigned)((rr * G + cc) * D + c4) * 4u : TM_OOB);
     }
   };
   if (team < ntiles) fetch(team);
   for (int t = team; t < ntiles; t += nteam) {
-    __syncthreads();   // the previous tile's LDS reads are done
-    stage();
     __syncthreads();
-    if (t + nteam < ntiles) fetch(t + nteam);   // in flight through this tile's arithmetic
-    const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
-    float acc[TC];
+    stage_window(win, px, tid);
 #pragma unroll
-    for (int j = 0; j < TC; ++j) acc[j] = bias;
+    for (int u = 0; u < DYT_PER; ++u) {
+      const int i = u * ST_THREADS + tid;
+      *(f32x4*)(dyt + (i >> 4) * 64 + (i & 15) * 4) = pg[u];
+    }
+    __syncthreads();
+    if (t + nteam < ntiles) fetch(t + nteam);
+    if (g < 14) {
 #pragma unroll 1
-    for (int dy = 0; dy < KS; ++dy) {   // window row w + dy (rolled: the row's 14 + 7 values live at once)
-      float xv[WC], wt[KS];
+      for (int orow = 4 * rs; orow < 4 * rs + 4; ++orow) {
+        f32x4 gv[TC], xv[WC];
 #pragma unroll
-      for (int ic = 0; ic < WC; ++ic) xv[ic] = win[((w + dy) * WC + ic) * 64 + lane];
+        for (int j = 0; j < TC; ++j) gv[j] = ld4(dyt + (orow * TC + j) * 64 + 4 * cq);
 #pragma unroll
-      for (int dx = 0; dx < KS; ++dx) wt[dx] = wl[(dy * KS + dx) * 64 + lane];
+        for (int ic = 0; ic < WC; ++ic) xv[ic] = ld4(win + ((orow + tdy) * WC + ic) * 64 + 4 * cq);
 #pragma unroll
-      for (int oc = 0; oc < TC; ++oc)
+        for (int j = 0; j < TC; ++j)
 #pragma unroll
-        for (int dx = 0; dx < KS; ++dx) acc[oc] = fmaf(wt[dx], xv[oc + dx], acc[oc]);
-    }
-    const int r = r0 + w;
+          for (int dx = 0; dx < KS; ++dx)
 #pragma unroll
-    for (int oc = 0; oc < TC; ++oc) {
-      const int c = c0 + oc;
-      if (r < G && c < G) {
-        yb[(size_t)(1 + r * G + c) * D + ch] = acc[oc];
-        if (fuse) droppad_store(dp, seed, b, S, D, 1 + r * G + c, ch, acc[oc]);
+            for (int e = 0; e < 4; ++e) accw[dx][e] = fmaf(gv[j][e], xv[j + dx][e], accw[dx][e]);
       }
-    }
-    if constexpr (BWD) {
-      // dW[dy][dx] += dy(r, c) x(r + dy - 3, c + dx - 3): dy(r, c) = centre of the dy window
-      float gv[TC];
+    } else {
 #pragma unroll
-      for (int oc = 0; oc < TC; ++oc) {
-        gv[oc] = win[((w + R) * WC + oc + R) * 64 + lane];
-        accw[NT] += gv[oc];
-      }
-#pragma unroll
-      for (int dy = 0; dy < KS; ++dy) {   // unrolled: accw is indexed by dy at compile time
-        float xv[WC];
-#pragma unroll
-        for (int ic = 0; ic < WC; ++ic) xv[ic] = winx[((w + dy) * WC + ic) * 64 + lane];
-#pragma unroll
-        for (int oc = 0; oc < TC; ++oc)
-#pragma unroll
-          for (int dx = 0; dx < KS; ++dx) accw[dy * KS + dx] = fmaf(gv[oc], xv[oc + dx], accw[dy * KS + dx]);
-      }
+      for (int cell = 32 * rs; cell < 32 * rs + 32; ++cell) accw[0] += ld4(dyt + cell * 64 + 4 * cq);
     }
   }
-  if constexpr (BWD) {
-    __syncthreads();   // the windows are no longer read: the LDS takes the 8 waves' partials
-    float* red = lds;  // [8][64][NT + 1]
+  // partial slab [D][50] of this member: the two tile-row halves summed (rs 0 + rs 1) through LDS
+  __syncthreads();
+  float* red = lds;   // [2][16 quads][8 rows: 7 tap rows + bias][7][4]
+  {
+    const int trow = g < 14 ? tdy : 7;
+    float* o = red + (((size_t)rs * 16 + cq) * 8 + trow) * 28;
 #pragma unroll
-    for (int t = 0; t <= NT; ++t) red[(w * 64 + lane) * (NT + 1) + t] = accw[t];
-    __syncthreads();
-    float* dst = part + ((size_t)b * nteam + team) * D * (NT + 1) + (size_t)chunk * 64 * (NT + 1);
-    constexpr int E = 64 * (NT + 1);
-    for (int e = tid; e < E; e += WALK_THREADS) {
-      float s = 0.f;
-#pragma unroll
-      for (int v = 0; v < 8; ++v) s += red[v * E + e];
-      dst[e] = s;
-    }
+    for (int dx = 0; dx < KS; ++dx) *(f32x4*)(o + dx * 4) = accw[dx];
+  }
+  __syncthreads();
+  float* dst = part + ((size_t)b * nteam + team) * D * (NT + 1) + (size_t)chunk * 64 * (NT + 1);
+  for (int e = tid; e < 64 * (NT + 1); e += ST_THREADS) {
+    const int cl = e / (NT + 1), tp = e - cl * (NT + 1);          // channel of the chunk, tap (49 = bias)
+    const int q = cl >> 2, ce = cl & 3;
+    const int trow = tp == NT ? 7 : tp / KS, dx = tp == NT ? 0 : tp - (tp / KS) * KS;
+    const size_t i0 = (((size_t)0 * 16 + q) * 8 + trow) * 28 + dx * 4 + ce;
+    const size_t i1 = (((size_t)1 * 16 + q) * 8 + trow) * 28 + dx * 4 + ce;
+    dst[e] = red[i0] + red[i1];
   }
 }
 
@@ -258,28 +326,25 @@ extern "C" int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, c
 }
 
 // x, y: [B, S, D] fp32 with S = 1 + G*G.  y must not alias x.
-// team members of the walker per chunk: the forward (50 KB of LDS) two workgroups per CU, the
-// backward (100 KB) one
-static int walk_nteam(int G, int D, bool bwd) {
+// team members per chunk: two 61-65 KB workgroups per CU
+static int walk_nteam(int G, int D) {
   const int ntiles = ((G + TR - 1) / TR) * ((G + TC - 1) / TC);
-  const int nchunk = D / 64;
-  return walk_team(ntiles, (bwd ? 1 : 2) * tm_cu_count() / nchunk);
+  return walk_team(ntiles, 2 * tm_cu_count() / (D / 64));
 }
 
 // x, y: [B, S, D] fp32 with S = 1 + G*G.  y must not alias x.
 extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
                            void* stream) {
   TM_REQUIRE(x && y && x != y && D % 64 == 0 && G > 0 && B > 0, "ppeg_fwd: bad args");
-  const int nteam = walk_nteam(G, D, false);
-  tm_allow_smem(ppeg_walk_kernel<false>, walk_lds<false>());
-  ppeg_walk_kernel<false><<<dim3(nteam * (D / 64), B), WALK_THREADS, walk_lds<false>(), (hipStream_t)stream>>>(
-      x, nullptr, 1 + G * G, G, D, nteam, wfold, bfold, y, DropPad{}, nullptr);
+  const int nteam = walk_nteam(G, D);
+  ppeg_stencil_walk_kernel<false><<<dim3(nteam * (D / 64), B), ST_THREADS, ST_LDS, (hipStream_t)stream>>>(
+      x, 1 + G * G, G, D, nteam, wfold, bfold, y, DropPad{});
   TM_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
-  return (long long)B * walk_nteam(G, D, true) * D * (NT + 1) * (long long)sizeof(float);
+  return (long long)B * walk_nteam(G, D) * D * (NT + 1) * (long long)sizeof(float);
 }
 
 // dy: [B,S,D] upstream gradient; x: PPEG input.  dx written (=); weight grads written.
@@ -293,10 +358,12 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
   hipStream_t st = (hipStream_t)stream;
   const int S = 1 + G * G;
   const DropPad dp{dout, dtype, n_pad, pad, p, p > 0.f ? 1.f / (1.f - p) : 1.f, seed, seed_ptr};
-  const int nteam = walk_nteam(G, D, true);
-  tm_allow_smem(ppeg_walk_kernel<true>, walk_lds<true>());
-  ppeg_walk_kernel<true><<<dim3(nteam * (D / 64), B), WALK_THREADS, walk_lds<true>(), st>>>(
-      dy, x, S, G, D, nteam, wfold, nullptr, dx, dp, work);
+  const int nteam = walk_nteam(G, D);
+  const dim3 grid(nteam * (D / 64), B);
+  ppeg_stencil_walk_kernel<true><<<grid, ST_THREADS, ST_LDS, st>>>(dy, S, G, D, nteam, wfold, nullptr, dx, dp);
+  TM_CHECK_LAUNCH();
+  tm_allow_smem(ppeg_wgrad_walk_kernel, WG_LDS);
+  ppeg_wgrad_walk_kernel<<<grid, ST_THREADS, WG_LDS, st>>>(x, dy, S, G, D, nteam, work);
   TM_CHECK_LAUNCH();
   (void)dwsum;
   ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, B * nteam, D, dw7, db7, dw5, db5, dw3,
