@@ -7,8 +7,8 @@
 // ONE 7x7 depthwise stencil (w = w7 + pad(w5) + pad(w3) + delta, b = b7+b5+b3),
 // applied channel-last directly on the [B, S, D] fp32 residual stream: token
 // t = 1 + r*G + c (row-major, :71).  No transpose to NCHW, no padded copy.
-// Persistent workgroups walk tiles of grid cells x 64 channels staged through LDS (coalesced
-// 256-B channel-row loads, the next tile's window in flight during the current tile); HBM-bound.
+// Workgroups own tiles of grid cells x 32 channels staged through LDS (coalesced
+// 128-B channel-row loads, three workgroups per CU in flight); HBM-bound.
 #include "common.h"
 #include "../../include/transmil_hip.h"
 
@@ -39,7 +39,6 @@ __global__ void ppeg_fold_kernel(const float* __restrict__ w7, const float* __re
 // as 16-B pieces (a wave covers 4 cells x 64 channels: four 256-B segments).
 constexpr int TR = 8, TC = 8, WR = TR + KS - 1, WC = TC + KS - 1;  // 14 x 14 window
 constexpr int WIN = WR * WC;                                       // 196 cells
-constexpr int TILE_LDS = WIN * 64 * 4;                             // 50 KB
 
 // Backward only, optional: the next layer-backward's first step fused into the stencil's stores --
 // dout[b][pad + t][c] = T(keep(b*S + t, c) * scale * dx[b*S + t][c]) and zero pad rows, the
@@ -60,62 +59,50 @@ TM_DEV void droppad_store(const DropPad& dp, uint64_t seed, int b, int S, int D,
 }
 
 // ---------------------------------------------------------------------------
-// Persistent tile walkers (the step's PPEG launches).  The tiles of one 64-channel chunk belong to
-// a team of workgroups launched as blockIdx.x = chunk + nchunk * team, so with the round-robin
-// dispatch a chunk's team sits on ONE XCD (nchunk = 8): the 3-cell halo each 8 x 8 tile re-reads is
-// served by that XCD's L2 (the chunk's slice of a [B, S, 512] tensor is 2.1 MB).  A member walks
-// tiles team, team + nteam, ... (row-major: the team works on neighbouring tiles at the same time)
-// and requests the next tile's operands into registers before it computes the current one, so the
-// HBM / L2 round trip overlaps the arithmetic.
-//
-// Register blocking: a thread owns 4 channels (one 16-B LDS piece) and 4 cells, so one ds_read_b128
-// feeds 4 FMAs per tap it meets (the one-channel-per-lane form was LDS-instruction bound:
-// 0.38 ds_read_b32 per FMA against the ~0.25 the VALU rate allows).
+// Tile kernels (the step's PPEG launches): one 8 x 8 tile x 32 channels per 256-thread workgroup,
+// high occupancy instead of a software pipeline.  The kernels are bound by how many window bytes a
+// CU has in flight (one tile's loads, then its arithmetic): 32 channels keep a workgroup's LDS at
+// 43-50 KB so three run per CU, and the channel chunk rides in the low bits of blockIdx.x
+// (chunk = blockIdx.x % nchunk) so with the round-robin dispatch each XCD serves two chunks and the
+// 3-cell halo of neighbouring tiles is re-read from its L2.  Windows sit in LDS with a 48-dword
+// (192 B) cell stride: the 16-lane groups of ds_read_b128 then hit 16 distinct 16-B bank slots.
+// Register blocking: a thread owns 4 channels (one 16-B piece) and 2 cells, so a ds_read_b128
+// feeds 4 FMAs for each tap it meets.
 //   stencil (forward y = conv(x) + b; backward dx = conv_flipped(dy) + the fused dropout-pad store):
-//     256 threads = 16 channel quads x 2 column halves x 8 tile rows; per window row dy: 10 x-pieces
-//     + 7 tap pieces -> 4 cells x 7 taps x 4 channels (the same tap order as before: window rows,
-//     then columns).
-//   weight gradient dW[tap] += dy(cell) x(cell + tap - 3), db += dy(cell): 224 threads = 16 channel
-//     quads x 7 tap rows x 2 tile-row halves (+ 32 threads for db): per tile row, the dy row (8
-//     pieces) and the x window row (14 pieces) -> 7 taps x 8 cells x 4 channels, accumulated in
-//     registers over the member's tiles, then ONE [D][50] partial slab per member.
-constexpr int ST_THREADS = 256;
-constexpr int ST_PER = (WIN * 16 + ST_THREADS - 1) / ST_THREADS;   // 16-B window pieces per thread: 13
-constexpr int TAPS_LDS = NT * 64 * 4;                               // the chunk's folded taps: 12.25 KB
-constexpr int ST_LDS = TILE_LDS + TAPS_LDS;                         // 61.25 KB: two workgroups per CU
-constexpr int DYT_LDS = TR * TC * 64 * 4;                           // dy tile: 16 KB
-constexpr int WG_LDS = TILE_LDS + DYT_LDS;                          // 65 KB
-constexpr int DYT_PER = TR * TC * 16 / ST_THREADS;                  // 4
-
-// tiles per team member for a chunk of `ntiles` tiles and at most `cap` members: the balanced team size
-inline int walk_team(int ntiles, int cap) {
-  cap = cap < 1 ? 1 : cap;
-  const int per = (ntiles + cap - 1) / cap;
-  return (ntiles + per - 1) / per;
-}
+//     256 threads = 8 channel quads x 4 column pairs x 8 tile rows; per window row: 8 x-pieces +
+//     7 tap pieces -> 2 cells x 7 taps x 4 channels, taps in the fixed order window rows, columns.
+//   weight gradient dW[tap] += dy(cell) x(cell + tap - 3), db += dy(cell): 224 threads = 8 channel
+//     quads x 7 tap rows x 4 tile-row pairs (+ 32 threads for db), WT tiles along a tile row per
+//     workgroup, then ONE [D][50] partial slab per workgroup (fixed-order sums).
+constexpr int CW = 32;                        // channels per workgroup
+constexpr int NQ = CW / 4;                    // channel quads
+constexpr int CS = 48;                        // LDS cell stride (dwords)
+constexpr int WIN_LDS = WIN * CS * 4;         // 37.6 KB
+constexpr int TAP_LDS = NT * NQ * 16;         // 6.1 KB
+constexpr int ST_LDS = WIN_LDS + TAP_LDS;     // 43.8 KB: three workgroups per CU
+constexpr int DYT_LDS = TR * TC * CS * 4;     // 12 KB
+constexpr int WG_LDS = WIN_LDS + DYT_LDS;     // 49.7 KB
+constexpr int WIN_PER = (WIN * NQ + 255) / 256;   // 16-B window pieces per thread: 7
+constexpr int WT = 3;                         // tiles per weight-gradient workgroup
 
 TM_DEV f32x4 ld4(const float* p) { return *(const f32x4*)p; }
 
-// the window of tile t (zero outside the grid): piece i = cell i / 16, channel quad i % 16
-// (rsrc: the bag's G x G cells from `base`, bounds-checked: out-of-grid pieces read zeros)
-template <int PER>
-TM_DEV void fetch_window(f32x4 (&v)[PER], __amdgpu_buffer_rsrc_t rsrc, int t, int ntc, int G, int D, int tid) {
-  const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
-  const int c4 = (tid & 15) * 4;
+// the 14 x 14 window of the tile at (r0, c0) into LDS (zero outside the grid; rsrc: the bag's G x G
+// cells from this chunk's first channel, bounds-checked -> out-of-grid pieces read zeros)
+TM_DEV void load_window(float* win, __amdgpu_buffer_rsrc_t rsrc, int r0, int c0, int G, int D, int tid) {
+  f32x4 v[WIN_PER];
+  const int q4 = (tid & (NQ - 1)) * 4;
 #pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int cell = u * (ST_THREADS / 16) + (tid >> 4);
+  for (int u = 0; u < WIN_PER; ++u) {
+    const int cell = u * (256 / NQ) + tid / NQ;
     const int rr = r0 - R + cell / WC, cc = c0 - R + cell % WC;
     const bool in = (cell < WIN) & ((unsigned)rr < (unsigned)G) & ((unsigned)cc < (unsigned)G);
-    v[u] = tm_bload4(rsrc, in ? (unsigned)((rr * G + cc) * D + c4) * 4u : TM_OOB);
+    v[u] = tm_bload4(rsrc, in ? (unsigned)((rr * G + cc) * D + q4) * 4u : TM_OOB);
   }
-}
-template <int PER>
-TM_DEV void stage_window(float* win, const f32x4 (&v)[PER], int tid) {
 #pragma unroll
-  for (int u = 0; u < PER; ++u) {
-    const int i = u * ST_THREADS + tid;
-    if (i < WIN * 16) *(f32x4*)(win + (i >> 4) * 64 + (i & 15) * 4) = v[u];
+  for (int u = 0; u < WIN_PER; ++u) {
+    const int cell = u * (256 / NQ) + tid / NQ;
+    if (cell < WIN) *(f32x4*)(win + cell * CS + q4) = v[u];
   }
 }
 
@@ -131,129 +118,116 @@ TM_DEV void droppad_store4(const DropPad& dp, uint64_t seed, int b, int S, int D
   else *(f32x4*)((float*)dp.out + o) = v;
 }
 
+// grid (nchunk * ntiles, B), block 256
 template <bool BWD>
-__global__ __launch_bounds__(ST_THREADS) void ppeg_stencil_walk_kernel(const float* __restrict__ src, int S, int G,
-                                                                      int D, int nteam, const float* __restrict__ wf,
-                                                                      const float* __restrict__ bf,
-                                                                      float* __restrict__ y, DropPad dp) {
+__global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ src, int S, int G, int D,
+                                                          const float* __restrict__ wf, const float* __restrict__ bf,
+                                                          float* __restrict__ y, DropPad dp) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* win = lds;                  // [WIN][64]: x (forward) / dy (backward)
-  float* wl = lds + WIN * 64;        // [49][64] taps (flipped for the backward)
-  const int nchunk = D / 64;
-  const int tid = threadIdx.x, cq = tid & 15, hf = (tid >> 4) & 1, orow = tid >> 5;
-  const int chunk = blockIdx.x % nchunk, team = blockIdx.x / nchunk, b = blockIdx.y;
-  const int ch0 = chunk * 64 + 4 * cq;
-  const int ntc = (G + TC - 1) / TC, ntiles = ((G + TR - 1) / TR) * ntc;
-  const float* sb = src + (size_t)b * S * D + D + chunk * 64;
+  float* win = lds;                  // [WIN][CS]: x (forward) / dy (backward)
+  float* wl = lds + WIN * CS;        // [49][CW] taps (flipped for the backward)
+  const int nchunk = D / CW;
+  const int tid = threadIdx.x, cq = tid & (NQ - 1), cp = (tid / NQ) & 3, orow = tid >> 5;
+  const int chunk = blockIdx.x % nchunk, t = blockIdx.x / nchunk, b = blockIdx.y;
+  const int ntc = (G + TC - 1) / TC, r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
+  const int ch0 = chunk * CW + 4 * cq;
+  const float* sb = src + (size_t)b * S * D + D + chunk * CW;
   float* yb = y + (size_t)b * S * D;
   const bool fuse = BWD && dp.out != nullptr;
   const uint64_t seed = fuse && dp.p > 0.f ? effective_seed(dp.seed0, dp.seed_ptr) : 0;
-  if (team == 0) {
-    const int lane = tid & 63, wv = tid >> 6, ch = chunk * 64 + lane;
-    if (wv == 0) {  // the class token passes through
-      const float v = src[(size_t)b * S * D + ch];
-      yb[ch] = v;
-      if (fuse) droppad_store(dp, seed, b, S, D, 0, ch, v);
+  if (t == 0) {
+    const int c = chunk * CW + (tid & (CW - 1)), g = tid / CW;
+    if (g == 0) {  // the class token passes through
+      const float v = src[(size_t)b * S * D + c];
+      yb[c] = v;
+      if (fuse) droppad_store(dp, seed, b, S, D, 0, c, v);
     }
     if (fuse)      // the front pad rows of dout are zero
-      for (int t = wv; t < dp.pad; t += ST_THREADS / 64) {
-        const size_t o = ((size_t)b * dp.n_pad + t) * D + ch;
+      for (int p = g; p < dp.pad; p += 256 / CW) {
+        const size_t o = ((size_t)b * dp.n_pad + p) * D + c;
         if (dp.dtype == TM_BF16) ((bf16*)dp.out)[o] = (bf16)0.f;
         else ((float*)dp.out)[o] = 0.f;
       }
   }
-  for (int i = tid; i < NT * 16; i += ST_THREADS) {
-    const int t = i >> 4, q = (i & 15) * 4;
-    *(f32x4*)(wl + t * 64 + q) = ld4(wf + (size_t)(BWD ? NT - 1 - t : t) * D + chunk * 64 + q);
+  for (int i = tid; i < NT * NQ; i += 256) {
+    const int tp = i / NQ, q = (i % NQ) * 4;
+    *(f32x4*)(wl + tp * CW + q) = ld4(wf + (size_t)(BWD ? NT - 1 - tp : tp) * D + chunk * CW + q);
   }
+  load_window(win, tm_rsrc(sb, (unsigned)(G * G * D) * 4u), r0, c0, G, D, tid);
   const f32x4 bias = BWD ? (f32x4){0.f, 0.f, 0.f, 0.f} : ld4(bf + ch0);
-  const __amdgpu_buffer_rsrc_t rs = tm_rsrc(sb, (unsigned)(G * G * D) * 4u);
-  f32x4 pa[ST_PER];
-  if (team < ntiles) fetch_window(pa, rs, team, ntc, G, D, tid);
-  for (int t = team; t < ntiles; t += nteam) {
-    __syncthreads();   // the previous tile's LDS reads are done (first pass: the taps are written)
-    stage_window(win, pa, tid);
-    __syncthreads();
-    if (t + nteam < ntiles) fetch_window(pa, rs, t + nteam, ntc, G, D, tid);   // in flight meanwhile
-    const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
-    f32x4 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = bias;
+  __syncthreads();
+  f32x4 acc[2] = {bias, bias};
 #pragma unroll 1
-    for (int dy = 0; dy < KS; ++dy) {
-      const float* wr = win + ((orow + dy) * WC + 4 * hf) * 64 + 4 * cq;
-      f32x4 xv[4 + KS - 1], wt[KS];
+  for (int dy = 0; dy < KS; ++dy) {
+    const float* wr = win + ((orow + dy) * WC + 2 * cp) * CS + 4 * cq;
+    f32x4 xv[2 + KS - 1], wt[KS];
 #pragma unroll
-      for (int ic = 0; ic < 4 + KS - 1; ++ic) xv[ic] = ld4(wr + ic * 64);
+    for (int ic = 0; ic < 2 + KS - 1; ++ic) xv[ic] = ld4(wr + ic * CS);
 #pragma unroll
-      for (int dx = 0; dx < KS; ++dx) wt[dx] = ld4(wl + (dy * KS + dx) * 64 + 4 * cq);
+    for (int dx = 0; dx < KS; ++dx) wt[dx] = ld4(wl + (dy * KS + dx) * CW + 4 * cq);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int dx = 0; dx < KS; ++dx)
+      for (int dx = 0; dx < KS; ++dx)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[j][e] = fmaf(wt[dx][e], xv[j + dx][e], acc[j][e]);
-    }
-    const int r = r0 + orow;
+        for (int e = 0; e < 4; ++e) acc[j][e] = fmaf(wt[dx][e], xv[j + dx][e], acc[j][e]);
+  }
+  const int r = r0 + orow;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = c0 + 4 * hf + j;
-      if (r < G && c < G) {
-        const int tok = 1 + r * G + c;
-        *(f32x4*)(yb + (size_t)tok * D + ch0) = acc[j];
-        if (fuse) droppad_store4(dp, seed, b, S, D, tok, ch0, acc[j]);
-      }
+  for (int j = 0; j < 2; ++j) {
+    const int c = c0 + 2 * cp + j;
+    if (r < G && c < G) {
+      const int tok = 1 + r * G + c;
+      *(f32x4*)(yb + (size_t)tok * D + ch0) = acc[j];
+      if (fuse) droppad_store4(dp, seed, b, S, D, tok, ch0, acc[j]);
     }
   }
 }
 
-__global__ __launch_bounds__(ST_THREADS) void ppeg_wgrad_walk_kernel(const float* __restrict__ x,
-                                                                    const float* __restrict__ dy_, int S, int G, int D,
-                                                                    int nteam, float* __restrict__ part) {
+// grid (nchunk * ntr * ceil(ntc / WT), B), block 256; part: [B * ntr * ceil(ntc / WT)][D][50]
+__global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy_,
+                                                        int S, int G, int D, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* win = lds;                  // [WIN][64] x window
-  float* dyt = lds + WIN * 64;       // [TR * TC][64] dy tile
-  const int nchunk = D / 64;
-  const int tid = threadIdx.x, cq = tid & 15, g = tid >> 4;   // g < 14: tap row g >> 1, tile rows 4 (g & 1) ..
-  const int chunk = blockIdx.x % nchunk, team = blockIdx.x / nchunk, b = blockIdx.y;
-  const int ntc = (G + TC - 1) / TC, ntiles = ((G + TR - 1) / TR) * ntc;
-  const float* xb = x + (size_t)b * S * D + D + chunk * 64;
-  const float* gb = dy_ + (size_t)b * S * D + D + chunk * 64;
-  const int tdy = g >> 1, rs = g & 1;   // g = 14 / 15: the bias sums of tile rows 0-3 / 4-7
+  float* win = lds;                  // [WIN][CS] x window
+  float* dyt = lds + WIN * CS;       // [TR * TC][CS] dy tile
+  const int nchunk = D / CW;
+  const int tid = threadIdx.x, cq = tid & (NQ - 1), g = tid / NQ;   // g < 28: tap row g >> 2, tile rows 2 (g & 3) ..
+  const int chunk = blockIdx.x % nchunk, grp = blockIdx.x / nchunk, b = blockIdx.y;
+  const int ntc = (G + TC - 1) / TC, ngc = (ntc + WT - 1) / WT;
+  const int tr = grp / ngc, tc0 = (grp % ngc) * WT;
+  const float* xb = x + (size_t)b * S * D + D + chunk * CW;
+  const float* gb = dy_ + (size_t)b * S * D + D + chunk * CW;
+  const __amdgpu_buffer_rsrc_t rx = tm_rsrc(xb, (unsigned)(G * G * D) * 4u), rg = tm_rsrc(gb, (unsigned)(G * G * D) * 4u);
+  const int tdy = g >> 2, rp = g & 3;   // g = 28..31: the bias sums of tile rows 2 (g - 28) ..
+  const int r0 = tr * TR;
   f32x4 accw[KS];
 #pragma unroll
   for (int dx = 0; dx < KS; ++dx) accw[dx] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const __amdgpu_buffer_rsrc_t rx = tm_rsrc(xb, (unsigned)(G * G * D) * 4u), rg = tm_rsrc(gb, (unsigned)(G * G * D) * 4u);
-  f32x4 px[ST_PER], pg[DYT_PER];
-  auto fetch = [&](int t) {
-    fetch_window(px, rx, t, ntc, G, D, tid);
-    const int r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
+  for (int tc = tc0; tc < min(ntc, tc0 + WT); ++tc) {
+    const int c0 = tc * TC;
+    __syncthreads();   // the previous tile's LDS reads are done
+    {
+      const int q4 = cq * 4;
+      const int cell = tid / NQ;   // 32 cells per pass, 2 passes
+      f32x4 v[2];
 #pragma unroll
-    for (int u = 0; u < DYT_PER; ++u) {
-      const int i = u * ST_THREADS + tid, cell = i >> 4, c4 = (i & 15) * 4;
-      const int rr = r0 + cell / TC, cc = c0 + cell % TC;
-      pg[u] = tm_bload4(rg, ((rr < G) & (cc < G)) ? (unsigned)((rr * G + cc) * D + c4) * 4u : TM_OOB);
-    }
-  };
-  if (team < ntiles) fetch(team);
-  for (int t = team; t < ntiles; t += nteam) {
-    __syncthreads();
-    stage_window(win, px, tid);
+      for (int u = 0; u < 2; ++u) {
+        const int cl = cell + 32 * u, rr = r0 + cl / TC, cc = c0 + cl % TC;
+        v[u] = tm_bload4(rg, ((rr < G) & (cc < G)) ? (unsigned)((rr * G + cc) * D + q4) * 4u : TM_OOB);
+      }
+      load_window(win, rx, r0, c0, G, D, tid);
 #pragma unroll
-    for (int u = 0; u < DYT_PER; ++u) {
-      const int i = u * ST_THREADS + tid;
-      *(f32x4*)(dyt + (i >> 4) * 64 + (i & 15) * 4) = pg[u];
+      for (int u = 0; u < 2; ++u) *(f32x4*)(dyt + (cell + 32 * u) * CS + q4) = v[u];
     }
     __syncthreads();
-    if (t + nteam < ntiles) fetch(t + nteam);
-    if (g < 14) {
+    if (g < 28) {
 #pragma unroll 1
-      for (int orow = 4 * rs; orow < 4 * rs + 4; ++orow) {
+      for (int orow = 2 * rp; orow < 2 * rp + 2; ++orow) {
         f32x4 gv[TC], xv[WC];
 #pragma unroll
-        for (int j = 0; j < TC; ++j) gv[j] = ld4(dyt + (orow * TC + j) * 64 + 4 * cq);
+        for (int j = 0; j < TC; ++j) gv[j] = ld4(dyt + (orow * TC + j) * CS + 4 * cq);
 #pragma unroll
-        for (int ic = 0; ic < WC; ++ic) xv[ic] = ld4(win + ((orow + tdy) * WC + ic) * 64 + 4 * cq);
+        for (int ic = 0; ic < WC; ++ic) xv[ic] = ld4(win + ((orow + tdy) * WC + ic) * CS + 4 * cq);
 #pragma unroll
         for (int j = 0; j < TC; ++j)
 #pragma unroll
@@ -262,28 +236,30 @@ __global__ __launch_bounds__(ST_THREADS) void ppeg_wgrad_walk_kernel(const float
             for (int e = 0; e < 4; ++e) accw[dx][e] = fmaf(gv[j][e], xv[j + dx][e], accw[dx][e]);
       }
     } else {
+      const int bp = g - 28;
 #pragma unroll
-      for (int cell = 32 * rs; cell < 32 * rs + 32; ++cell) accw[0] += ld4(dyt + cell * 64 + 4 * cq);
+      for (int cell = 16 * bp; cell < 16 * bp + 16; ++cell) accw[0] += ld4(dyt + cell * CS + 4 * cq);
     }
   }
-  // partial slab [D][50] of this member: the two tile-row halves summed (rs 0 + rs 1) through LDS
+  // partial slab: the four tile-row pairs summed in a fixed order through LDS
   __syncthreads();
-  float* red = lds;   // [2][16 quads][8 rows: 7 tap rows + bias][7][4]
+  float* red = lds;   // [4 row pairs][8 tap rows: 7 + bias][NQ][7][4]
   {
-    const int trow = g < 14 ? tdy : 7;
-    float* o = red + (((size_t)rs * 16 + cq) * 8 + trow) * 28;
+    const int pr = g < 28 ? rp : g - 28, trow = g < 28 ? tdy : 7;
+    float* o = red + (((size_t)pr * 8 + trow) * NQ + cq) * 28;
 #pragma unroll
     for (int dx = 0; dx < KS; ++dx) *(f32x4*)(o + dx * 4) = accw[dx];
   }
   __syncthreads();
-  float* dst = part + ((size_t)b * nteam + team) * D * (NT + 1) + (size_t)chunk * 64 * (NT + 1);
-  for (int e = tid; e < 64 * (NT + 1); e += ST_THREADS) {
+  float* dst = part + ((size_t)b * (gridDim.x / nchunk) + grp) * D * (NT + 1) + (size_t)chunk * CW * (NT + 1);
+  for (int e = tid; e < CW * (NT + 1); e += 256) {
     const int cl = e / (NT + 1), tp = e - cl * (NT + 1);          // channel of the chunk, tap (49 = bias)
     const int q = cl >> 2, ce = cl & 3;
     const int trow = tp == NT ? 7 : tp / KS, dx = tp == NT ? 0 : tp - (tp / KS) * KS;
-    const size_t i0 = (((size_t)0 * 16 + q) * 8 + trow) * 28 + dx * 4 + ce;
-    const size_t i1 = (((size_t)1 * 16 + q) * 8 + trow) * 28 + dx * 4 + ce;
-    dst[e] = red[i0] + red[i1];
+    float s = 0.f;
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) s += red[(((size_t)pr * 8 + trow) * NQ + q) * 28 + dx * 4 + ce];
+    dst[e] = s;
   }
 }
 
@@ -326,25 +302,24 @@ extern "C" int tm_ppeg_fold(const float* w7, const float* b7, const float* w5, c
 }
 
 // x, y: [B, S, D] fp32 with S = 1 + G*G.  y must not alias x.
-// team members per chunk: two 61-65 KB workgroups per CU
-static int walk_nteam(int G, int D) {
-  const int ntiles = ((G + TR - 1) / TR) * ((G + TC - 1) / TC);
-  return walk_team(ntiles, 2 * tm_cu_count() / (D / 64));
+static int wgrad_groups(int G) {
+  const int ntc = (G + TC - 1) / TC;
+  return ((G + TR - 1) / TR) * ((ntc + WT - 1) / WT);
 }
 
 // x, y: [B, S, D] fp32 with S = 1 + G*G.  y must not alias x.
 extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
                            void* stream) {
-  TM_REQUIRE(x && y && x != y && D % 64 == 0 && G > 0 && B > 0, "ppeg_fwd: bad args");
-  const int nteam = walk_nteam(G, D);
-  ppeg_stencil_walk_kernel<false><<<dim3(nteam * (D / 64), B), ST_THREADS, ST_LDS, (hipStream_t)stream>>>(
-      x, 1 + G * G, G, D, nteam, wfold, bfold, y, DropPad{});
+  TM_REQUIRE(x && y && x != y && D % CW == 0 && G > 0 && B > 0, "ppeg_fwd: bad args");
+  const int ntiles = ((G + TR - 1) / TR) * ((G + TC - 1) / TC);
+  ppeg_stencil_kernel<false><<<dim3(ntiles * (D / CW), B), 256, ST_LDS, (hipStream_t)stream>>>(
+      x, 1 + G * G, G, D, wfold, bfold, y, DropPad{});
   TM_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
-  return (long long)B * walk_nteam(G, D) * D * (NT + 1) * (long long)sizeof(float);
+  return (long long)B * wgrad_groups(G) * D * (NT + 1) * (long long)sizeof(float);
 }
 
 // dy: [B,S,D] upstream gradient; x: PPEG input.  dx written (=); weight grads written.
@@ -352,22 +327,20 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
                            float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
                            float* db3, int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
                            const uint64_t* seed_ptr, void* stream) {
-  TM_REQUIRE(x && dy && dx && dx != dy && D % 64 == 0 && G > 0 && B > 0, "ppeg_bwd: bad args");
+  TM_REQUIRE(x && dy && dx && dx != dy && D % CW == 0 && G > 0 && B > 0, "ppeg_bwd: bad args");
   TM_REQUIRE(!dout || ((dtype == TM_BF16 || dtype == TM_F32) && n_pad >= pad + 1 + G * G && pad >= 0),
              "ppeg_bwd: bad dropout-pad output");
   hipStream_t st = (hipStream_t)stream;
   const int S = 1 + G * G;
   const DropPad dp{dout, dtype, n_pad, pad, p, p > 0.f ? 1.f / (1.f - p) : 1.f, seed, seed_ptr};
-  const int nteam = walk_nteam(G, D);
-  const dim3 grid(nteam * (D / 64), B);
-  ppeg_stencil_walk_kernel<true><<<grid, ST_THREADS, ST_LDS, st>>>(dy, S, G, D, nteam, wfold, nullptr, dx, dp);
+  const int ntiles = ((G + TR - 1) / TR) * ((G + TC - 1) / TC);
+  ppeg_stencil_kernel<true><<<dim3(ntiles * (D / CW), B), 256, ST_LDS, st>>>(dy, S, G, D, wfold, nullptr, dx, dp);
   TM_CHECK_LAUNCH();
-  tm_allow_smem(ppeg_wgrad_walk_kernel, WG_LDS);
-  ppeg_wgrad_walk_kernel<<<grid, ST_THREADS, WG_LDS, st>>>(x, dy, S, G, D, nteam, work);
+  ppeg_wgrad_kernel<<<dim3(wgrad_groups(G) * (D / CW), B), 256, WG_LDS, st>>>(x, dy, S, G, D, work);
   TM_CHECK_LAUNCH();
   (void)dwsum;
-  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, B * nteam, D, dw7, db7, dw5, db5, dw3,
-                                                                     db3);
+  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, B * wgrad_groups(G), D, dw7, db7, dw5,
+                                                                     db5, dw3, db3);
   TM_CHECK_LAUNCH();
   return 0;
 }
