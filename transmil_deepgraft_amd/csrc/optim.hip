@@ -27,6 +27,10 @@ namespace {
 
 constexpr int OPT_THREADS = 256, OPT_PIECES = 2, OPT_PER_BLOCK = OPT_THREADS * 4 * OPT_PIECES;
 
+__global__ void optim_tick_kernel(int* counters) {
+  counters[0] += 1;
+  counters[1] += 1;
+}
 
 struct RAdamScal {
   float bc1, bc2, rect;
@@ -101,10 +105,8 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
       }
     }
   }
-  // this call's step counts: the stored counts + 1 (every workgroup reads them before any write;
-  // the last workgroup to finish stores the advanced counts, below)
-  const float step = (float)(__hip_atomic_load(counters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1);
-  const int la_step = __hip_atomic_load(counters + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+  const float step = (float)counters[0];
+  const int la_step = counters[1];
   RAdamScal r;
   r.bc1 = 1.0f - powf(beta1, step);
   const float b2t = powf(beta2, step);
@@ -146,18 +148,6 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
       for (int e = 0; e < n; ++e) pc[u].param[pc[u].j0 + e] = p4[u][e];
     }
   }
-  // advance the step counts once every workgroup has read them: an arrival ticket in counters[2]
-  // (the scratch count); the workgroup that arrives last stores count + 1 and re-arms the ticket.
-  // (Replaces a separate one-thread launch before this kernel.)
-  __syncthreads();   // every wave of this workgroup has read the counts
-  if (threadIdx.x == 0) {
-    const int ticket = __hip_atomic_fetch_add(counters + 2, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (ticket == (int)gridDim.x - 1) {
-      __hip_atomic_store(counters, (int)step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(counters + 1, la_step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(counters + 2, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 }  // namespace
@@ -179,6 +169,7 @@ extern "C" int tm_radam_lookahead_step(const tm_optim_table* table, float* exp_a
   const long long total = table->offset[table->count];
   if (total == 0) return 0;
   const long long blocks = (total + OPT_PER_BLOCK - 1) / OPT_PER_BLOCK;
+  optim_tick_kernel<<<1, 1, 0, (hipStream_t)stream>>>(counters);
   radam_lookahead_kernel<<<(unsigned)blocks, OPT_THREADS, 0, (hipStream_t)stream>>>(
       *table, exp_avg, exp_avg_sq, slow, counters, beta1, beta2, eps, lookahead_k, lookahead_alpha);
   TM_CHECK_LAUNCH();
