@@ -295,6 +295,15 @@ int tm_gelu_bwd(int dtype, const float* dy, const float* pre, long long count, v
 /* y = max(a + b, 0) elementwise (the C5 encoder's residual add + ReLU, Bottleneck.forward,
  * code/models/ResNet.py:97-124); 16-B aligned, y may alias a */
 int tm_add_relu(int dtype, const void* a, const void* b, void* y, long long count, void* stream);
+/* y[r, c] = act(y[r, c] + bias[c]) in place over rows x C channels-last (C % 8 == 0; act = ReLU
+ * when relu != 0): a 3x3 convolution's folded conv+BN bias + ReLU (ResNet.py:95-104) in one pass */
+int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int relu, void* stream);
+/* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
+ * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T + bias[cout]
+ * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.
+ * residual may be NULL, must not alias y.  Returns 3 on a hipBLASLt error. */
+int tm_conv1x1(int dtype, const void* x, const void* w, const void* bias, const void* residual, void* y,
+               long long rows, int cin, int cout, int relu, void* stream);
 
 /* ---- class-row specialisation of the last TransLayer (clsrow.hip) -- code/models/TransMIL.py:195-203 ----
  * The logits read layer 2 only through the class token (norm(h)[:, 0]), which sits at row r = pad of

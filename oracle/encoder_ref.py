@@ -1,7 +1,9 @@
 """CPU oracle (test infrastructure only) for the C5 tile encoder: RetCCL ResNet-50 with
 ``fc = Identity`` as ``ModelInterface`` builds it (code/models/model_interface.py:238-245:
 ``ResNet.resnet50(num_classes=128, mlp=False, two_branch=False, normlinear=True)``), restated as a
-plain functional forward over a state_dict, eval-mode BatchNorm (running statistics).
+plain functional forward over a state_dict: eval-mode BatchNorm (running statistics) or, with
+``train=True``, train-mode BatchNorm (statistics of the whole batch, running statistics updated
+with ``momentum`` as nn.BatchNorm2d does -- the reference's frozen encoder under ``model.train()``).
 
 Follows code/models/ResNet.py:
   * stem: conv1 7x7/2 pad 3 -> bn1 -> ReLU -> maxpool 3/2 pad 1 (ResNet.forward :249-252);
@@ -25,7 +27,7 @@ BN_EPS = 1e-5
 
 def _bn(x, sd, pre):
     return F.batch_norm(x, sd[pre + ".running_mean"], sd[pre + ".running_var"], sd[pre + ".weight"],
-                        sd[pre + ".bias"], training=False, eps=BN_EPS)
+                        sd[pre + ".bias"], training=sd["__train__"], momentum=sd["__momentum__"], eps=BN_EPS)
 
 
 def _bottleneck(x, sd, pre, stride):
@@ -39,9 +41,14 @@ def _bottleneck(x, sd, pre, stride):
     return F.relu(out + idt)
 
 
-def features(tiles: torch.Tensor, state_dict: dict, dtype=torch.float64) -> torch.Tensor:
-    """tiles [n, 3, 224, 224] -> features [n, 2048] (``dtype`` arithmetic on the CPU)."""
-    sd = {k: v.detach().to("cpu", dtype) for k, v in state_dict.items() if not k.endswith("num_batches_tracked")}
+def features(tiles: torch.Tensor, state_dict: dict, dtype=torch.float64, train=False, momentum=0.1,
+             stats_out: dict | None = None) -> torch.Tensor:
+    """tiles [n, 3, 224, 224] -> features [n, 2048] (``dtype`` arithmetic on the CPU).  With
+    ``train``: batch-statistics BatchNorm over all n tiles; the updated running statistics go into
+    ``stats_out`` (name -> tensor) when given."""
+    sd = {k: v.detach().to("cpu", dtype).clone() for k, v in state_dict.items()
+          if not k.endswith("num_batches_tracked")}
+    sd["__train__"], sd["__momentum__"] = bool(train), momentum
     x = tiles.detach().to("cpu", dtype)
     x = F.relu(_bn(F.conv2d(x, sd["conv1.weight"], stride=2, padding=3), sd, "bn1"))
     x = F.max_pool2d(x, 3, 2, 1)
@@ -49,4 +56,6 @@ def features(tiles: torch.Tensor, state_dict: dict, dtype=torch.float64) -> torc
         for bi in range(nb):
             stride = 2 if (li > 1 and bi == 0) else 1
             x = _bottleneck(x, sd, f"layer{li}.{bi}", stride)
+    if stats_out is not None:
+        stats_out.update({k: v for k, v in sd.items() if k.endswith(("running_mean", "running_var"))})
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -181,3 +181,64 @@ def test_c5_full_bag_4096_tiles(enc_dtype, mil_dtype, rtol, ltol, gtol):
     assert all(p.grad is None for p in enc.parameters())
     moved = max((p.detach() - before[n]).abs().max().item() for n, p in ours.named_parameters())
     assert 0 < moved < 1 and all(torch.isfinite(p).all() for p in ours.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,rtol,stol", [(torch.float32, 2e-3, 1e-3), (torch.bfloat16, 6e-2, 3e-2)])
+def test_train_mode_bn_uses_whole_bag_statistics(dtype, rtol, stol):
+    """Train-mode encoder (frozen parameters, BatchNorm in training mode, as the reference's
+    model_ft under Lightning's model.train()): the batch statistics span every tile of the bag,
+    because ModelInterface.forward feeds model_ft the whole [B*bag] batch in one call
+    (model_interface.py:303-309).  With chunk (2) < bag (6) the features and the updated running
+    statistics still equal the fp64 oracle's whole-batch train-mode BN."""
+    from oracle.encoder_ref import features
+    enc = _encoder(dtype)
+    enc.chunk = 2
+    sd0 = {k: v.clone() for k, v in enc.state_dict().items()}
+    enc = enc.cuda().train()
+    x = torch.from_numpy(encoder_tiles(6, seed=3))
+    with torch.no_grad():
+        got = enc(x.cuda()).double().cpu()
+    stats = {}
+    ref = features(x, sd0, train=True, momentum=0.1, stats_out=stats)
+    err = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert err < rtol, err
+    sd = enc.state_dict()
+    worst = max(((sd[k].double().cpu() - v).abs().max() / v.abs().max().clamp_min(1e-6)).item()
+                for k, v in stats.items())
+    assert worst < stol, worst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("rows,cin,cout", [(3136 * 2, 64, 256), (49 * 3 + 5, 512, 2048), (100, 1024, 256)])
+@pytest.mark.parametrize("relu,res", [(True, True), (True, False), (False, False)])
+def test_conv1x1_epilogue_matches_torch(dtype, tol, rows, cin, cout, relu, res):
+    """tm_conv1x1 (hipBLASLt GEMM, bias / residual / ReLU epilogue) against an fp32 torch
+    reference act(x w^T + b (+ r)) -- the order ResNet.py:95-117 applies them."""
+    from transmil_deepgraft_amd import _lib
+    from transmil_deepgraft_amd.encoder import _dtype_code
+    from transmil_deepgraft_amd.engine import _p, _stream
+    g = torch.Generator(device="cuda").manual_seed(rows + cin)
+    x = torch.randn(rows, cin, device="cuda", generator=g).to(dtype)
+    w = (torch.randn(cout, cin, device="cuda", generator=g) / cin ** 0.5).to(dtype)
+    b = torch.randn(cout, device="cuda", generator=g).to(dtype)
+    r = torch.randn(rows, cout, device="cuda", generator=g).to(dtype) if res else None
+    y = torch.full((rows, cout), float("nan"), device="cuda", dtype=dtype)
+    _lib.call("tm_conv1x1", _dtype_code(x), _p(x), _p(w), _p(b), _p(r), _p(y), rows, cin, cout, int(relu), _stream())
+    ref = x.float() @ w.float().t() + b.float() + (r.float() if res else 0)
+    ref = ref.clamp_min(0) if relu else ref
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bias_act_matches_torch(dtype):
+    from transmil_deepgraft_amd.encoder import _bias_act_
+    g = torch.Generator(device="cuda").manual_seed(5)
+    y = torch.randn(3, 128, 7, 9, device="cuda", generator=g).to(dtype).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(128, device="cuda", generator=g).to(dtype)
+    ref = (y.float() + b.float()[None, :, None, None]).clamp_min(0).to(dtype)
+    out = _bias_act_(y, b)
+    assert out.data_ptr() == y.data_ptr()
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)

@@ -128,6 +128,8 @@ _SIGS = {
     "tm_ce_bwd": (I, [P, P, I, I, P, P, P]),
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_add_relu": (I, [I, P, P, P, L, P]),
+    "tm_bias_act": (I, [I, P, P, L, I, I, P]),
+    "tm_conv1x1": (I, [I, P, P, P, P, P, L, I, I, I, P]),
     "tm_cls_a1_row_fwd": (I, [I, P, P, P, P, P, I, I, I, I, P, P, P]),
     "tm_cls_out_fwd": (I, [I, P, P, P, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_cls_out_bwd": (I, [I, P, P, P, I, I, I, I, I, Fl, U64, P, P, P, P, P]),

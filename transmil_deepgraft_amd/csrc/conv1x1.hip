@@ -1,0 +1,142 @@
+// C5 tile encoder: a 1x1 convolution over channels-last activations is a GEMM over their
+// [rows = n*h*w, cin] matrix.  Runs it as a hipBLASLt GEMM whose epilogue adds the folded
+// conv+BN bias, the Bottleneck's residual (beta = 1 on the C operand) and applies the ReLU
+// (code/models/ResNet.py:95-117: conv3 -> bn3 -> out + identity -> ReLU), so the block output is
+// written once instead of GEMM store + a separate add/ReLU pass re-reading it (the add/ReLU pass
+// was 19 % of the C5 eval kernel time at HBM speed, profiles/r04_c5_kernel_summary.txt).
+//
+// Column-major view (hipBLASLt): D^T [cout x rows] = W [cout x cin] . X^T [cin x rows], i.e.
+// A = W stored [cout][cin] (col-major cin x cout, op T), B = X stored [rows][cin] (col-major
+// cin x rows, op N), C = residual and D = y stored [rows][cout] (col-major cout x rows); the
+// bias vector has one entry per D row (cout).  Plans (descriptors + heuristic algorithm) are cached
+// per shape; one handle and workspace per device.  A library GEMM, not a hand-written kernel: the
+// encoder is frozen and outside the NystromAttention / PPEG hot path.
+#include "common.h"
+
+#include <hipblaslt/hipblaslt.h>
+
+#include <map>
+#include <mutex>
+#include <tuple>
+
+namespace {
+
+constexpr size_t kWorkspace = 32u << 20;
+constexpr int kMaxDev = 16;
+
+struct Device {
+  hipblasLtHandle_t handle = nullptr;
+  void* ws = nullptr;
+};
+
+struct Plan {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, cd = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+  size_t ws = 0;
+};
+
+using Key = std::tuple<int, int, int, int, long long, int, int>;   // dev dtype relu res rows cin cout
+
+std::mutex g_mu;
+Device g_dev[kMaxDev];
+std::map<Key, Plan> g_plans;
+
+const char* lt_error(hipblasStatus_t s) {
+  switch (s) {
+    case HIPBLAS_STATUS_NOT_INITIALIZED: return "conv1x1: hipBLASLt not initialized";
+    case HIPBLAS_STATUS_ALLOC_FAILED: return "conv1x1: hipBLASLt allocation failed";
+    case HIPBLAS_STATUS_INVALID_VALUE: return "conv1x1: hipBLASLt invalid value";
+    case HIPBLAS_STATUS_NOT_SUPPORTED: return "conv1x1: hipBLASLt: shape/epilogue not supported";
+    case HIPBLAS_STATUS_EXECUTION_FAILED: return "conv1x1: hipBLASLt execution failed";
+    default: return "conv1x1: hipBLASLt error";
+  }
+}
+
+#define LT_CHECK(expr)                                                        \
+  do {                                                                        \
+    hipblasStatus_t s__ = (expr);                                             \
+    if (s__ != HIPBLAS_STATUS_SUCCESS) { tm_set_error(lt_error(s__)); return 3; } \
+  } while (0)
+
+int device_state(int dev, Device** out) {
+  Device& d = g_dev[dev];
+  if (!d.handle) {
+    LT_CHECK(hipblasLtCreate(&d.handle));
+    if (hipMalloc(&d.ws, kWorkspace) != hipSuccess) {
+      tm_set_error("conv1x1: workspace allocation failed");
+      return 2;
+    }
+  }
+  *out = &d;
+  return 0;
+}
+
+int make_plan(Device& d, int dtype, int relu, int res, long long rows, int cin, int cout, Plan* p) {
+  const hipDataType t = dtype == TM_BF16 ? HIP_R_16BF : HIP_R_32F;
+  LT_CHECK(hipblasLtMatmulDescCreate(&p->desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
+  const hipblasOperation_t opA = HIPBLAS_OP_T, opB = HIPBLAS_OP_N;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
+  const hipblasLtEpilogue_t epi = relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
+  const int32_t bt = (int32_t)t;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p->a, t, (uint64_t)cin, (uint64_t)cout, (int64_t)cin));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p->b, t, (uint64_t)cin, (uint64_t)rows, (int64_t)cin));
+  LT_CHECK(hipblasLtMatrixLayoutCreate(&p->cd, t, (uint64_t)cout, (uint64_t)rows, (int64_t)cout));
+  hipblasLtMatmulPreference_t pref = nullptr;
+  LT_CHECK(hipblasLtMatmulPreferenceCreate(&pref));
+  const uint64_t wsb = kWorkspace;
+  hipblasStatus_t s = hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
+                                                            &wsb, sizeof(wsb));
+  hipblasLtMatmulHeuristicResult_t r[1];
+  int n = 0;
+  if (s == HIPBLAS_STATUS_SUCCESS)
+    s = hipblasLtMatmulAlgoGetHeuristic(d.handle, p->desc, p->a, p->b, p->cd, p->cd, pref, 1, r, &n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  LT_CHECK(s);
+  (void)res;
+  if (n < 1) {
+    tm_set_error("conv1x1: hipBLASLt found no algorithm for this shape/epilogue");
+    return 3;
+  }
+  p->algo = r[0].algo;
+  p->ws = r[0].workspaceSize;
+  return 0;
+}
+
+}  // namespace
+
+// y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T + bias[cout] (+ residual[rows, cout])),
+// act = ReLU when relu != 0.  Row-major buffers (channels-last activations), dtype TM_BF16 or
+// TM_F32 for all of x, w, bias, residual, y (fp32 accumulation); residual may be NULL and must
+// not alias y.
+extern "C" int tm_conv1x1(int dtype, const void* x, const void* w, const void* bias, const void* residual,
+                          void* y, long long rows, int cin, int cout, int relu, void* stream) {
+  TM_REQUIRE(x && w && bias && y && rows >= 0 && cin > 0 && cout > 0, "conv1x1: bad args");
+  TM_REQUIRE(dtype == TM_BF16 || dtype == TM_F32, "conv1x1: dtype");
+  TM_REQUIRE(residual != y, "conv1x1: residual must not alias the output");
+  if (rows == 0) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) {
+    tm_set_error("conv1x1: no current device");
+    return 2;
+  }
+  std::lock_guard<std::mutex> lock(g_mu);
+  Device* d = nullptr;
+  if (int rc = device_state(dev, &d)) return rc;
+  const Key key{dev, dtype, relu ? 1 : 0, residual ? 1 : 0, rows, cin, cout};
+  auto it = g_plans.find(key);
+  if (it == g_plans.end()) {
+    Plan p;
+    if (int rc = make_plan(*d, dtype, relu ? 1 : 0, residual ? 1 : 0, rows, cin, cout, &p)) return rc;
+    it = g_plans.emplace(key, p).first;
+  }
+  Plan& p = it->second;
+  LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
+  const float alpha = 1.f, beta = residual ? 1.f : 0.f;
+  LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, w, p.a, x, p.b, &beta, residual ? residual : y, p.cd, y, p.cd,
+                           &p.algo, d->ws, p.ws, (hipStream_t)stream));
+  return 0;
+}

@@ -190,6 +190,23 @@ __global__ __launch_bounds__(256) void add_relu_kernel(const T* __restrict__ a, 
   }
 }
 
+// y[r, c] = act(y[r, c] + bias[c]) in place over channels-last rows of C channels (C % 8 == 0):
+// the C5 encoder's 3x3 convolutions' folded conv+BN bias and ReLU in one pass (MIOpen's
+// convolution + a bias add + a ReLU clamp were two extra read+write passes).
+template <typename T>
+__global__ __launch_bounds__(256) void bias_act_kernel(T* y, const T* __restrict__ bias, long long count, int C,
+                                                       int relu) {
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= count) return;
+  const int c = (int)(i % C);
+  const vec8<T> x = load8(y + i), b = load8(bias + c);
+  vec8<T> o;
+  const float lo = relu ? 0.f : -INFINITY;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = from_f<T>(fmaxf(to_f(x[e]) + to_f(b[e]), lo));
+  store8<T>(y + i, o);
+}
+
 }  // namespace
 
 // CrossEntropyLoss(logits, one_hot(label).float()) averaged over the B rows
@@ -349,6 +366,24 @@ extern "C" int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* str
   const long long threads = (off + 3) / 4;
   TM_DTYPE_DISPATCH(dtype, (cast_many_kernel<T><<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
                                *table)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int relu, void* stream) {
+  TM_REQUIRE(y && bias && rows >= 0 && C > 0 && C % 8 == 0, "bias_act: bad args (C % 8 == 0)");
+  TM_REQUIRE(((uintptr_t)y % 16) == 0 && ((uintptr_t)bias % 16) == 0, "bias_act: 16-B aligned buffers");
+  const long long count = rows * (long long)C;
+  if (count == 0) return 0;
+  const unsigned blocks = (unsigned)((count + 2047) / 2048);
+  if (dtype == TM_BF16)
+    bias_act_kernel<bf16><<<blocks, 256, 0, (hipStream_t)stream>>>((bf16*)y, (const bf16*)bias, count, C, relu);
+  else if (dtype == TM_F32)
+    bias_act_kernel<float><<<blocks, 256, 0, (hipStream_t)stream>>>((float*)y, (const float*)bias, count, C, relu);
+  else {
+    tm_set_error("bias_act: dtype");
+    return 1;
+  }
   TM_CHECK_LAUNCH();
   return 0;
 }

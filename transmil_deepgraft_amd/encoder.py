@@ -13,12 +13,15 @@ Same module / parameter / buffer names as code/models/ResNet.py (ResNet :130-277
   the encoder is frozen and outside the hand-written NystromAttention/PPEG path;
 * in eval mode every BatchNorm is folded into its convolution once (weights rescaled, bias
   added) -- no separate normalisation passes -- and every 1x1 convolution (36 of the 53) runs
-  as a hipBLASLt GEMM over the channels-last [n*h*w, c] rows with the bias (+ ReLU) epilogue;
+  as a hipBLASLt GEMM over the channels-last [n*h*w, c] rows (csrc/conv1x1.hip) whose epilogue
+  adds the bias, the residual (conv3) and applies the ReLU; the 3x3 convolutions' bias + ReLU is
+  one in-place HIP pass (tm_bias_act);
 * in train mode the BatchNorms run as written (batch statistics, running-stat updates), as the
   reference's frozen-but-train-mode encoder does under Lightning;
-* tiles go through in chunks (``chunk`` tiles, default 512) so the activation peak stays a few
-  GB whatever the bag size, and the [B*bag, 2048] features stay on the device for the fused
-  TransMIL engine (no host round trip).
+* in eval mode tiles go through in chunks (``chunk`` tiles, default 512; per-tile math, so the
+  chunking is exact) so the activation peak stays a few GB whatever the bag size; in train mode
+  the whole batch goes through at once, since batch statistics span it; the [B*bag, 2048]
+  features stay on the device for the fused TransMIL engine (no host round trip).
 """
 from __future__ import annotations
 
@@ -60,16 +63,40 @@ def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, dtype, cl=True):
     return w.contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format), b
 
 
-def _add_relu_(y, idt):
-    """y = relu(y + idt) in place, one HIP pass (tm_add_relu) over two channels-last tensors."""
-    from . import _lib
+def _dtype_code(t):
     from ._lib import BF16, F32
+    if t.dtype not in (torch.bfloat16, torch.float32):
+        raise RuntimeError("encoder: bf16 or fp32 tensors expected")
+    return BF16 if t.dtype == torch.bfloat16 else F32
+
+
+def _conv1x1_gemm(x, w, b, relu, residual=None):
+    """1x1 convolution (BN folded) over a channels-last tensor as one hipBLASLt GEMM over its
+    [n*h*w, c] rows with the bias (+ residual) (+ ReLU) epilogue (tm_conv1x1)."""
+    from . import _lib
     from .engine import _p, _stream
     cl = torch.channels_last
-    if y.shape != idt.shape or y.dtype != idt.dtype or not (y.is_contiguous(memory_format=cl) and
-                                                            idt.is_contiguous(memory_format=cl)):
-        raise RuntimeError("add_relu: channels-last operands of one shape and dtype expected")
-    _lib.call("tm_add_relu", BF16 if y.dtype == torch.bfloat16 else F32, _p(y), _p(idt), _p(y), y.numel(), _stream())
+    n, c, h, wd = x.shape
+    cout = w.shape[0]
+    if not x.is_contiguous(memory_format=cl) or w.dtype != x.dtype or b.dtype != x.dtype:
+        raise RuntimeError("conv1x1: channels-last input, weight and bias of one dtype expected")
+    y = torch.empty((n, h, wd, cout), dtype=x.dtype, device=x.device).permute(0, 3, 1, 2)
+    if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or
+                                 not residual.is_contiguous(memory_format=cl)):
+        raise RuntimeError("conv1x1: channels-last residual of the output's shape and dtype expected")
+    _lib.call("tm_conv1x1", _dtype_code(x), _p(x), _p(w.contiguous()), _p(b), _p(residual) if residual is not None else None,
+              _p(y), n * h * wd, c, cout, int(relu), _stream())
+    return y
+
+
+def _bias_act_(y, b, relu=True):
+    """y = act(y + b[channel]) in place over a channels-last tensor, one HIP pass (tm_bias_act)."""
+    from . import _lib
+    from .engine import _p, _stream
+    if not y.is_contiguous(memory_format=torch.channels_last):
+        y = y.contiguous(memory_format=torch.channels_last)
+    n, c, h, wd = y.shape
+    _lib.call("tm_bias_act", _dtype_code(y), _p(y), _p(b), n * h * wd, c, int(relu), _stream())
     return y
 
 
@@ -150,29 +177,28 @@ class RetCCLResNet50(nn.Module):
                                     _fold(blk.conv3, blk.bn3, dt, cl), d))
         self._folded = f
 
-    def _conv1x1(self, x, w, b, relu, stride=1):
-        """A 1x1 convolution over a channels-last tensor IS a GEMM over its [n*h*w, c] rows:
-        hipBLASLt with the bias (+ ReLU) epilogue instead of a MIOpen convolution."""
-        if stride != 1:
-            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
-        n, c, h, wd = x.shape
-        X = x.permute(0, 2, 3, 1).reshape(n * h * wd, c)
-        W = w.reshape(w.shape[0], c).t()
-        Y = torch._addmm_activation(b, X, W) if relu else torch.addmm(b, X, W)
-        return Y.view(n, h, wd, -1).permute(0, 3, 1, 2)
-
     def _forward_folded(self, x):
+        """Eval mode, BN folded.  On the GPU with channels-last activations: every 1x1 convolution
+        one hipBLASLt GEMM with its epilogue (conv1: bias + ReLU; downsample: bias; conv3: bias +
+        residual + ReLU -- the block output is written once), the 3x3 / stem convolutions through
+        MIOpen without bias, then bias + ReLU in one in-place pass."""
         f = self._folded
-        gemm1x1 = self.channels_last and x.is_cuda
         w, b = f["stem"]
+        if self.channels_last and x.is_cuda:
+            x = F.max_pool2d(_bias_act_(F.conv2d(x, w, None, stride=2, padding=3), b), 3, 2, 1)
+            for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
+                y = _conv1x1_gemm(x, w1, b1, True)
+                y = _bias_act_(F.conv2d(y, w2, None, stride=s2, padding=1), b2)
+                if d is None:
+                    idt = x
+                else:
+                    s = d[2][0]
+                    xs = x if s == 1 else x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
+                    idt = _conv1x1_gemm(xs, d[0], d[1], False)
+                x = _conv1x1_gemm(y, w3, b3, True, residual=idt)
+            return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         x = F.max_pool2d(F.relu(F.conv2d(x, w, b, stride=2, padding=3)), 3, 2, 1)
         for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
-            if gemm1x1:
-                y = self._conv1x1(x, w1, b1, True)
-                y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
-                idt = x if d is None else self._conv1x1(x, d[0], d[1], False, d[2][0])
-                x = _add_relu_(self._conv1x1(y, w3, b3, False), idt)
-                continue
             y = F.relu(F.conv2d(x, w1, b1))
             y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
             y = F.conv2d(y, w3, b3)
@@ -199,14 +225,18 @@ class RetCCLResNet50(nn.Module):
                 not self.conv1.weight.is_contiguous(memory_format=torch.channels_last):
             self.to(memory_format=torch.channels_last)
         grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        # train-mode BatchNorm normalises with the statistics of the whole [B*bag] batch the
+        # reference feeds model_ft in one call (model_interface.py:303-309): no chunking there
+        # (a 4096-tile bag's activations are tens of GB, well inside one GPU's HBM)
+        chunk = x.shape[0] if self.training else self.chunk
         with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16,
                                                           enabled=self.training and dt == torch.bfloat16):
-            for s in range(0, x.shape[0], self.chunk):
-                xc = x[s:s + self.chunk].to(dt if not self.training else torch.float32)
+            for s in range(0, x.shape[0], chunk):
+                xc = x[s:s + chunk].to(dt if not self.training else torch.float32)
                 xc = xc.contiguous(memory_format=torch.channels_last if self.channels_last
                                    else torch.contiguous_format)
                 y = self._forward_folded(xc) if not self.training else self._forward_modules(xc)
-                out[s:s + self.chunk] = y.float()
+                out[s:s + chunk] = y.float()
         return out
 
 
