@@ -299,11 +299,26 @@ int tm_add_relu(int dtype, const void* a, const void* b, void* y, long long coun
  * when relu != 0): a 3x3 convolution's folded conv+BN bias + ReLU (ResNet.py:95-104) in one pass */
 int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int relu, void* stream);
 /* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
- * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T + bias[cout]
+ * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout])
  * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.
- * residual may be NULL, must not alias y.  Returns 3 on a hipBLASLt error. */
+ * bias / residual may be NULL; residual must not alias y.  Returns 3 on a hipBLASLt error. */
 int tm_conv1x1(int dtype, const void* x, const void* w, const void* bias, const void* residual, void* y,
                long long rows, int cin, int cout, int relu, void* stream);
+/* Train-mode BatchNorm2d over a channels-last activation given as npieces (1..64) row pieces
+ * xs[p] of [rows[p], C] (host arrays; C a power of two, 8..2048; nn.BatchNorm2d.forward in
+ * training, code/models/ResNet.py:95-117 under model.train()): batch statistics over all pieces
+ * (biased variance for the normalisation) -> scale = gamma / sqrt(var + eps), shift = beta -
+ * mean * scale (fp32 [C]); running_mean / running_var (may be NULL) updated with the unbiased
+ * variance and momentum.  workspace >= tm_bn_train_workspace(C) floats. */
+long long tm_bn_train_workspace(int C);
+int tm_bn_train_stats(int dtype, const void* const* xs, const long long* rows, int npieces, int C,
+                      const float* gamma, const float* beta, float* running_mean, float* running_var,
+                      float momentum, float eps, float* scale, float* shift, float* workspace, long long ws_floats,
+                      void* stream);
+/* y = act(y * scale[c] + shift[c] (+ residual | + residual * rscale[c] + rshift[c])) in place over
+ * rows x C channels-last (C % 8 == 0): BN apply + ReLU, or bn3 + (BN'd) identity + ReLU, one pass */
+int tm_bn_apply(int dtype, void* y, const float* scale, const float* shift, const void* residual,
+                const float* rscale, const float* rshift, long long rows, int C, int relu, void* stream);
 
 /* ---- class-row specialisation of the last TransLayer (clsrow.hip) -- code/models/TransMIL.py:195-203 ----
  * The logits read layer 2 only through the class token (norm(h)[:, 0]), which sits at row r = pad of

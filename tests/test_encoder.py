@@ -242,3 +242,45 @@ def test_bias_act_matches_torch(dtype):
     out = _bias_act_(y, b)
     assert out.data_ptr() == y.data_ptr()
     torch.testing.assert_close(out, ref, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,C", [(4096 * 49, 2048), (512 * 3136 + 7, 64), (33, 256)])
+def test_bn_train_kernels_match_fp64(dtype, rows, C):
+    """tm_bn_train_stats / tm_bn_apply against fp64 batch statistics on the same (rounded)
+    input: values offset by 3 with spread 0.5 (E[x^2] - E[x]^2 would cancel in fp32 without the
+    shift), running statistics with momentum 0.1 and the unbiased variance (nn.BatchNorm2d)."""
+    from transmil_deepgraft_amd.encoder import _bn_apply_, _bn_train_stats
+    g = torch.Generator(device="cuda").manual_seed(rows % 1000 + C)
+    x = (3 + 0.5 * torch.randn(rows, C, device="cuda", generator=g)).to(dtype)
+    x4 = x.view(1, rows, 1, C).permute(0, 3, 1, 2)               # channels-last [1, C, rows, 1]
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5, generator=g)
+        bn.bias.uniform_(-0.2, 0.2, generator=g)
+    rm0, rv0 = bn.running_mean.clone(), bn.running_var.clone()
+    ws = torch.empty(4 * 2048 * 2048, device="cuda")
+    cut = rows // 3 if rows > 64 else rows          # two pieces (or one): statistics span them
+    st = _bn_train_stats([x4[:, :, :cut]] + ([x4[:, :, cut:]] if cut < rows else []), bn, ws)
+    xd = x.double()
+    mean, var = xd.mean(0), xd.var(0, unbiased=False)
+    sc = bn.weight.double() / torch.sqrt(var + bn.eps)
+    torch.testing.assert_close(st[0].double(), sc, rtol=1e-5, atol=0)
+    torch.testing.assert_close(st[1].double(), bn.bias.double() - mean * sc, rtol=0, atol=1e-5 * sc.abs().max().item() * 4)
+    torch.testing.assert_close(bn.running_mean.double(), 0.9 * rm0.double() + 0.1 * mean, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(bn.running_var.double(), 0.9 * rv0.double() + 0.1 * xd.var(0, unbiased=True),
+                               rtol=1e-5, atol=1e-6)
+    assert bn.num_batches_tracked.item() == 1
+    r = torch.randn(rows, C, device="cuda", generator=g).to(dtype)
+    r4 = r.view(1, rows, 1, C).permute(0, 3, 1, 2)
+    for res, rst in ((None, None), (r4, None), (r4, st)):
+        y = x4.clone(memory_format=torch.channels_last)
+        _bn_apply_(y, st, residual=res, rst=rst)
+        ref = xd * st[0].double() + st[1].double()
+        if res is not None:
+            ref = ref + (r.double() * st[0].double() + st[1].double() if rst is not None else r.double())
+        ref = ref.clamp_min(0)
+        got = y.permute(0, 2, 3, 1).reshape(rows, C).double()
+        tol = 1e-5 if dtype == torch.float32 else 1e-2
+        torch.testing.assert_close(got, ref, rtol=tol, atol=tol)

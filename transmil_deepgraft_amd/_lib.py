@@ -130,6 +130,9 @@ _SIGS = {
     "tm_add_relu": (I, [I, P, P, P, L, P]),
     "tm_bias_act": (I, [I, P, P, L, I, I, P]),
     "tm_conv1x1": (I, [I, P, P, P, P, P, L, I, I, I, P]),
+    "tm_bn_train_workspace": (L, [I]),
+    "tm_bn_train_stats": (I, [I, P, P, I, I, P, P, P, P, Fl, Fl, P, P, P, L, P]),
+    "tm_bn_apply": (I, [I, P, P, P, P, P, P, L, I, I, P]),
     "tm_cls_a1_row_fwd": (I, [I, P, P, P, P, P, I, I, I, I, P, P, P]),
     "tm_cls_out_fwd": (I, [I, P, P, P, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_cls_out_bwd": (I, [I, P, P, P, I, I, I, I, I, Fl, U64, P, P, P, P, P]),
@@ -153,7 +156,6 @@ DIAG_SIGS = {
     "tm_debug_set_split_stamps": (None, [P]),
     "tm_debug_a1_stamps": (I, [P, I]),
     "tm_debug_gemm_stamps": (I, [P, I]),
-    "tm_debug_set_ppeg_wt": (None, [I]),
 }
 
 _lib = None

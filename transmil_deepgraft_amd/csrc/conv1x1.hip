@@ -23,6 +23,7 @@ namespace {
 
 constexpr size_t kWorkspace = 32u << 20;
 constexpr int kMaxDev = 16;
+constexpr long long kMaxRows = 1LL << 21;
 
 struct Device {
   hipblasLtHandle_t handle = nullptr;
@@ -36,7 +37,7 @@ struct Plan {
   size_t ws = 0;
 };
 
-using Key = std::tuple<int, int, int, int, long long, int, int>;   // dev dtype relu res rows cin cout
+using Key = std::tuple<int, int, int, int, int, long long, int, int>;   // dev dtype relu bias res rows cin cout
 
 std::mutex g_mu;
 Device g_dev[kMaxDev];
@@ -72,16 +73,19 @@ int device_state(int dev, Device** out) {
   return 0;
 }
 
-int make_plan(Device& d, int dtype, int relu, int res, long long rows, int cin, int cout, Plan* p) {
+int make_plan(Device& d, int dtype, int relu, int has_bias, long long rows, int cin, int cout, Plan* p) {
   const hipDataType t = dtype == TM_BF16 ? HIP_R_16BF : HIP_R_32F;
   LT_CHECK(hipblasLtMatmulDescCreate(&p->desc, HIPBLAS_COMPUTE_32F, HIP_R_32F));
   const hipblasOperation_t opA = HIPBLAS_OP_T, opB = HIPBLAS_OP_N;
   LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
   LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
-  const hipblasLtEpilogue_t epi = relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS;
+  const hipblasLtEpilogue_t epi = has_bias ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
+                                           : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);
   LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
-  const int32_t bt = (int32_t)t;
-  LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  if (has_bias) {
+    const int32_t bt = (int32_t)t;
+    LT_CHECK(hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)));
+  }
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p->a, t, (uint64_t)cin, (uint64_t)cout, (int64_t)cin));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p->b, t, (uint64_t)cin, (uint64_t)rows, (int64_t)cin));
   LT_CHECK(hipblasLtMatrixLayoutCreate(&p->cd, t, (uint64_t)cout, (uint64_t)rows, (int64_t)cout));
@@ -96,7 +100,6 @@ int make_plan(Device& d, int dtype, int relu, int res, long long rows, int cin, 
     s = hipblasLtMatmulAlgoGetHeuristic(d.handle, p->desc, p->a, p->b, p->cd, p->cd, pref, 1, r, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   LT_CHECK(s);
-  (void)res;
   if (n < 1) {
     tm_set_error("conv1x1: hipBLASLt found no algorithm for this shape/epilogue");
     return 3;
@@ -108,13 +111,13 @@ int make_plan(Device& d, int dtype, int relu, int res, long long rows, int cin, 
 
 }  // namespace
 
-// y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T + bias[cout] (+ residual[rows, cout])),
-// act = ReLU when relu != 0.  Row-major buffers (channels-last activations), dtype TM_BF16 or
-// TM_F32 for all of x, w, bias, residual, y (fp32 accumulation); residual may be NULL and must
-// not alias y.
+// y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout]) (+ residual[rows, cout])),
+// act = ReLU when relu != 0; bias NULL = none (the train-mode path: BN applied afterwards).
+// Row-major buffers (channels-last activations), dtype TM_BF16 or TM_F32 for all of x, w, bias,
+// residual, y (fp32 accumulation); residual may be NULL and must not alias y.
 extern "C" int tm_conv1x1(int dtype, const void* x, const void* w, const void* bias, const void* residual,
                           void* y, long long rows, int cin, int cout, int relu, void* stream) {
-  TM_REQUIRE(x && w && bias && y && rows >= 0 && cin > 0 && cout > 0, "conv1x1: bad args");
+  TM_REQUIRE(x && w && y && rows >= 0 && cin > 0 && cout > 0, "conv1x1: bad args");
   TM_REQUIRE(dtype == TM_BF16 || dtype == TM_F32, "conv1x1: dtype");
   TM_REQUIRE(residual != y, "conv1x1: residual must not alias the output");
   if (rows == 0) return 0;
@@ -126,17 +129,27 @@ extern "C" int tm_conv1x1(int dtype, const void* x, const void* w, const void* b
   std::lock_guard<std::mutex> lock(g_mu);
   Device* d = nullptr;
   if (int rc = device_state(dev, &d)) return rc;
-  const Key key{dev, dtype, relu ? 1 : 0, residual ? 1 : 0, rows, cin, cout};
-  auto it = g_plans.find(key);
-  if (it == g_plans.end()) {
-    Plan p;
-    if (int rc = make_plan(*d, dtype, relu ? 1 : 0, residual ? 1 : 0, rows, cin, cout, &p)) return rc;
-    it = g_plans.emplace(key, p).first;
+  // row pieces of at most kMaxRows: one launch per piece keeps hipBLASLt's grid / index math in
+  // the range it is tuned for (a whole 4096-tile bag is 12.8 M rows at layer 1)
+  const size_t esz = dtype == TM_BF16 ? 2 : 4;
+  for (long long r0 = 0; r0 < rows; r0 += kMaxRows) {
+    const long long nr = rows - r0 < kMaxRows ? rows - r0 : kMaxRows;
+    const Key key{dev, dtype, relu ? 1 : 0, bias ? 1 : 0, residual ? 1 : 0, nr, cin, cout};
+    auto it = g_plans.find(key);
+    if (it == g_plans.end()) {
+      Plan p;
+      if (int rc = make_plan(*d, dtype, relu ? 1 : 0, bias ? 1 : 0, nr, cin, cout, &p)) return rc;
+      it = g_plans.emplace(key, p).first;
+    }
+    Plan& p = it->second;
+    if (bias)
+      LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
+    const float alpha = 1.f, beta = residual ? 1.f : 0.f;
+    const char* xp = (const char*)x + (size_t)r0 * cin * esz;
+    char* yp = (char*)y + (size_t)r0 * cout * esz;
+    const char* rp = residual ? (const char*)residual + (size_t)r0 * cout * esz : yp;
+    LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, w, p.a, xp, p.b, &beta, rp, p.cd, yp, p.cd, &p.algo, d->ws,
+                             p.ws, (hipStream_t)stream));
   }
-  Plan& p = it->second;
-  LT_CHECK(hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias)));
-  const float alpha = 1.f, beta = residual ? 1.f : 0.f;
-  LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, w, p.a, x, p.b, &beta, residual ? residual : y, p.cd, y, p.cd,
-                           &p.algo, d->ws, p.ws, (hipStream_t)stream));
   return 0;
 }

@@ -16,12 +16,16 @@ Same module / parameter / buffer names as code/models/ResNet.py (ResNet :130-277
   as a hipBLASLt GEMM over the channels-last [n*h*w, c] rows (csrc/conv1x1.hip) whose epilogue
   adds the bias, the residual (conv3) and applies the ReLU; the 3x3 convolutions' bias + ReLU is
   one in-place HIP pass (tm_bias_act);
-* in train mode the BatchNorms run as written (batch statistics, running-stat updates), as the
-  reference's frozen-but-train-mode encoder does under Lightning;
+* in train mode the BatchNorms use batch statistics and update the running statistics, as the
+  reference's frozen-but-train-mode encoder does under Lightning: each one statistics pass + one
+  apply pass fused with its ReLU (bn3 with the residual), csrc/bn_train.hip, convolutions without
+  bias (1x1 through the same hipBLASLt GEMM); with autograd on (unfrozen parameters) the modules
+  run as written;
 * in eval mode tiles go through in chunks (``chunk`` tiles, default 512; per-tile math, so the
   chunking is exact) so the activation peak stays a few GB whatever the bag size; in train mode
-  the whole batch goes through at once, since batch statistics span it; the [B*bag, 2048]
-  features stay on the device for the fused TransMIL engine (no host round trip).
+  the bag is held as pieces of ``chunk`` tiles while every BatchNorm's statistics span the whole
+  batch (tens of GB for a 4096-tile bag, well inside one GPU's HBM); the [B*bag, 2048] features
+  stay on the device for the fused TransMIL engine (no host round trip).
 """
 from __future__ import annotations
 
@@ -78,7 +82,7 @@ def _conv1x1_gemm(x, w, b, relu, residual=None):
     cl = torch.channels_last
     n, c, h, wd = x.shape
     cout = w.shape[0]
-    if not x.is_contiguous(memory_format=cl) or w.dtype != x.dtype or b.dtype != x.dtype:
+    if not x.is_contiguous(memory_format=cl) or w.dtype != x.dtype or (b is not None and b.dtype != x.dtype):
         raise RuntimeError("conv1x1: channels-last input, weight and bias of one dtype expected")
     y = torch.empty((n, h, wd, cout), dtype=x.dtype, device=x.device).permute(0, 3, 1, 2)
     if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or
@@ -98,6 +102,53 @@ def _bias_act_(y, b, relu=True):
     n, c, h, wd = y.shape
     _lib.call("tm_bias_act", _dtype_code(y), _p(y), _p(b), n * h * wd, c, int(relu), _stream())
     return y
+
+
+def _bn_train_stats(ys, bn, ws):
+    """Train-mode BatchNorm statistics of a channels-last activation held as a list of bag pieces
+    (tm_bn_train_stats: the statistics span every piece): returns fp32 [2, C] (scale, shift) and
+    updates the module's running statistics as nn.BatchNorm2d does (momentum; None = cumulative
+    average)."""
+    import ctypes as C
+    from . import _lib
+    from .engine import _p, _stream
+    if any(not y.is_contiguous(memory_format=torch.channels_last) for y in ys):
+        raise RuntimeError("bn_train_stats: channels-last activations expected")
+    c = ys[0].shape[1]
+    st = torch.empty(2, c, dtype=torch.float32, device=ys[0].device)
+    track = bn.track_running_stats and bn.running_mean is not None
+    if track:
+        bn.num_batches_tracked.add_(1)
+    m = bn.momentum if bn.momentum is not None else (1.0 / float(bn.num_batches_tracked.item()) if track else 0.0)
+    g = bn.weight.detach() if bn.weight is not None else torch.ones(c, device=ys[0].device)
+    b = bn.bias.detach() if bn.bias is not None else torch.zeros(c, device=ys[0].device)
+    ptrs = (C.c_void_p * len(ys))(*[y.data_ptr() for y in ys])
+    rows = (C.c_longlong * len(ys))(*[y.numel() // c for y in ys])
+    _lib.call("tm_bn_train_stats", _dtype_code(ys[0]), ptrs, rows, len(ys), c, _p(g), _p(b),
+              _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None, float(m),
+              float(bn.eps), _p(st[0]), _p(st[1]), _p(ws), ws.numel(), _stream())
+    return st
+
+
+def _bn_apply_(y, st, residual=None, rst=None, relu=True):
+    """y = act(y * scale + shift (+ residual | + residual * rscale + rshift)) in place
+    (tm_bn_apply) over channels-last tensors."""
+    from . import _lib
+    from .engine import _p, _stream
+    if not y.is_contiguous(memory_format=torch.channels_last):
+        raise RuntimeError("bn_apply: channels-last activation expected")
+    n, c, h, wd = y.shape
+    if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or
+                                 not residual.is_contiguous(memory_format=torch.channels_last)):
+        raise RuntimeError("bn_apply: channels-last residual of the output's shape and dtype expected")
+    _lib.call("tm_bn_apply", _dtype_code(y), _p(y), _p(st[0]), _p(st[1]), _p(residual),
+              _p(rst[0]) if rst is not None else None, _p(rst[1]) if rst is not None else None,
+              n * h * wd, c, int(relu), _stream())
+    return y
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
 
 
 class RetCCLResNet50(nn.Module):
@@ -122,6 +173,8 @@ class RetCCLResNet50(nn.Module):
         self.channels_last = True
         self._folded = None
         self._folded_key = None
+        self._cast = None               # train mode: conv weights in the compute dtype, channels-last
+        self._cast_key = None
         for p in self.parameters():                     # model_interface.py:243-244
             p.requires_grad = False
 
@@ -206,6 +259,53 @@ class RetCCLResNet50(nn.Module):
             x = F.relu(y + idt)
         return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
 
+    def _forward_train_fused(self, x):
+        """Train mode (batch-statistics BatchNorm, frozen parameters, no autograd) on the GPU.
+        The bag is held as pieces of ``chunk`` tiles (every convolution / pooling runs at the
+        piece size the eval path uses) while each BatchNorm's statistics span all pieces
+        (tm_bn_train_stats).  Convolutions without bias (1x1: hipBLASLt GEMM; 3x3 / stem: MIOpen),
+        each BatchNorm one statistics pass + one apply pass fused with its ReLU, and bn3 + (BN'd
+        downsample) identity + ReLU one pass (tm_bn_apply)."""
+        key = self._fold_key()
+        if self._cast is None or self._cast_key != key:
+            self._cast = {n: _cl(p.detach().to(self.compute_dtype)) for n, p in self.named_parameters()
+                          if p.dim() == 4}
+            self._cast_key = key
+        w = self._cast
+        ws = torch.empty(self._bn_ws_floats(), dtype=torch.float32, device=x.device)
+        xs = [_cl(F.conv2d(x[i:i + self.chunk], w["conv1.weight"], None, stride=2, padding=3))
+              for i in range(0, x.shape[0], self.chunk)]
+        st = _bn_train_stats(xs, self.bn1, ws)
+        xs = [F.max_pool2d(_bn_apply_(p, st), 3, 2, 1) for p in xs]
+        for si, stage in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
+            for bi, blk in enumerate(stage):
+                pre = f"layer{si}.{bi}."
+                ys = [_conv1x1_gemm(p, w[pre + "conv1.weight"], None, False) for p in xs]
+                st = _bn_train_stats(ys, blk.bn1, ws)
+                ys = [_cl(F.conv2d(_bn_apply_(y, st), w[pre + "conv2.weight"], None, stride=blk.stride, padding=1))
+                      for y in ys]
+                st = _bn_train_stats(ys, blk.bn2, ws)
+                ys = [_conv1x1_gemm(_bn_apply_(y, st), w[pre + "conv3.weight"], None, False) for y in ys]
+                st3 = _bn_train_stats(ys, blk.bn3, ws)
+                if blk.downsample is None:
+                    for y, p in zip(ys, xs):
+                        _bn_apply_(y, st3, residual=p)
+                else:
+                    s = blk.downsample[0].stride[0]
+                    ds = [_conv1x1_gemm(p if s == 1 else _cl(p[:, :, ::s, ::s]), w[pre + "downsample.0.weight"],
+                                        None, False) for p in xs]
+                    sd = _bn_train_stats(ds, blk.downsample[1], ws)
+                    for y, d in zip(ys, ds):
+                        _bn_apply_(y, st3, residual=d, rst=sd)
+                    del ds
+                xs = ys
+        return torch.cat([torch.flatten(F.adaptive_avg_pool2d(p, 1), 1) for p in xs])
+
+    @staticmethod
+    def _bn_ws_floats():
+        from . import _lib
+        return _lib.query("tm_bn_train_workspace", 2048)
+
     def _forward_modules(self, x):
         x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
@@ -229,13 +329,19 @@ class RetCCLResNet50(nn.Module):
         # reference feeds model_ft in one call (model_interface.py:303-309): no chunking there
         # (a 4096-tile bag's activations are tens of GB, well inside one GPU's HBM)
         chunk = x.shape[0] if self.training else self.chunk
-        with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16,
-                                                          enabled=self.training and dt == torch.bfloat16):
+        fused_train = self.training and not grad and self.channels_last
+        autocast = self.training and not fused_train and dt == torch.bfloat16
+        with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
             for s in range(0, x.shape[0], chunk):
-                xc = x[s:s + chunk].to(dt if not self.training else torch.float32)
+                xc = x[s:s + chunk].to(torch.float32 if autocast else dt)
                 xc = xc.contiguous(memory_format=torch.channels_last if self.channels_last
                                    else torch.contiguous_format)
-                y = self._forward_folded(xc) if not self.training else self._forward_modules(xc)
+                if not self.training:
+                    y = self._forward_folded(xc)
+                elif fused_train:
+                    y = self._forward_train_fused(xc)
+                else:
+                    y = self._forward_modules(xc)
                 out[s:s + chunk] = y.float()
         return out
 
