@@ -59,6 +59,9 @@ def parse():
                     help="in_features: 512 (Linear+GELU _fc1, the metric's config) or 2048 (the RCC "
                          "_fc1 branch on RetCCL-width features, config C5 without its encoder)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--accumulate", type=int, default=1,
+                    help="accumulate_grad_batches K (code/train.py:199 uses 10 under DDP): a timed step is one "
+                         "micro-batch; every K-th one all-reduces and steps the optimizer (C4's every-10-steps row)")
     ap.add_argument("--probe", default="pinv_fwd", help="call site timed for the roofline object")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch every kernel from Python instead of "
@@ -296,11 +299,20 @@ def main():
     static_x = torch.empty_like(bags[0])
     static_y = torch.empty_like(labels[0])
 
-    def body(x=None, y=None):
+    K = max(1, args.accumulate)
+
+    def body(x=None, y=None, phase="last"):
+        """phase: "first" / "mid" micro-batch of an accumulation window (no all-reduce, no step;
+        first writes the gradients, mid adds), "last" (adds, all-reduces, steps; K = 1: the step)."""
         loss = task.training_step((static_x if x is None else x, static_y if y is None else y, None))
-        task.backward(loss)
-        allreduce()
-        opt.step()
+        allreduce.sync = phase == "last"
+        task.backward(loss / K if K > 1 else loss)
+        if phase == "last":
+            allreduce()
+            opt.step()
+
+    def phase_of(i):
+        return "last" if (i + 1) % K == 0 else ("first" if i % K == 0 else "mid")
 
     def load(i):
         static_x.copy_(bags[i % 4])
@@ -310,8 +322,9 @@ def main():
     if args.eager:
         def step(i):
             load(i)
-            body()
-            opt.zero_grad(set_to_none=True)
+            body(phase=phase_of(i))
+            if phase_of(i) == "last":
+                opt.zero_grad(set_to_none=True)
         for i in range(args.warmup):
             step(i)
     else:
@@ -319,25 +332,28 @@ def main():
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
-            for i in range(max(args.warmup, 2)):
+            for i in range(max(args.warmup, 2) * K):
                 load(i)
-                body()
-                opt.zero_grad(set_to_none=True)
+                body(phase=phase_of(i))
+                if phase_of(i) == "last":
+                    opt.zero_grad(set_to_none=True)
         torch.cuda.current_stream().wait_stream(side)
         # one captured step per resident bag (reading that bag in place: no copy into a static
         # input inside the timed region), all four on one memory pool -- they never run at once
         pool = torch.cuda.graph_pool_handle()
-        graphs = []
+        graphs = {}
+        phases = ["last"] if K == 1 else (["first", "mid", "last"] if K > 2 else ["first", "last"])
         for j in range(len(bags)):
-            opt.zero_grad(set_to_none=True)   # each capture takes the first-micro-batch (=) path
-            gj = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gj, pool=pool):
-                body(bags[j], labels[j])
-            graphs.append(gj)
-        graph = graphs[0]
+            opt.zero_grad(set_to_none=True)   # the first capture takes the first-micro-batch (=) path,
+            for ph in phases:                 # the ones after it the accumulating (+=) path
+                gj = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gj, pool=pool):
+                    body(bags[j], labels[j], phase=ph if K > 1 else "last")
+                graphs[j, ph] = gj
+        graph = graphs[0, "last"]
 
         def step(i):
-            graphs[i % len(graphs)].replay()
+            graphs[i % len(bags), phase_of(i) if K > 1 else "last"].replay()
 
     # the roofline call site, and the pseudo-inverse backward beside the forward chain
     probe_sites = {args.probe, "pinv_bwd"} if args.probe == "pinv_fwd" else {args.probe}
@@ -491,7 +507,8 @@ def main():
             "config": {"workload": f"TransMIL_feat {args.classes}-class, 1 bag N={args.n}x{args.features} per GPU, "
                                    "train step fwd+CE+bwd+allreduce+Lookahead(RAdam)",
                        "execution": "eager" if args.eager else "hipGraph replay of the whole step (one graph per resident bag)",
-                       "global_batch": world, "seq_len": args.n, "parallelism": f"dp{world}"},
+                       "global_batch": world, "seq_len": args.n, "parallelism": f"dp{world}",
+                       "accumulate_grad_batches": K},
             "roofline": roof,
             "roofline_pinv_bwd": roofline_obj("pinv_bwd") if args.probe == "pinv_fwd" else None,
             "hbm_roofline": hbm,
