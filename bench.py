@@ -51,8 +51,8 @@ F32_MATRIX_PEAK_TFS = 157.3  # v_mfma_f32_32x32x2_f32 = the fp32 vector rate (MI
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)   # 20 warm-up, >= 200 timed steps
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--n", type=int, default=8192, help="patches per bag")
     ap.add_argument("--classes", type=int, default=2)
     ap.add_argument("--features", type=int, default=512, choices=[512, 2048],
