@@ -1173,7 +1173,8 @@ inline bool use_ring160(const tm_gemm_args& g) {
   // per CU) the 128-row ring stays faster (24.5 vs 27.6 us; scripts/dev/gemm_variants.py 9,10)
   const long long tn = (g.N + BN - 1) / BN;
   const long long t128 = (g.M + 127) / 128 * tn, t160 = (g.M + BM160 - 1) / BM160 * tn;
-  return t128 > 256 && t160 <= 256;
+  const long long cu = tm_cu_count();
+  return t128 > cu && t160 <= cu;
 }
 
 template <typename OutT>

@@ -890,7 +890,7 @@ constexpr size_t A3V_BYTES = 2 * A3V_BUF;                          // two chunk 
 constexpr int A3V_PIECES = (A3V_KEYS * 8 + 511) / 512;             // 16-B pieces per thread per operand
 
 // partials per head of the v2 kernel
-inline int a3v_splits(int nbh, int n) { return std::max(1, std::min(n / 32, 256 / std::max(nbh, 1))); }
+inline int a3v_splits(int nbh, int n) { return std::max(1, std::min(n / 32, tm_cu_count() / std::max(nbh, 1))); }
 
 // S2R > 0: the workgroup also writes A2 = softmax(q~ k~^T) rows p * 2 S2R .. + 2 S2R - 1 of its head
 // (sim2_rows, two 256-thread groups of S2R rows; host-checked 2 S2R P == 256) before its first key
@@ -1280,9 +1280,10 @@ struct CbLay {
   static constexpr size_t BYTES = CS_OFF + 8 * 36 * 4;                    // 161152
 };
 
-// rows per workgroup of the bf16 conv backward (256 workgroups over all heads when possible)
+// rows per workgroup of the bf16 conv backward (one workgroup per CU over all heads when possible)
 inline int conv_bwd_rows(int nbh, int n) {
-  const long long want = ((long long)n * nbh + 255) / 256;
+  const long long cu = tm_cu_count();
+  const long long want = ((long long)n * nbh + cu - 1) / cu;
   const int r = (int)((want + 7) / 8 * 8);
   return r < 32 ? 32 : (r > CB_ROWS ? CB_ROWS : r);
 }
@@ -2237,7 +2238,7 @@ extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void
   hipStream_t st = (hipStream_t)stream;
   if (dtype == TM_BF16 && NYS_VARIANT != 14) {
     const int cph = n / 32;
-    int wpg = std::max(1, std::min(256 / std::max(nbh, 1), cph));
+    int wpg = std::max(1, std::min(tm_cu_count() / std::max(nbh, 1), cph));
     wpg = std::max(wpg, (cph + A1P_MAXCH - 1) / A1P_MAXCH);  // <= A1P_MAXCH chunks per workgroup
 #ifdef TM_DIAG
     // ablation variants 11-19 (microbench only): 10 + VAR
@@ -2319,7 +2320,7 @@ namespace {
 // workgroups per head of the bf16 A1 backward (even split of the n / 32 query chunks)
 int a1_bwd_split(int nbh, int n) {
   const int cph = n / 32;
-  const int w = std::min(cph, std::max(1, 256 / std::max(nbh, 1)));
+  const int w = std::min(cph, std::max(1, tm_cu_count() / std::max(nbh, 1)));
   return std::max(w, (cph + BwdLay16::MAXQ / 32 - 1) / (BwdLay16::MAXQ / 32));
 }
 }  // namespace
@@ -2374,7 +2375,7 @@ namespace {
 struct A3Split { int wpg, nw; };
 A3Split a3_bwd_split(int nbh, int n) {
   const int units = n / 32;
-  const int w = std::max(1, std::min(units, 256 / std::max(nbh, 1)));
+  const int w = std::max(1, std::min(units, tm_cu_count() / std::max(nbh, 1)));
   const int per = (units + w - 1) / w;
   if (per <= 8) return {w, 8};
   if (per == 9) return {w, 9};

@@ -149,10 +149,22 @@ def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c
     _lib.call("tm_gemm", _p(A), _p(B), _p(Cout), C.byref(g), _stream())
 
 
+_CU = {}
+
+
+def cu_count():
+    """Compute units of the current device (the schedules size grids to one workgroup per CU;
+    256 on MI355X, also the value without a GPU)."""
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else -1
+    if dev not in _CU:
+        _CU[dev] = torch.cuda.get_device_properties(dev).multi_processor_count if dev >= 0 else 256
+    return _CU[dev]
+
+
 def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool):
     """out[M,N] (fp32) = sum_k dY[k, m] X[k, n]  (split-K, deterministic)."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
-    splits = max(1, min(16, 256 // max(tiles, 1), (K + 255) // 256))   # <= one workgroup per CU
+    splits = max(1, min(16, cu_count() // max(tiles, 1), (K + 255) // 256))   # <= one workgroup per CU
     if splits == 1:
         gemm(dY, X, out, M, N, K, lda=ldy, ldb=ldx, ldc=N, a_trans=1, b_kn=1, dtype=dtype, c_dtype=F32)
         return
