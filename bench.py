@@ -36,6 +36,7 @@ import json
 import os
 import sys
 import time
+import types
 
 import torch
 import torch.distributed as dist
@@ -270,6 +271,74 @@ def cpu_baseline(n_patches, ncls, steps, feat=512, as_written=False, threads=Non
                        f"N={n_patches}x{feat}, fp32, train mode, {variant}, torch.set_num_threads in {counts}")
 
 
+def make_step(task, opt, allreduce, bags, labels, K, warmup, eager=False):
+    """The timed step over the resident bags: ``step(i)`` runs micro-batch i (bag i % len(bags)).
+
+    K = 1: fwd + CE + bwd + all-reduce + optimizer, one captured hipGraph per bag.  K > 1
+    (accumulate_grad_batches, Lightning's semantics as TransMILTask.optimization_step): micro-batch
+    i is "first" (i % K == 0: loss / K, gradients written), "mid" (added) or "last" ((i + 1) % K == 0:
+    added, all-reduced, optimizer step), one captured graph per (bag, phase).  Warm-up: warmup * K
+    eager micro-batches (at least 2 K) on a side stream before the captures.  Returns a namespace
+    with ``step``, ``body(x, y, phase)``, ``load(i)`` and ``graph`` (None when eager)."""
+    static_x = torch.empty_like(bags[0])
+    static_y = torch.empty_like(labels[0])
+
+    def body(x=None, y=None, phase="last"):
+        """phase: "first" / "mid" micro-batch of an accumulation window (no all-reduce, no step;
+        first writes the gradients, mid adds), "last" (adds, all-reduces, steps; K = 1: the step)."""
+        loss = task.training_step((static_x if x is None else x, static_y if y is None else y, None))
+        allreduce.sync = phase == "last"
+        task.backward(loss / K if K > 1 else loss)
+        if phase == "last":
+            allreduce()
+            opt.step()
+
+    def phase_of(i):
+        return "last" if (i + 1) % K == 0 else ("first" if i % K == 0 else "mid")
+
+    def load(i):
+        static_x.copy_(bags[i % len(bags)])
+        static_y.copy_(labels[i % len(bags)])
+
+    graph = None
+    if eager:
+        def step(i):
+            load(i)
+            body(phase=phase_of(i))
+            if phase_of(i) == "last":
+                opt.zero_grad(set_to_none=True)
+        for i in range(warmup * K):
+            step(i)
+    else:
+        # warm up on a side stream, then capture fwd + CE + bwd + all-reduce + optimizer as ONE hipGraph
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for i in range(max(warmup, 2) * K):
+                load(i)
+                body(phase=phase_of(i))
+                if phase_of(i) == "last":
+                    opt.zero_grad(set_to_none=True)
+        torch.cuda.current_stream().wait_stream(side)
+        # one captured step per resident bag (reading that bag in place: no copy into a static
+        # input inside the timed region), all on one memory pool -- they never run at once
+        pool = torch.cuda.graph_pool_handle()
+        graphs = {}
+        phases = ["last"] if K == 1 else (["first", "mid", "last"] if K > 2 else ["first", "last"])
+        for j in range(len(bags)):
+            opt.zero_grad(set_to_none=True)   # the first capture takes the first-micro-batch (=) path,
+            for ph in phases:                 # the ones after it the accumulating (+=) path
+                gj = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gj, pool=pool):
+                    body(bags[j], labels[j], phase=ph)
+                graphs[j, ph] = gj
+        graph = graphs[0, "last"]
+
+        def step(i):
+            graphs[i % len(bags), phase_of(i)].replay()
+    return types.SimpleNamespace(step=step, body=body, load=load, graph=graph, phase_of=phase_of)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -296,64 +365,9 @@ def main():
     g = torch.Generator(device=dev).manual_seed(2021 + rank)
     bags = [torch.rand(1, args.n, args.features, device=dev, generator=g) for _ in range(4)]
     labels = [torch.randint(0, args.classes, (1,), device=dev, generator=g) for _ in range(4)]
-    static_x = torch.empty_like(bags[0])
-    static_y = torch.empty_like(labels[0])
-
     K = max(1, args.accumulate)
-
-    def body(x=None, y=None, phase="last"):
-        """phase: "first" / "mid" micro-batch of an accumulation window (no all-reduce, no step;
-        first writes the gradients, mid adds), "last" (adds, all-reduces, steps; K = 1: the step)."""
-        loss = task.training_step((static_x if x is None else x, static_y if y is None else y, None))
-        allreduce.sync = phase == "last"
-        task.backward(loss / K if K > 1 else loss)
-        if phase == "last":
-            allreduce()
-            opt.step()
-
-    def phase_of(i):
-        return "last" if (i + 1) % K == 0 else ("first" if i % K == 0 else "mid")
-
-    def load(i):
-        static_x.copy_(bags[i % 4])
-        static_y.copy_(labels[i % 4])
-
-    graph = None
-    if args.eager:
-        def step(i):
-            load(i)
-            body(phase=phase_of(i))
-            if phase_of(i) == "last":
-                opt.zero_grad(set_to_none=True)
-        for i in range(args.warmup):
-            step(i)
-    else:
-        # warm up on a side stream, then capture fwd + CE + bwd + all-reduce + optimizer as ONE hipGraph
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for i in range(max(args.warmup, 2) * K):
-                load(i)
-                body(phase=phase_of(i))
-                if phase_of(i) == "last":
-                    opt.zero_grad(set_to_none=True)
-        torch.cuda.current_stream().wait_stream(side)
-        # one captured step per resident bag (reading that bag in place: no copy into a static
-        # input inside the timed region), all four on one memory pool -- they never run at once
-        pool = torch.cuda.graph_pool_handle()
-        graphs = {}
-        phases = ["last"] if K == 1 else (["first", "mid", "last"] if K > 2 else ["first", "last"])
-        for j in range(len(bags)):
-            opt.zero_grad(set_to_none=True)   # the first capture takes the first-micro-batch (=) path,
-            for ph in phases:                 # the ones after it the accumulating (+=) path
-                gj = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gj, pool=pool):
-                    body(bags[j], labels[j], phase=ph if K > 1 else "last")
-                graphs[j, ph] = gj
-        graph = graphs[0, "last"]
-
-        def step(i):
-            graphs[i % len(bags), phase_of(i) if K > 1 else "last"].replay()
+    st = make_step(task, opt, allreduce, bags, labels, K, args.warmup, eager=args.eager)
+    body, load, step, graph = st.body, st.load, st.step, st.graph
 
     # the roofline call site, and the pseudo-inverse backward beside the forward chain
     probe_sites = {args.probe, "pinv_bwd"} if args.probe == "pinv_fwd" else {args.probe}

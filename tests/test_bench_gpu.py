@@ -1,0 +1,50 @@
+"""bench.py's timed step (make_step: captured hipGraphs per bag and accumulation phase) against
+TransMILTask.optimization_step run eagerly on the same micro-batch sequence: the parameters after
+the warm-up + timed micro-batches must be bitwise identical, with accumulate_grad_batches K = 1
+(the driver's bench line) and K = 3 (C4's all-reduce every K micro-batches; code/train.py:199)."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 3])
+def test_bench_graph_step_equals_eager_optimization_step(K):
+    import bench
+    from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
+    from transmil_deepgraft_amd.models import TransMIL
+
+    def build():
+        torch.manual_seed(7)
+        m = TransMIL(2, 512, 512).cuda().train().set_compute_dtype(torch.float32)
+        task = TransMILTask(m, accumulate_grad_batches=K)
+        return m, task, task.configure_optimizers()[0][0], GradAllReduce(m.parameters(), model=m)
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    bags = [torch.rand(1, 300, 512, device="cuda", generator=g) for _ in range(2)]
+    labels = [torch.tensor([j % 2], device="cuda") for j in range(2)]
+    timed = 2 * K
+
+    ma, ta, oa, ara = build()
+    st = bench.make_step(ta, oa, ara, bags, labels, K, warmup=1)
+    assert st.graph is not None
+    for i in range(timed):
+        st.step(i)
+    torch.cuda.synchronize()
+
+    mb, tb, ob, arb = build()
+    for i in list(range(2 * K)) + list(range(timed)):      # make_step's warm-up, then the timed ones
+        tb.optimization_step((bags[i % 2], labels[i % 2], None), ob, allreduce=arb)
+    torch.cuda.synchronize()
+
+    pa, pb = dict(ma.named_parameters()), dict(mb.named_parameters())
+    moved = any(not torch.equal(pa[n], p0) for n, p0 in [(n, p.detach().clone()) for n, p in build()[0].named_parameters()])
+    assert moved
+    bad = [n for n in pa if not torch.equal(pa[n], pb[n])]
+    assert not bad, bad
