@@ -172,13 +172,21 @@ int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const flo
 /* bf16 mode, fused key side: the A3 backward writes the final bf16 k / v parts of dqkv
  * (k = dK + dk~[t/l]/l, v = dv_conv + dV) and dql (=) from its slabs; then tm_nys_assemble_q
  * writes the q part, scale * (dq + (dql_a + dql_b)[t/l]/l).  dv_conv is read only for rows
- * [dv_lo, dv_hi) (zero elsewhere; 0, n = dense); dq_row >= 0: dq is zero outside that row. */
+ * [dv_lo, dv_hi) (zero elsewhere; 0, n = dense); dq_row >= 0: dq is zero outside that row.
+ * dql = NULL: the dq~ partial slab is left in work ([tm_nys_a3_bwd_slabs][B*h][256][64] fp32) for
+ * tm_nys_assemble_q_slab, which reduces it while writing the q part (one launch fewer). */
 int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v, const float* lse3,
                         const float* d3, int nbh, int nh, int n, const float* dv_conv, int dv_lo, int dv_hi,
                         const float* dkl, float* work, float* dql, void* dqkv, tm_reduce_queue* rq,
                         void* stream);
 int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a, const float* dql_b, int nbags,
                       int nh, int n, float scale, void* dqkv, void* stream);
+/* partial slabs the bf16 A3 backward writes (tm_nys_a3_bwd_fused's work) */
+int tm_nys_a3_bwd_slabs(int nbh, int n);
+/* q part of dqkv, scale * (dq + (dql + sum_p slab[p])[t/l]/l), the slab sum in the same launch
+ * (nh <= 8; slab [slabs][nbags*nh][256][64] fp32 as tm_nys_a3_bwd_fused(dql = NULL) leaves it) */
+int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, const float* dql, const float* slab, int slabs,
+                           int nbags, int nh, int n, float scale, void* dqkv, void* stream);
 
 /* ---- pseudo-inverse + small fp32 batched products (pinv.hip) -------------
  * moore_penrose_iter_pinv of nystrom_attention (App. A eq. 7).

@@ -638,3 +638,36 @@ def test_colsum_bf16_matches_fp64(rows, cols, ld, acc):
     torch.cuda.synchronize()
     ref = X[:, :cols].double().sum(0).cpu() + (base.double().cpu() if acc else 0)
     assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=2e-3)   # fp32 sums of ~8 K terms of size ~1
+
+
+# ----------------------------------------------------------------------------- assemble_q_slab
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dq_row", [-1, 300])
+def test_assemble_q_slab_reduces_the_a3_partials(dtype, dq_row):
+    """tm_nys_assemble_q_slab: q part of dqkv = scale * (dq + (dql + sum_p slab[p])[t / l] / l)
+    against fp64, the other two thirds of dqkv untouched (the fused A3 backward wrote them)."""
+    from transmil_deepgraft_amd._lib import BF16, F32
+    from transmil_deepgraft_amd.engine import _p, _stream
+    lib = _lib()
+    B, nh, n, slabs, scale = 2, 8, 768, 33, 0.125
+    nbh, l = B * nh, n // 256
+    g = torch.Generator(device=DEV).manual_seed(11)
+    dq = torch.randn(nbh, n, 64, device=DEV, generator=g)
+    dql = torch.randn(nbh, 256, 64, device=DEV, generator=g)
+    slab = torch.randn(slabs, nbh, 256, 64, device=DEV, generator=g)
+    dqkv = torch.full((B, n, 3 * nh * 64), 7.0, device=DEV).to(dtype)
+    lib.call("tm_nys_assemble_q_slab", BF16 if dtype == torch.bfloat16 else F32, _p(dq), dq_row, _p(dql), _p(slab),
+             slabs, B, nh, n, C.c_float(scale), _p(dqkv), _stream())
+    torch.cuda.synchronize()
+    dqd = dq.double()
+    if dq_row >= 0:
+        keep = torch.zeros_like(dqd)
+        keep[:, dq_row] = dqd[:, dq_row]
+        dqd = keep
+    lm = (dql.double() + slab.double().sum(0)) / l                       # [nbh, 256, 64]
+    ref = scale * (dqd + lm.repeat_interleave(l, dim=1))                  # [nbh, n, 64]
+    ref = ref.view(B, nh, n, 64).permute(0, 2, 1, 3).reshape(B, n, nh * 64)
+    got = dqkv[:, :, :nh * 64].double()
+    tol = 1e-5 if dtype == torch.float32 else 8e-3
+    assert _rel(got, ref) < tol
+    assert (dqkv[:, :, nh * 64:] == 7).all()

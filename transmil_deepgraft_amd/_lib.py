@@ -96,6 +96,8 @@ _SIGS = {
     "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
     "tm_nys_a3_bwd_fused": (I, [P, P, P, P, P, P, I, I, I, P, I, I, P, P, P, P, P, P]),
     "tm_nys_assemble_q": (I, [I, P, I, P, P, I, I, I, Fl, P, P]),
+    "tm_nys_a3_bwd_slabs": (I, [I, I]),
+    "tm_nys_assemble_q_slab": (I, [I, P, I, P, P, I, I, I, I, Fl, P, P]),
     "tm_nys_attn_row": (I, [I, P, P, P, P, P, P, I, I, I, P, P]),
     "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
     "tm_pinv_saved_floats": (L, [I, I]),

@@ -2094,6 +2094,53 @@ __global__ void assemble_q_kernel(const float* __restrict__ dq, int dq_row, cons
   store8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c, out);
 }
 
+// q part of dqkv with the A3 backward's dq~ partial slab reduced in the same launch (no separate
+// split-K reduce, no dq~3 round trip): q = scale * (dq + (dql + sum_p slab[p])[t / l] / l).
+// grid (256 landmarks, nbags), block 256: the workgroup sums landmark j's row over the partial
+// slabs (four part groups, combined in a fixed order), then writes the l tokens of segment j.
+template <typename T>
+__global__ __launch_bounds__(256) void assemble_q_slab_kernel(const float* __restrict__ dq, int dq_row,
+                                                              const float* __restrict__ dql,
+                                                              const float* __restrict__ slab, int slabs,
+                                                              long long slab_count, int n, int l, int nh,
+                                                              float scale, T* __restrict__ dqkv) {
+  __shared__ __attribute__((aligned(16))) float part[4][8 * DH];   // [group][nh <= 8 heads x 64 d]
+  const int j = blockIdx.x, bag = blockIdx.y, tid = threadIdx.x;
+  const int inner = nh * DH, pieces = inner / 8;                          // <= 64
+  {
+    const int pc = tid & 63, g = tid >> 6;
+    if (pc < pieces) {
+      const int c = pc * 8, head = c / DH, d = c % DH;
+      const size_t off = (((size_t)bag * nh + head) * NL + j) * DH + d;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int p = g; p < slabs; p += 4) {
+        const f32x8 v = load8<float>(slab + (size_t)p * slab_count + off);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part[g][c + e] = acc[e];
+    }
+  }
+  __syncthreads();
+  for (int col = tid; col < inner; col += 256) {   // (group 0 + 1) + (2 + 3), then the landmark path's dq~
+    const int head = col / DH, d = col % DH;
+    const float sum = (part[0][col] + part[1][col]) + (part[2][col] + part[3][col]);
+    part[0][col] = (dql[(((size_t)bag * nh + head) * NL + j) * DH + d] + sum) * (1.0f / (float)l);
+  }
+  __syncthreads();
+  for (int it = tid; it < l * pieces; it += 256) {
+    const int t = j * l + it / pieces, c = (it % pieces) * 8;
+    const int head = c / DH, d = c % DH;
+    const size_t row = (((size_t)bag * nh + head) * n + t) * DH + d;
+    const f32x8 a = (dq_row < 0 || t == dq_row) ? load8<float>(dq + row) : (f32x8){};
+    vec8<T> out;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[e] = from_f<T>(scale * (a[e] + part[0][c + e]));
+    store8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c, out);
+  }
+}
+
 }  // namespace
 
 // ============================ C entry points ===============================
@@ -2467,7 +2514,21 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   int slabs = nkb;
   launch_a3_bwd_bf16(a, nbh, n, st, slabs);
   TM_CHECK_LAUNCH();
+  if (!dql) return 0;   // the slab stays for tm_nys_assemble_q_slab
   return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, 0, rq, stream);
+}
+
+extern "C" int tm_nys_a3_bwd_slabs(int nbh, int n) { return a3_bwd_split(nbh, n).wpg; }
+
+extern "C" int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, const float* dql, const float* slab,
+                                      int slabs, int nbags, int nh, int n, float scale, void* dqkv, void* stream) {
+  TM_REQUIRE(n > 0 && n % NL == 0 && nh > 0 && nh <= 8 && slabs > 0, "assemble_q_slab: bad shape");
+  TM_REQUIRE(dq && dql && slab && dqkv, "assemble_q_slab: null operand");
+  TM_DTYPE_DISPATCH(dtype, (assemble_q_slab_kernel<T><<<dim3(NL, nbags), 256, 0, (hipStream_t)stream>>>(
+                               dq, dq_row, dql, slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL, nh, scale,
+                               (T*)dqkv)));
+  TM_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a, const float* dql_b,

@@ -474,10 +474,11 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
              bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
         with probe("a3_bwd"):
             lo, hi = (0, n) if cls_row is None else (max(cls_row - 16, 0), min(cls_row + 17, n))
+            # dql = NULL: the dq~3 partial slab stays in work3; assemble_q_slab sums it in place
             _lib.call("tm_nys_a3_bwd_fused", _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]), _p(d3),
-                      nbh, nh, n, _p(dv), lo, hi, _p(dkl), _p(work3), _p(dql3), _p(dqkv), _rq(), st)
-        _lib.call("tm_nys_assemble_q", dt_code, _p(dq), -1 if cls_row is None else cls_row, _p(dql), _p(dql3),
-                  geo.B, nh, n, C.c_float(scale), _p(dqkv), st)
+                      nbh, nh, n, _p(dv), lo, hi, _p(dkl), _p(work3), None, _p(dqkv), _rq(), st)
+        _lib.call("tm_nys_assemble_q_slab", dt_code, _p(dq), -1 if cls_row is None else cls_row, _p(dql),
+                  _p(work3), _lib.query("tm_nys_a3_bwd_slabs", nbh, n), geo.B, nh, n, C.c_float(scale), _p(dqkv), st)
         return dqkv
     bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL, E1=dql3, e1=1.0),
          bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
