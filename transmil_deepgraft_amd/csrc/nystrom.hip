@@ -2113,7 +2113,17 @@ __global__ __launch_bounds__(256) void assemble_q_slab_kernel(const float* __res
       const int c = pc * 8, head = c / DH, d = c % DH;
       const size_t off = (((size_t)bag * nh + head) * NL + j) * DH + d;
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int p = g; p < slabs; p += 4) {
+      int p = g;
+      for (; p + 12 < slabs; p += 16) {   // four partials in flight per thread
+        f32x8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = load8<float>(slab + (size_t)(p + 4 * u) * slab_count + off);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += v[u][e];
+      }
+      for (; p < slabs; p += 4) {
         const f32x8 v = load8<float>(slab + (size_t)p * slab_count + off);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += v[e];
