@@ -371,8 +371,10 @@ int tm_step_prepare(int dtype, const tm_cast_table* table, const float* w7, cons
  * Lookahead sync (code/MyOptimizer/lookahead.py, wrapped at optim_factory.py:118-121)
  * over up to 40 parameter tensors in one launch.  exp_avg / exp_avg_sq / slow are
  * flat 16-B aligned fp32 buffers indexed by the table's offsets (prefix sums of numel, each
- * rounded up to a multiple of 4); counters (int32[3], device, zero-initialised) hold the
- * RAdam and Lookahead step counts (advanced by the call itself) and a scratch count.
+ * rounded up to a multiple of 4); counters (int32[tm_radam_counters_len(total)], device,
+ * zero-initialised; total = the table's last offset) hold one (RAdam step, Lookahead step) pair per
+ * workgroup of the launch, each advanced by its workgroup in the same launch (no tick launch);
+ * the pairs stay equal as long as the table's total is fixed, and pair 0 is the one to checkpoint.
  * lookahead_k == 0 disables the sync (plain RAdam). */
 #define TM_OPTIM_MAX_TENSORS 40
 typedef struct tm_optim_tensor {
@@ -388,6 +390,7 @@ typedef struct tm_optim_table {
   long long offset[TM_OPTIM_MAX_TENSORS + 1];
   tm_optim_tensor t[TM_OPTIM_MAX_TENSORS];
 } tm_optim_table;
+long long tm_radam_counters_len(long long total_elements);
 int tm_radam_lookahead_step(const tm_optim_table* table, float* exp_avg, float* exp_avg_sq, float* slow,
                             int* counters, float beta1, float beta2, float eps, int lookahead_k,
                             float lookahead_alpha, void* stream);

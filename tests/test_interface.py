@@ -253,6 +253,12 @@ def test_fused_radam_lookahead_matches_torch(k):
         torch.testing.assert_close(pa, pb, rtol=2e-5, atol=2e-6)
     sd = opt_a.state_dict()
     assert int(sd["fused_counters"][0]) == 20
+    c = opt_a._counters.cpu()          # one (RAdam, Lookahead) step pair per update workgroup
+    assert (c[:c.numel() // 2 * 2].view(-1, 2) == 20).all()
+    opt_c = FusedRAdamLookahead(add_weight_decay(b, 0.05), lr=3e-3, lookahead_k=k)
+    opt_c.load_state_dict(sd)
+    c2 = opt_c._counters.cpu()
+    assert (c2[:c2.numel() // 2 * 2].view(-1, 2) == 20).all()
     for pa, pb in zip(a.parameters(), b.parameters()):
         sa, sb = opt_a.state[pa], base.state[pb]
         torch.testing.assert_close(sa["exp_avg"], sb["exp_avg"], rtol=2e-5, atol=1e-8)

@@ -643,13 +643,14 @@ def test_colsum_bf16_matches_fp64(rows, cols, ld, acc):
 # ----------------------------------------------------------------------------- assemble_q_slab
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("dq_row", [-1, 300])
-def test_assemble_q_slab_reduces_the_a3_partials(dtype, dq_row):
+@pytest.mark.parametrize("B,n", [(2, 768), (1, 8448), (1, 33280)])   # l = 3, 33 (C2), 130 (C3)
+def test_assemble_q_slab_reduces_the_a3_partials(dtype, dq_row, B, n):
     """tm_nys_assemble_q_slab: q part of dqkv = scale * (dq + (dql + sum_p slab[p])[t / l] / l)
     against fp64, the other two thirds of dqkv untouched (the fused A3 backward wrote them)."""
     from transmil_deepgraft_amd._lib import BF16, F32
     from transmil_deepgraft_amd.engine import _p, _stream
     lib = _lib()
-    B, nh, n, slabs, scale = 2, 8, 768, 33, 0.125
+    nh, slabs, scale = 8, 33, 0.125
     nbh, l = B * nh, n // 256
     g = torch.Generator(device=DEV).manual_seed(11)
     dq = torch.randn(nbh, n, 64, device=DEV, generator=g)

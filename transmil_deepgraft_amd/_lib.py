@@ -143,6 +143,7 @@ _SIGS = {
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),
     "tm_gelu_bwd": (I, [I, P, P, L, P, P]),
     "tm_cast_f32_many": (I, [I, C.POINTER(CastTable), P]),
+    "tm_radam_counters_len": (L, [L]),
     "tm_radam_lookahead_step": (I, [C.POINTER(OptimTable), P, P, P, P, Fl, Fl, Fl, I, Fl, P]),
 }
 

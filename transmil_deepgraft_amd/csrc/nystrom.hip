@@ -2096,17 +2096,33 @@ __global__ void assemble_q_kernel(const float* __restrict__ dq, int dq_row, cons
 
 // q part of dqkv with the A3 backward's dq~ partial slab reduced in the same launch (no separate
 // split-K reduce, no dq~3 round trip): q = scale * (dq + (dql + sum_p slab[p])[t / l] / l).
-// grid (256 landmarks, nbags), block 256: the workgroup sums landmark j's row over the partial
-// slabs (four part groups, combined in a fixed order), then writes the l tokens of segment j.
+// grid (256 landmarks, nbags), block 512: the workgroup's first QP dq pieces per thread are
+// requested first, then landmark j's slab row is summed (eight part groups, combined in a fixed
+// order) while they are in flight, then the l tokens of segment j are written.
+constexpr int AQ_THREADS = 512, AQ_GROUPS = AQ_THREADS / 64, AQ_QP = 5;
 template <typename T>
-__global__ __launch_bounds__(256) void assemble_q_slab_kernel(const float* __restrict__ dq, int dq_row,
-                                                              const float* __restrict__ dql,
-                                                              const float* __restrict__ slab, int slabs,
-                                                              long long slab_count, int n, int l, int nh,
-                                                              float scale, T* __restrict__ dqkv) {
-  __shared__ __attribute__((aligned(16))) float part[4][8 * DH];   // [group][nh <= 8 heads x 64 d]
+__global__ __launch_bounds__(AQ_THREADS) void assemble_q_slab_kernel(const float* __restrict__ dq, int dq_row,
+                                                                     const float* __restrict__ dql,
+                                                                     const float* __restrict__ slab, int slabs,
+                                                                     long long slab_count, int n, int l, int nh,
+                                                                     float scale, T* __restrict__ dqkv) {
+  __shared__ __attribute__((aligned(16))) float part[AQ_GROUPS][8 * DH];   // [group][nh <= 8 heads x 64 d]
   const int j = blockIdx.x, bag = blockIdx.y, tid = threadIdx.x;
   const int inner = nh * DH, pieces = inner / 8;                          // <= 64
+  const int items = l * pieces;
+  auto dq_row_of = [&](int it, int& t, int& c) -> size_t {
+    t = j * l + it / pieces;
+    c = (it % pieces) * 8;
+    return (((size_t)bag * nh + c / DH) * n + t) * DH + c % DH;
+  };
+  f32x8 a[AQ_QP];
+#pragma unroll
+  for (int u = 0; u < AQ_QP; ++u) {
+    const int it = tid + AQ_THREADS * u;
+    int t, c;
+    const size_t row = it < items ? dq_row_of(it, t, c) : 0;
+    a[u] = (it < items && (dq_row < 0 || t == dq_row)) ? load8<float>(dq + row) : (f32x8){};
+  }
   {
     const int pc = tid & 63, g = tid >> 6;
     if (pc < pieces) {
@@ -2114,16 +2130,16 @@ __global__ __launch_bounds__(256) void assemble_q_slab_kernel(const float* __res
       const size_t off = (((size_t)bag * nh + head) * NL + j) * DH + d;
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       int p = g;
-      for (; p + 12 < slabs; p += 16) {   // four partials in flight per thread
+      for (; p + 3 * AQ_GROUPS < slabs; p += 4 * AQ_GROUPS) {   // four partials in flight per thread
         f32x8 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = load8<float>(slab + (size_t)(p + 4 * u) * slab_count + off);
+        for (int u = 0; u < 4; ++u) v[u] = load8<float>(slab + (size_t)(p + AQ_GROUPS * u) * slab_count + off);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[e] += v[u][e];
       }
-      for (; p < slabs; p += 4) {
+      for (; p < slabs; p += AQ_GROUPS) {
         const f32x8 v = load8<float>(slab + (size_t)p * slab_count + off);
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += v[e];
@@ -2133,21 +2149,28 @@ __global__ __launch_bounds__(256) void assemble_q_slab_kernel(const float* __res
     }
   }
   __syncthreads();
-  for (int col = tid; col < inner; col += 256) {   // (group 0 + 1) + (2 + 3), then the landmark path's dq~
+  for (int col = tid; col < inner; col += AQ_THREADS) {   // pairwise over the groups, then the landmark path's dq~
     const int head = col / DH, d = col % DH;
-    const float sum = (part[0][col] + part[1][col]) + (part[2][col] + part[3][col]);
+    const float sum = ((part[0][col] + part[1][col]) + (part[2][col] + part[3][col])) +
+                      ((part[4][col] + part[5][col]) + (part[6][col] + part[7][col]));
     part[0][col] = (dql[(((size_t)bag * nh + head) * NL + j) * DH + d] + sum) * (1.0f / (float)l);
   }
   __syncthreads();
-  for (int it = tid; it < l * pieces; it += 256) {
-    const int t = j * l + it / pieces, c = (it % pieces) * 8;
-    const int head = c / DH, d = c % DH;
-    const size_t row = (((size_t)bag * nh + head) * n + t) * DH + d;
-    const f32x8 a = (dq_row < 0 || t == dq_row) ? load8<float>(dq + row) : (f32x8){};
+  auto store = [&](int it, const f32x8& av) {
+    int t, c;
+    (void)dq_row_of(it, t, c);
     vec8<T> out;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) out[e] = from_f<T>(scale * (a[e] + part[0][c + e]));
+    for (int e = 0; e < 8; ++e) out[e] = from_f<T>(scale * (av[e] + part[0][c + e]));
     store8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c, out);
+  };
+#pragma unroll
+  for (int u = 0; u < AQ_QP; ++u)
+    if (tid + AQ_THREADS * u < items) store(tid + AQ_THREADS * u, a[u]);
+  for (int it = tid + AQ_THREADS * AQ_QP; it < items; it += AQ_THREADS) {   // long segments (l > 40)
+    int t, c;
+    const size_t row = dq_row_of(it, t, c);
+    store(it, (dq_row < 0 || t == dq_row) ? load8<float>(dq + row) : (f32x8){});
   }
 }
 
@@ -2534,7 +2557,7 @@ extern "C" int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, co
                                       int slabs, int nbags, int nh, int n, float scale, void* dqkv, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0 && nh > 0 && nh <= 8 && slabs > 0, "assemble_q_slab: bad shape");
   TM_REQUIRE(dq && dql && slab && dqkv, "assemble_q_slab: null operand");
-  TM_DTYPE_DISPATCH(dtype, (assemble_q_slab_kernel<T><<<dim3(NL, nbags), 256, 0, (hipStream_t)stream>>>(
+  TM_DTYPE_DISPATCH(dtype, (assemble_q_slab_kernel<T><<<dim3(NL, nbags), AQ_THREADS, 0, (hipStream_t)stream>>>(
                                dq, dq_row, dql, slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL, nh, scale,
                                (T*)dqkv)));
   TM_CHECK_LAUNCH();

@@ -12,11 +12,14 @@
 //   p += m * (rect > 0 ? -lr rect sqrt(1-b2^t) / ((1-b1^t)(sqrt(v)+eps)) : -lr / (1-b1^t))
 // and Lookahead every k-th step: slow = first_sync ? p : slow + alpha (p - slow); p = slow.
 //
-// The step counters live in device memory (counters[0] = RAdam step, counters[1] = Lookahead
-// step; counters[2] unused), advanced by a 1-thread launch before the update, so the pair is
-// hipGraph-replayable.  (Advancing them from the last-finishing workgroup instead -- one
-// agent-scope fence + one same-address atomic per workgroup -- made the step 3.4x slower:
-// 108 vs 32 us.)  Flat-state offsets are multiples of 4 (each tensor padded), so a thread
+// The step counters live in device memory, one (RAdam step, Lookahead step) pair per workgroup
+// (tm_radam_counters_len ints; pair 0 is the canonical one a checkpoint stores): a workgroup reads
+// its own pair, updates with pair + 1 and writes pair + 1 back after its threads have read it, so
+// no launch or cross-workgroup ordering advances them and the step stays hipGraph-replayable.
+// Every workgroup runs every step (the tensor set is fixed once the optimizer is active), so the
+// pairs stay equal.  (A one-thread tick launch before the update cost 4.6 us per step; advancing
+// one shared pair from the last-finishing workgroup -- an agent-scope fence + a same-address
+// atomic per workgroup -- made the step 3.4x slower.)  Flat-state offsets are multiples of 4 (each tensor padded), so a thread
 // updates 4 consecutive elements with 16-B loads / stores; tensors whose param / grad pointers
 // are not 16-B aligned fall back to element-wise access.
 // HBM traffic per element: p, m, v read+write, g read = 28 B (+8 B slow on sync steps).
@@ -26,11 +29,6 @@
 namespace {
 
 constexpr int OPT_THREADS = 256, OPT_PIECES = 2, OPT_PER_BLOCK = OPT_THREADS * 4 * OPT_PIECES;
-
-__global__ void optim_tick_kernel(int* counters) {
-  counters[0] += 1;
-  counters[1] += 1;
-}
 
 struct RAdamScal {
   float bc1, bc2, rect;
@@ -105,8 +103,8 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
       }
     }
   }
-  const float step = (float)counters[0];
-  const int la_step = counters[1];
+  const int step_i = counters[2 * blockIdx.x] + 1, la_step = counters[2 * blockIdx.x + 1] + 1;
+  const float step = (float)step_i;
   RAdamScal r;
   r.bc1 = 1.0f - powf(beta1, step);
   const float b2t = powf(beta2, step);
@@ -148,9 +146,18 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
       for (int e = 0; e < n; ++e) pc[u].param[pc[u].j0 + e] = p4[u][e];
     }
   }
+  __syncthreads();   // every thread of the workgroup has read its counter pair
+  if (threadIdx.x == 0) {
+    counters[2 * blockIdx.x] = step_i;
+    counters[2 * blockIdx.x + 1] = la_step;
+  }
 }
 
 }  // namespace
+
+extern "C" long long tm_radam_counters_len(long long total_elements) {
+  return 2 * ((total_elements + OPT_PER_BLOCK - 1) / OPT_PER_BLOCK);
+}
 
 extern "C" int tm_radam_lookahead_step(const tm_optim_table* table, float* exp_avg, float* exp_avg_sq, float* slow,
                                        int* counters, float beta1, float beta2, float eps, int lookahead_k,
@@ -169,7 +176,6 @@ extern "C" int tm_radam_lookahead_step(const tm_optim_table* table, float* exp_a
   const long long total = table->offset[table->count];
   if (total == 0) return 0;
   const long long blocks = (total + OPT_PER_BLOCK - 1) / OPT_PER_BLOCK;
-  optim_tick_kernel<<<1, 1, 0, (hipStream_t)stream>>>(counters);
   radam_lookahead_kernel<<<(unsigned)blocks, OPT_THREADS, 0, (hipStream_t)stream>>>(
       *table, exp_avg, exp_avg_sq, slow, counters, beta1, beta2, eps, lookahead_k, lookahead_alpha);
   TM_CHECK_LAUNCH();

@@ -171,7 +171,9 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
         total = sum((p.numel() + 3) // 4 * 4 for p in plist)
         dev = plist[0].device
         self._flat = torch.zeros(3, total, dtype=torch.float32, device=dev)  # exp_avg, exp_avg_sq, slow
-        self._counters = torch.zeros(3, dtype=torch.int32, device=dev)   # steps + the kernel's scratch count
+        # one (RAdam step, Lookahead step) pair per workgroup of the update launch; pair 0 is checkpointed
+        self._counters = torch.zeros(max(3, int(self._lib.query("tm_radam_counters_len", total))),
+                                     dtype=torch.int32, device=dev)
         self._offsets = [0]
         for p in plist:     # each tensor's flat state padded to a multiple of 4 (16-B vectors)
             self._offsets.append(self._offsets[-1] + (p.numel() + 3) // 4 * 4)
@@ -225,7 +227,7 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
     def state_dict(self):
         sd = super().state_dict()
         if self._params is not None:
-            sd["fused_counters"] = self._counters.cpu()
+            sd["fused_counters"] = self._counters[:3].cpu()
         return sd
 
     def load_state_dict(self, state_dict):
@@ -248,7 +250,8 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
                         self._flat[row, a:b].copy_(st[key].reshape(-1))
             if counters is not None:
                 self._counters.zero_()
-                self._counters[:2].copy_(counters[:2])
+                npairs = self._counters.numel() // 2
+                self._counters[:2 * npairs].view(npairs, 2).copy_(counters[:2].to(self._counters).expand(npairs, 2))
 
 
 def create_optimizer(model: nn.Module, opt: str = "lookahead_radam", lr: float = 2e-4,
