@@ -342,6 +342,16 @@ int tm_cls_out_fwd(int dtype, const void* merged, const void* wo, const float* b
 int tm_cls_out_bwd(int dtype, const float* dH, const void* merged, const void* wo, int B, int n, int r, int S, int D,
                    float p, uint64_t seed, const uint64_t* seed_ptr, float* dwo, float* dbo, void* dmerged,
                    void* stream);
+/* tm_head_ce_bwd's one-bag fast path (B = 1, C <= 4, D = 512, no extra logits gradient) folded
+ * into tm_cls_out_bwd: every block recomputes dL/dH3 at the class row from the saved softmax, x^
+ * and rstd; dH's class row and the head / norm gradients are written as tm_head_ce_bwd writes
+ * them.  One launch instead of two on the training step's tail (code/models/TransMIL.py:202-204,
+ * model_interface.py:346-347 backward). */
+int tm_cls_head_out_bwd(int dtype, const float* prob, const long long* label, const float* gloss, int C,
+                        const float* xhat, const float* rstd, const float* gamma, const float* beta, const float* W,
+                        float* dW, float* dbias, float* dgamma, float* dbeta, float* dH, const void* merged,
+                        const void* wo, int n, int r, int S, int D, float p, uint64_t seed, const uint64_t* seed_ptr,
+                        float* dwo, float* dbo, void* dmerged, void* stream);
 int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, const void* v, const void* kl_t, const void* y_t,
                       const float* lse1, const float* wconv, int B, int nh, int n, int r, float* dq, float* dkl,
                       float* dy, float* dv, float* dwconv, void* stream);

@@ -426,3 +426,29 @@ def test_grad_allreduce_param_unused_on_one_rank():
         torch.testing.assert_close(res[r][0], torch.full((5,), 1.5))
         torch.testing.assert_close(res[r][1], torch.full((5,), 2.0))
         assert res[r][2] is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("train", [False, True])
+def test_fused_head_backward_equals_two_launch_path(train):
+    """tm_cls_head_out_bwd (head + CE backward inside layer 2's class-row to_out backward) against
+    the two-launch path (tm_head_ce_bwd then tm_cls_out_bwd, taken when the logits carry a gradient
+    of their own, here an exact zero): every parameter gradient bitwise equal, dropout on and off."""
+    from transmil_deepgraft_amd.models import TransMIL
+    torch.manual_seed(0)
+    model = TransMIL(2, 512, 512).cuda().train(train).set_compute_dtype(torch.bfloat16)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.rand(1, 700, 512, device="cuda", generator=g)
+    lab = torch.tensor([1], device="cuda")
+    c0 = model._dropout_counter.clone()
+    grads = []
+    for extra in (False, True):
+        model.zero_grad(set_to_none=True)
+        model._dropout_counter.copy_(c0)
+        logits, loss, _, _ = model.forward_ce(x, lab)
+        (loss + 0.0 * logits.sum() if extra else loss).backward()
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().clone() for n, p in model.named_parameters()})
+    bad = [n for n in grads[0] if not torch.equal(grads[0][n], grads[1][n])]
+    assert not bad, bad
+    assert all(torch.isfinite(v).all() for v in grads[0].values())

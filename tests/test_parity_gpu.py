@@ -150,14 +150,17 @@ def test_bf16_mode_close_to_oracle(N):
         assert (lo.numpy().argmax(1) == lr_np.argmax(1)).all()
 
 
-@pytest.mark.parametrize("N", [1000, 4000])
-def test_bf16_mode_grads_close_to_oracle(N):
+@pytest.mark.parametrize("N,B,ncls", [(1, 1, 2), (2, 1, 2), (3, 1, 2), (255, 1, 2), (256, 1, 3), (257, 1, 2),
+                                      (300, 2, 2), (1000, 1, 2), (4000, 1, 2)])
+def test_bf16_mode_grads_close_to_oracle(N, B, ncls):
     """Bench-mode (bf16 operands) gradients against the fp64 oracle: every parameter's
-    gradient within 6e-2 of its max magnitude (bf16 operands carry ~3 significant digits)."""
-    ref, ours = _pair(2, dtype=torch.bfloat16)
-    x = torch.from_numpy(bag_input(N, 512, 99 + N))
-    lr, gr = _ref_forward_backward(ref, x, 1, 2)
-    lo, go = _ours_forward_backward(ours, x, 1, 2)
+    gradient within 6e-2 of its max magnitude (bf16 operands carry ~3 significant digits).
+    Ragged and tiny bags (n' = 256: one landmark segment of l = 1; S = 256 / 257 around the pad
+    boundary) and B = 2 bags through the bf16 kernels' split / clamp paths."""
+    ref, ours = _pair(ncls, dtype=torch.bfloat16)
+    x = torch.from_numpy(bag_input(N, 512, 99 + N, B))
+    lr, gr = _ref_forward_backward(ref, x, 1, ncls)
+    lo, go = _ours_forward_backward(ours, x, 1, ncls)
     np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=5e-2)
     bad = []
     for name, g in gr.items():

@@ -138,6 +138,7 @@ _SIGS = {
     "tm_cls_a1_row_fwd": (I, [I, P, P, P, P, P, I, I, I, I, P, P, P]),
     "tm_cls_out_fwd": (I, [I, P, P, P, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_cls_out_bwd": (I, [I, P, P, P, I, I, I, I, I, Fl, U64, P, P, P, P, P]),
+    "tm_cls_head_out_bwd": (I, [I, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, Fl, U64, P, P, P, P, P]),
     "tm_cls_a1_row_bwd": (I, [I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),

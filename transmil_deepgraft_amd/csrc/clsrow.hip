@@ -13,6 +13,7 @@
 // kernels.  The values computed here are the ones the dense kernels produce for these rows
 // (the other rows' contributions are exact zeros), summed in a fixed order.
 #include "common.h"
+#include "head_bwd.h"
 #include "../../include/transmil_hip.h"
 
 namespace {
@@ -195,16 +196,38 @@ TM_DEV float dout_at(const float* __restrict__ dH, int b, int c, int S, int D, f
 //   blocks [B*D/64, +D/2):         dWo[c][k] = sum_b dout[b][c] merged[b][r][k]   (2 rows c per block)
 //   the last block:                dbo[c] = sum_b dout[b][c]
 // block 256.
+// head + CrossEntropy backward folded into the class-row to_out backward (one bag, <= 4 classes,
+// D = 512: the training step's fast path; layernorm.hip head_ce_bwd_kernel's B = 1 branch, same
+// arithmetic): every block recomputes dL/dH3 at the class row (one wave, 8 channels per lane) from
+// the saved softmax, x^ and rstd; the last block also writes it to dH and the head / norm gradients.
+struct HeadBwd {
+  const float* prob; const long long* label; const float* g;   // prob [C], label [1], dL/dloss [1]
+  const float* xhat; const float* rstd; const float* gamma; const float* beta; const float* W;   // W [C][D]
+  float* dW; float* dbias; float* dgamma; float* dbeta;
+  int C;
+};
+
 template <typename T>
-__global__ __launch_bounds__(256) void cls_out_bwd_kernel(const float* __restrict__ dH, const T* __restrict__ merged,
+__global__ __launch_bounds__(256) void cls_out_bwd_kernel(const float* __restrict__ dH_in, const T* __restrict__ merged,
                                                           const T* __restrict__ wo, int B, int n, int r, int S, int D,
                                                           float p, float scale, uint64_t seed0,
                                                           const uint64_t* __restrict__ seed_ptr, float* __restrict__ dwo,
-                                                          float* __restrict__ dbo, T* __restrict__ dmerged) {
-  extern __shared__ float dsh[];  // [D] dout of one bag, then [32][64] partials
+                                                          float* __restrict__ dbo, T* __restrict__ dmerged, HeadBwd hb) {
+  extern __shared__ float dsh[];  // [D] dout of one bag, then [32][64] partials; head mode: [D] dL/dH3 after them
   const int tid = threadIdx.x, blk = blockIdx.x;
   const uint64_t seed = p > 0.f ? effective_seed(seed0, seed_ptr) : 0;
   const int nm = B * (D / 64);
+  const float* dH = dH_in;
+  if (hb.prob) {   // B = 1, D = 512 (host-checked): the class row's gradient from the head, in LDS
+    float* hs = dsh + D + 32 * DH;
+    if (tid < 64) {
+      const bool last = blk == (int)gridDim.x - 1;
+      head_bwd_b1<8>(hb.prob, hb.label, hb.g, nullptr, hb.C, hb.xhat, hb.rstd, hb.gamma, hb.beta, hb.W,
+                     last ? hb.dW : nullptr, hb.dbias, hb.dgamma, hb.dbeta, last ? (float*)dH_in : nullptr, hs, tid);
+    }
+    __syncthreads();
+    dH = hs;        // dout_at reads row b * S = 0 of it
+  }
   if (blk < nm) {
     const int b = blk / (D / 64), k0 = (blk % (D / 64)) * 64;
     for (int c = tid; c < D; c += 256) dsh[c] = dout_at<T>(dH, b, c, S, D, p, scale, seed);
@@ -366,7 +389,29 @@ extern "C" int tm_cls_out_bwd(int dtype, const float* dH, const void* merged, co
   const int blocks = B * (D / 64) + D / 2 + 1;
   const size_t sm = (size_t)(D + 32 * 64) * sizeof(float);
   TM_CLS_DISPATCH(dtype, (cls_out_bwd_kernel<T><<<blocks, 256, sm, (hipStream_t)stream>>>(
-                             dH, (const T*)merged, (const T*)wo, B, n, r, S, D, p, scale, seed, seed_ptr, dwo, dbo, (T*)dmerged)));
+                             dH, (const T*)merged, (const T*)wo, B, n, r, S, D, p, scale, seed, seed_ptr, dwo, dbo, (T*)dmerged,
+                             HeadBwd{})));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_cls_head_out_bwd(int dtype, const float* prob, const long long* label, const float* gloss, int C,
+                                   const float* xhat, const float* rstd, const float* gamma, const float* beta,
+                                   const float* W, float* dW, float* dbias, float* dgamma, float* dbeta, float* dH,
+                                   const void* merged, const void* wo, int n, int r, int S, int D, float p,
+                                   uint64_t seed, const uint64_t* seed_ptr, float* dwo, float* dbo, void* dmerged,
+                                   void* stream) {
+  TM_REQUIRE(prob && label && gloss && xhat && rstd && gamma && beta && W && dW && dbias && dgamma && dbeta,
+             "cls_head_out_bwd: bad head args");
+  TM_REQUIRE(dH && merged && wo && dwo && dbo && dmerged, "cls_head_out_bwd: bad args");
+  TM_REQUIRE(D == 512 && C >= 1 && C <= 4, "cls_head_out_bwd: one bag, D = 512, <= 4 classes");
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const int blocks = (D / 64) + D / 2 + 1;
+  const size_t sm = (size_t)(2 * D + 32 * 64) * sizeof(float);
+  const HeadBwd hb{prob, label, gloss, xhat, rstd, gamma, beta, W, dW, dbias, dgamma, dbeta, C};
+  TM_CLS_DISPATCH(dtype, (cls_out_bwd_kernel<T><<<blocks, 256, sm, (hipStream_t)stream>>>(
+                             dH, (const T*)merged, (const T*)wo, 1, n, r, S, D, p, scale, seed, seed_ptr, dwo, dbo, (T*)dmerged,
+                             hb)));
   TM_CHECK_LAUNCH();
   return 0;
 }

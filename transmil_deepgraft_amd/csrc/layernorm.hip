@@ -7,6 +7,7 @@
 // [B, n', D] layout NystromAttention consumes (SURVEY.md App. A eq. 1), with
 // the pad rows zeroed, so no separate pad copy exists.
 #include "common.h"
+#include "head_bwd.h"
 #include "../../include/transmil_hip.h"
 
 namespace {
@@ -378,42 +379,8 @@ __global__ void head_ce_bwd_kernel(const float* __restrict__ prob, const long lo
   const int lane = threadIdx.x;
   const float gs = g[0] / (float)B;
   if (B == 1 && C <= 4) {
-    const int lab = (int)label[0];
-    float dl[4], gm[VPL], bt[VPL], xh[VPL], w[4][VPL];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      dl[k] = k < C ? gs * (prob[k] - (k == lab ? 1.f : 0.f)) + (dlogits_in ? dlogits_in[k] : 0.f) : 0.f;
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int c = lane * VPL + i;
-      gm[i] = gamma[c]; bt[i] = beta[c]; xh[i] = xhat[c];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) w[k][i] = k < C ? W[(size_t)k * D + c] : 0.f;
-    }
-    float gg[VPL], s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) {
-      const int c = lane * VPL + i;
-      float dy = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (k < C) {
-          dW[(size_t)k * D + c] = 0.f + dl[k] * (xh[i] * gm[i] + bt[i]);
-          dy += dl[k] * w[k][i];
-        }
-      dgamma[c] = 0.f + dy * xh[i];
-      dbeta[c] = 0.f + dy;
-      gg[i] = dy * gm[i];
-      s1 += gg[i];
-      s2 += gg[i] * xh[i];
-    }
-    if (lane == 0)
-      for (int k = 0; k < C; ++k) dbias[k] = 0.f + dl[k];
-    s1 = wave_sum(s1) * (1.0f / D);
-    s2 = wave_sum(s2) * (1.0f / D);
-    const float rs = rstd[0];
-#pragma unroll
-    for (int i = 0; i < VPL; ++i) dh[lane * VPL + i] = rs * (gg[i] - s1 - xh[i] * s2);
+    head_bwd_b1<VPL>(prob, label, g, dlogits_in, C, xhat, rstd, gamma, beta, W, dW, dbias, dgamma, dbeta, dh, nullptr,
+                     lane);
     return;
   }
   // general B / C: dlogits into the scratch, then the general head backward

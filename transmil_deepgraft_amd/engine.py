@@ -520,18 +520,25 @@ def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, see
     return Hout, saved
 
 
-def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_code, pool, dout=None):
+def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_code, pool, dout=None, head=None):
     """dH [B*S, D] fp32 (gradient of the layer output) is turned IN PLACE into the
     gradient of the layer input.  Parameter gradients go to ``grads``.  ``dout``: the padded
-    to_out-dropout gradient, already written by the producer of dH (tm_ppeg_bwd)."""
+    to_out-dropout gradient, already written by the producer of dH (tm_ppeg_bwd).  ``head``: the
+    tm_cls_head_out_bwd head arguments (class-row layer only): dH's class row is then computed
+    by that launch from the CE head instead of read."""
     B, S, n, D, pad = geo.B, geo.S, geo.n, geo.D, geo.pad
     st = _stream()
     if saved["cls_only"]:
         # dH is zero outside the class rows: dropout, dWo, dbo and dmerged on those rows only
         dmerged = pool(B * D, tdtype).view(B, D)
-        _lib.call("tm_cls_out_bwd", dt_code, _p(dH), _p(saved["merged"]), _p(prm["wo"]), B, n, pad, S, D,
-                  C.c_float(saved["drop_p"]), C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(grads["wo"]),
-                  _p(grads["bo"]), _p(dmerged), st)
+        if head is not None:
+            _lib.call("tm_cls_head_out_bwd", dt_code, *head, _p(dH), _p(saved["merged"]), _p(prm["wo"]), n, pad, S,
+                      D, C.c_float(saved["drop_p"]), C.c_uint64(saved["seed"]), _p(saved["seed_dev"]),
+                      _p(grads["wo"]), _p(grads["bo"]), _p(dmerged), st)
+        else:
+            _lib.call("tm_cls_out_bwd", dt_code, _p(dH), _p(saved["merged"]), _p(prm["wo"]), B, n, pad, S, D,
+                      C.c_float(saved["drop_p"]), C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(grads["wo"]),
+                      _p(grads["bo"]), _p(dmerged), st)
     else:
         if dout is None:
             dout = pool(B * n * D, tdtype).view(B, n, D)
@@ -793,7 +800,15 @@ class TransMILEngine:
         Ccls = prm["fc_w"].shape[0]
         # layer 2 on the class rows reads dL/dH3 only there (its LayerNorm backward writes the rest)
         dH = (torch.empty if self.cls_only else torch.zeros)(B * S, D, dtype=torch.float32, device=dev)
-        if gloss is not None:
+        head = None
+        if gloss is not None and dlogits is None and self.cls_only and B == 1 and Ccls <= 4 and D == 512:
+            # the head + CE backward rides in layer 2's class-row to_out backward launch
+            gls = gloss.float().contiguous()
+            ctx["_gloss"] = gls     # keep the scalar alive until the launch is enqueued
+            head = (_p(ctx["ce"][1]), _p(ctx["ce"][0]), _p(gls), Ccls, _p(ctx["xhat"]), _p(ctx["hrstd"]),
+                    _p(prm["norm_w"]), _p(prm["norm_b"]), _p(prm["fc_w"]), _p(g[self.head + ".weight"]),
+                    _p(g[self.head + ".bias"]), _p(g["norm.weight"]), _p(g["norm.bias"]))
+        elif gloss is not None:
             label, prob = ctx["ce"][0], ctx["ce"][1]
             scratch = None if (B == 1 and Ccls <= 4) else pool(B * Ccls)
             dl_in = None if dlogits is None else dlogits.float().contiguous()
@@ -812,7 +827,8 @@ class TransMILEngine:
             gl = {"wo": g[pre + "attn.to_out.0.weight"], "bo": g[pre + "attn.to_out.0.bias"],
                   "wqkv": g[pre + "attn.to_qkv.weight"], "wconv": g[pre + "attn.res_conv.weight"],
                   "norm_w": g[pre + "norm.weight"], "norm_b": g[pre + "norm.bias"]}
-            translayer_backward(dH, Hin, saved, geo, prm[li], gl, self.tdtype, self.dt_code, pool, dout=dout1)
+            translayer_backward(dH, Hin, saved, geo, prm[li], gl, self.tdtype, self.dt_code, pool, dout=dout1,
+                                head=head if li == 2 else None)
             if li == 2:
                 dH1 = pool(B * S * D).view(B * S, D)
                 work = pool(_lib.query("tm_ppeg_bwd_workspace", B, geo.G, D) // 4)
