@@ -63,6 +63,10 @@ typedef struct tm_gemm_args {
   /* dropout seed read from device memory when non-NULL: seed = *seed_ptr * 0x9E3779B97F4A7C15 + seed
    * (keeps a hipGraph replay drawing a fresh mask every step) */
   const uint64_t* seed_ptr;
+  /* bf16 weight-gradient split-K (a_trans = 1, TM_EPI_SPLITK, K and k_per_split multiples of 64)
+   * only, else NULL: colsum[z][m] = sum over split z's k of A[k][m] (the bias gradient of the same
+   * dY, summed by the workgroups of the first column tile while they stage A) -- [splits][M] fp32 */
+  float* colsum;
 } tm_gemm_args;
 
 int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* args, void* stream);

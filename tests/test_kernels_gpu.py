@@ -124,18 +124,23 @@ def test_gemm_dropout_residual_and_splitk():
     assert _rel(res.cpu(), dY.double().t() @ X.double()) < 1e-5
 
 
-def test_gemm_ring_splitk_weight_grad_bf16():
-    """bf16 split-K weight gradient through the global_load_lds ring (K = 33 x 256)."""
-    from transmil_deepgraft_amd.engine import weight_grad, Pool
+@pytest.mark.parametrize("M,N,K", [(192, 136, 33 * 256), (512, 512, 8448), (520, 512, 8192)])
+def test_gemm_ring_splitk_weight_grad_bf16(M, N, K):
+    """bf16 split-K weight gradient through the global_load_lds ring, with the bias gradient
+    (column sums of dY) summed by the same launch (tm_gemm_args.colsum); M = 520: a ragged last
+    column tile of the A image (clamped chunks must not leak into the sums)."""
+    from transmil_deepgraft_amd.engine import weight_grad, Pool, flush_reductions
     from transmil_deepgraft_amd._lib import BF16
     g = torch.Generator().manual_seed(5)
-    K = 33 * 256
-    dY = torch.randn(K, 192, generator=g).bfloat16()
-    X = torch.randn(K, 136, generator=g).bfloat16()
-    res = torch.empty(192, 136, device=DEV)
-    weight_grad(dY.to(DEV), X.to(DEV), res, 192, 136, K, ldy=192, ldx=136, dtype=BF16, work_pool=Pool(DEV))
+    dY = torch.randn(K, M, generator=g).bfloat16()
+    X = torch.randn(K, N, generator=g).bfloat16()
+    res = torch.empty(M, N, device=DEV)
+    bias = torch.full((M,), float("nan"), device=DEV)
+    weight_grad(dY.to(DEV), X.to(DEV), res, M, N, K, ldy=M, ldx=N, dtype=BF16, work_pool=Pool(DEV), bias_out=bias)
+    flush_reductions()
     torch.cuda.synchronize()
     assert _rel(res.cpu(), dY.double().t() @ X.double()) < 1e-5
+    assert _rel(bias.cpu(), dY.double().sum(0)) < 1e-5
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

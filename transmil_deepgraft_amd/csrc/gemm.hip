@@ -654,6 +654,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
   f32x16 acc[2];
   acc[0] = (f32x16){};
   acc[1] = (f32x16){};
+  constexpr bool COLSUM = A_T && KIND == EK_SPLITK && !STAMP;
+  const bool do_cs = COLSUM && g.colsum != nullptr && n0 == 0;   // block-uniform
+  const int cs_c = tid & 15, cs_r = tid >> 4;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   // fragment addresses relative to a stage: A at +0, B at +STAGE_BYTES/2
   unsigned akc[4] = {0, 0, 0, 0}, bkc0[4] = {0, 0, 0, 0}, bkc1[4] = {0, 0, 0, 0};
   unsigned aks = 0, bks0 = 0, bks1 = 0;
@@ -690,6 +694,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
     const unsigned sb = ring + (kt % NS) * STAGE_BYTES;
     ring_tile_mma<A_T, B_KN>(acc, (A_T ? aks : 0) + sb, (B_KN ? bks0 : 0) + sb, (B_KN ? bks1 : 0) + sb,
                              akc, bkc0, bkc1);
+    if constexpr (COLSUM) {
+      // the bias gradient of the same dY: this tile's 64 k-rows of A summed per column (thread:
+      // 16-B column chunk cs_c of k-rows cs_r and cs_r + 32), behind the tile's MFMAs
+      if (do_cs) {
+        const char* img = smem + (kt % NS) * STAGE_BYTES;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int kk = cs_r + 32 * j;
+          const bf16x8 v = *(const bf16x8*)(img + kk * 256 + ((cs_c ^ (2 * (kk & 3))) << 4));
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += (float)v[e];
+        }
+      }
+    }
   }
   ring_stamp<STAMP>(ts, 3);
   __syncthreads();  // all fragment reads done before the epilogue reuses the ring
@@ -718,6 +736,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
     }
   } else
   gemm_epilogue_rows<OutT, BN, BM, 512, KIND>(smem, C, g, m0, n0, zs);
+  if constexpr (COLSUM) {
+    if (do_cs) {
+      // the 32 k-row groups of each column chunk: lanes c, c + 16, c + 32, c + 48 of a wave, then
+      // the 8 waves through LDS (the epilogue is done with it), summed in wave order
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        csum[e] += __shfl_xor(csum[e], 16, 64);
+        csum[e] += __shfl_xor(csum[e], 32, 64);
+      }
+      __syncthreads();
+      float* red = (float*)smem;   // [8 waves][128 columns]
+      if (lane < 16) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[wave * 128 + cs_c * 8 + e] = csum[e];
+      }
+      __syncthreads();
+      if (tid < 128 && m0 + tid < g.M) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) s += red[w * 128 + tid];
+        g.colsum[(size_t)zs * g.M + m0 + tid] = s;
+      }
+    }
+  }
   if constexpr (STAMP) {
     ring_stamp<STAMP>(ts, 5);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1391,6 +1433,10 @@ extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args
   TM_REQUIRE(g->lda % E == 0 && g->ldb % E == 0, "gemm: leading dimensions must be multiples of 16 B");
   TM_REQUIRE(g->mode != TM_EPI_QKV || (g->dh % 8 == 0 && g->N % 8 == 0), "gemm: QKV scatter needs dh % 8 == 0");
   if (g->M == 0 || g->N == 0) return 0;
+  // the fused bias-gradient column sums ride in the bf16 ring kernel's split-K weight-gradient form only
+  TM_REQUIRE(!g->colsum || (g->ab_dtype == TM_BF16 && g->c_dtype == TM_F32 && g->a_trans && g->mode == TM_EPI_SPLITK &&
+                            ring_ok<float>(*g) && (GEMM_VARIANT == 0 || GEMM_VARIANT == 5 || GEMM_VARIANT == 9)),
+             "gemm: colsum needs the bf16 split-K weight-gradient ring path (a_trans, K % 64 == 0, M % 8 == 0)");
   hipStream_t st = (hipStream_t)stream;
   if (g->ab_dtype == TM_BF16) {
     TM_REQUIRE(g->k_per_split % 64 == 0 || g->splits == 1, "gemm: bf16 k_per_split must be a multiple of 64");

@@ -161,12 +161,16 @@ def cu_count():
     return _CU[dev]
 
 
-def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool):
-    """out[M,N] (fp32) = sum_k dY[k, m] X[k, n]  (split-K, deterministic)."""
+def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=None):
+    """out[M,N] (fp32) = sum_k dY[k, m] X[k, n]  (split-K, deterministic).  ``bias_out`` [M]: also
+    the bias gradient sum_k dY[k, m] -- in bf16 mode summed by the weight-gradient kernel itself
+    while it stages dY (tm_gemm_args.colsum), else one tm_colsum pass."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     splits = max(1, min(16, cu_count() // max(tiles, 1), (K + 255) // 256))   # <= one workgroup per CU
     if splits == 1:
         gemm(dY, X, out, M, N, K, lda=ldy, ldb=ldx, ldc=N, a_trans=1, b_kn=1, dtype=dtype, c_dtype=F32)
+        if bias_out is not None:
+            colsum(dY, K, M, ldy, dtype, bias_out, work_pool)
         return
     bk = 64 if dtype == BF16 else 32
     kps = ((K + splits - 1) // splits + bk - 1) // bk * bk
@@ -180,8 +184,16 @@ def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool):
     g.splits, g.k_per_split = splits, kps
     g.mode = EPI_SPLITK
     g.alpha = 1.0
+    fuse = bias_out is not None and dtype == BF16 and K % 64 == 0 and M % 8 == 0 and N % 8 == 0
+    cs = work_pool(splits * M) if fuse else None
+    if fuse:
+        g.colsum = cs.data_ptr()
     _lib.call("tm_gemm", _p(dY), _p(X), _p(slab), C.byref(g), _stream())
     _lib.call("tm_splitk_reduce", _p(slab), _p(out), splits, M * N, C.c_float(1.0), 0, _rq(), _stream())
+    if fuse:
+        _lib.call("tm_splitk_reduce", _p(cs), _p(bias_out), splits, M, C.c_float(1.0), 0, _rq(), _stream())
+    elif bias_out is not None:
+        colsum(dY, K, M, ldy, dtype, bias_out, work_pool)
 
 
 def colsum(X, rows, cols, ld, dtype, out, work_pool, accumulate=False):
@@ -547,8 +559,7 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
         # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
         with defer_reductions():
             weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code,
-                        work_pool=pool)
-            colsum(dout, B * n, D, D, dt_code, grads["bo"], pool)
+                        work_pool=pool, bias_out=grads["bo"])
         dmerged = pool(B * n * D, tdtype).view(B, n, D)
         gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     dqkv = nystrom_core_backward(dmerged, saved["merged"], saved["qkv"], saved["core"], geo, prm["wconv"],
@@ -867,8 +878,7 @@ class TransMILEngine:
         Fx = F if inner is None else prm["w0"].shape[0]
         with defer_reductions():
             weight_grad(dpre, ctx["xt"], g[main + ".weight"], D, Fx, B * N, ldy=D, ldx=Fx, dtype=self.dt_code,
-                        work_pool=pool)
-            colsum(dpre, B * N, D, D, self.dt_code, g[main + ".bias"], pool)
+                        work_pool=pool, bias_out=g[main + ".bias"])
         if inner is not None:
             # d LN-out = dpre W1 ; LayerNorm backward ; GELU backward ; W0 / b0 gradients
             w0n, lnn = self.fc1["inner"]
@@ -884,8 +894,7 @@ class TransMILEngine:
             dpre0 = pool(B * N * Fm, self.tdtype).view(B * N, Fm)
             _lib.call("tm_gelu_bwd", self.dt_code, _p(dy0), _p(inner["pre0"]), B * N * Fm, _p(dpre0), st)
             weight_grad(dpre0, inner["xt"], g[w0n + ".weight"], Fm, Fin, B * N, ldy=Fm, ldx=Fin, dtype=self.dt_code,
-                        work_pool=pool)
-            colsum(dpre0, B * N, Fm, Fm, self.dt_code, g[w0n + ".bias"], pool)
+                        work_pool=pool, bias_out=g[w0n + ".bias"])
         flush_reductions()
         if ready is not None:
             ready(1)
@@ -947,8 +956,8 @@ class NystromEngine:
                   C.c_float(ctx["drop_p"]), C.c_uint64(ctx["seed"]), _p(ctx["seed_dev"]), _p(dpad), st)
         dwo = torch.empty(D, D, dtype=torch.float32, device=dout.device)
         dbo = torch.empty(D, dtype=torch.float32, device=dout.device)
-        weight_grad(dpad, ctx["merged"], dwo, D, D, B * n, ldy=D, ldx=D, dtype=self.dt_code, work_pool=pool)
-        colsum(dpad, B * n, D, D, self.dt_code, dbo, pool)
+        weight_grad(dpad, ctx["merged"], dwo, D, D, B * n, ldy=D, ldx=D, dtype=self.dt_code, work_pool=pool,
+                    bias_out=dbo)
         dmerged = pool(B * n * D, self.tdtype).view(B, n, D)
         gemm(dpad, ctx["wo_t"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=self.dt_code)
         dwconv = torch.empty_like(ctx["wconv"], dtype=torch.float32)
