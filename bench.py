@@ -92,17 +92,17 @@ def roofline_model(site, n_patches, dtype_bytes):
                     note="fp32-class products as bf16 hi/lo x3 on the bf16 MFMA; units = launches per call")
     if site == "pinv_bwd":
         # the adjoint of the chain (pinv_split.hip bwd_level_job), per iteration 8 products of 256^3 per
-        # head in 4 launches (dT5, dZa | dP, dT3 | dP += dT3 P^T + P^T dT3 | dX, G), then the c-gradient
-        # dot and the apply launch (Z_0 = X^T / c terms + the A2 softmax backward);
-        # bytes: every operand / addend read and every output written once per level as split bf16
-        # planes (4 B per element; dX fp32): 14 matrices read + 7 written per iteration, then G, X
-        # (c-dot) and X, G, dX in + out (apply)
+        # head in 4 launches (dT5, dZa | dP, dT3 | dP += dT3 P^T + P^T dT3 | dX, G; the last one also
+        # the c-gradient dot of G0 with X^T), then the apply launch (Z_0 = X^T / c terms + the A2
+        # softmax backward); bytes: every operand / addend read and every output written once per
+        # level as split bf16 planes (4 B per element; dX fp32): 14 matrices read + 7 written per
+        # iteration, X (fp32, the dot), then X, G, dX in + out (apply)
         mat = heads * m * m * 4
         flops = 6 * 8 * heads * 2 * m ** 3
-        byts = mat * (6 * (14 + 7) + 2 + 4)
-        return dict(bytes=byts, flops=flops, peak_tfs=F32_MATRIX_PEAK_TFS, units=26,
+        byts = mat * (6 * (14 + 7) + 1 + 4)
+        return dict(bytes=byts, flops=flops, peak_tfs=F32_MATRIX_PEAK_TFS, units=25,
                     note="fp32-class products as bf16 hi/lo x3 on the bf16 MFMA; 24 pinv_stage_kernel launches "
-                         "+ pinv_c_dot_kernel + pinv_apply_bwd_kernel per call; units = launches per call")
+                         "(the last with the c-gradient dot) + pinv_apply_bwd_kernel per call; units = launches per call")
     if site == "a1_fwd":
         # read q, v (conv) [n, 512] T; write merged [n, 512] T + lse [8, n] fp32; landmarks/Y fp32
         byts = 3 * n * 512 * t + heads * n * 4 + 2 * heads * m * dh * 4
@@ -487,8 +487,7 @@ def main():
             roof.update(event_span_ms=round(site_mean(span_samples, site), 5),
                         event_pair_overhead_ms=round(site_mean(overhead_samples, site), 5))
         kname = {"pinv_fwd": "pinv_stage_kernel x14 (tm_pinv_fwd_split_a3)",
-                 "pinv_bwd": "pinv_stage_kernel x24 + pinv_c_dot_kernel + pinv_apply_bwd_kernel "
-                             "(tm_pinv_bwd_split)"}.get(site, site)
+                 "pinv_bwd": "pinv_stage_kernel x24 + pinv_apply_bwd_kernel (tm_pinv_bwd_split)"}.get(site, site)
         roof.update(kernel=kname, kernel_ms=round(kernel_ms, 5),
                     samples=sum(1 for nm, _ in kernel_ms_samples if nm == site),
                     algorithmic_bytes=rm["bytes"], algorithmic_flops=rm["flops"])

@@ -104,22 +104,21 @@ def main():
         sites["pinv_fwd"] = dict(n=a.n, dtype="bf16", kernel="pinv_stage_kernel x14 (tm_pinv_fwd_split_a3)",
                                  traffic_bytes=int(2 * mean(cf) + mean(cw)),
                                  algorithmic_bytes=work.get("bytes"), dispatches=[len(cf), len(cw)])
-    # pinv backward: the 24 pinv_stage dispatches before each pinv_c_dot_kernel, the c-dot, and the
-    # pinv_apply_bwd_kernel after it
+    # pinv backward: the 24 pinv_stage dispatches before each pinv_apply_bwd_kernel (the last one
+    # also computes the c-gradient dot) and the apply itself
     def bwd_chains(rows):
         out = []
         for i, (_, k, b) in enumerate(rows):
-            if not k.startswith("pinv_c_dot_kernel"):
+            if not k.startswith("pinv_apply_bwd_kernel"):
                 continue
             seq = [bb for _, kk, bb in rows[max(0, i - 60):i] if kk.startswith("pinv_stage_kernel")][-24:]
-            app = [bb for _, kk, bb in rows[i + 1:i + 4] if kk.startswith("pinv_apply_bwd_kernel")][:1]
-            if len(seq) == 24 and app:
-                out.append(sum(seq) + b + app[0])
+            if len(seq) == 24:
+                out.append(sum(seq) + b)
         return out
     bf, bw = bwd_chains(fe), bwd_chains(wr)
     if bf and bw:
         work = bench.roofline_model("pinv_bwd", a.n, 2)
-        sites["pinv_bwd"] = dict(n=a.n, dtype="bf16", kernel="pinv_stage_kernel x24 + pinv_c_dot_kernel + "
+        sites["pinv_bwd"] = dict(n=a.n, dtype="bf16", kernel="pinv_stage_kernel x24 + "
                                  "pinv_apply_bwd_kernel (tm_pinv_bwd_split)",
                                  traffic_bytes=int(2 * mean(bf) + mean(bw)),
                                  algorithmic_bytes=work.get("bytes"), dispatches=[len(bf), len(bw)])

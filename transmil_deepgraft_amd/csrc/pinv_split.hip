@@ -78,6 +78,10 @@ struct SJob {
   float* cf;                                // optional fp32 copy of v
   bf16* c2; float c2_alpha, c2_diag, c2_e1; // optional split: c2_alpha*s + c2_diag*I + c2_e1*E1'
   bf16* c3; float c3_e1; int pad1;          // optional split: c3_e1 * E1'
+  // optional: per-wave partials of sum_ij v[i][j] * dotx[j][i] (dotx fp32, head-major like the
+  // output) at dot_part[((head * 16 + tile) * 8 + wave)] -- the c gradient's dot of the backward's
+  // last level, without a separate launch
+  const float* dotx; float* dot_part;
 };
 
 struct SLaunch {
@@ -318,6 +322,12 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
   const bool epi = tid < 512;  // the 512 threads that each own one 8-element piece of the 64x64 tile
   if (e1p && epi) eload(e1p, e1f, e1raw);
   if (e2p && epi) eload(e2p, e2f, e2raw);
+  // the transposed dotx piece of this thread's 8 outputs: dotx[col + e][row]
+  float dxv[8];
+  if (J.dotx && epi) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dxv[e] = J.dotx[hoff + (size_t)(n0 + lc + e) * NL + m0 + lr];
+  }
   // per-head maxima for 1/c: one raw vector load per lane now, reduced in the epilogue
   const bool need_c = J.alpha_cpow || J.e1_cpow;
   float mcv = -INFINITY, mrv = -INFINITY;
@@ -446,6 +456,13 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
       for (int e = 0; e < 8; ++e) w[e] = c3e * e1v[e];
       store_split8(J.c3, plane, eoff, w);
     }
+    if (J.dotx) {
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(v[e], dxv[e], d);
+      d = wave_sum(d);
+      if (lane == 0) J.dot_part[((size_t)head * 16 + tile) * 8 + wv] = d;
+    }
   }
   if (st_on && wv < 4) {
     ts[6] = stamp();
@@ -494,33 +511,8 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
 
 // ---------------------------------------------------------------------------
 // Backward of Z_0 = X^T / c (c = max_i rowsum|X|_i * max_j colsum|X|_j) and of A2 = softmax.
-// part[bh*16 + y] = sum over rows i of slice y of G0[i][j] * X[j][i]   (grid (nbh, 16))
-__global__ __launch_bounds__(256) void pinv_c_dot_kernel(const bf16* __restrict__ G0, long long plane,
-                                                         const float* __restrict__ X, float* __restrict__ part) {
-  __shared__ float red[4];
-  const int bh = blockIdx.x, i0 = blockIdx.y * 16, j = threadIdx.x;
-  const size_t hb = (size_t)bh * MAT;
-  float xs[16];
-  {
-    const float* xr = X + hb + (size_t)j * NL + i0;  // X[j][i0..i0+15]
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 v = *(const f32x4*)(xr + 4 * q);
-      xs[4 * q] = v[0]; xs[4 * q + 1] = v[1]; xs[4 * q + 2] = v[2]; xs[4 * q + 3] = v[3];
-    }
-  }
-  float s = 0.f;
-#pragma unroll
-  for (int ii = 0; ii < 16; ++ii) {
-    const size_t o = hb + (size_t)(i0 + ii) * NL + j;
-    s += ((float)G0[o] + (float)G0[o + plane]) * xs[ii];
-  }
-  s = wave_sum(s);
-  if ((j & 63) == 0) red[j >> 6] = s;
-  __syncthreads();
-  if (j == 0) part[bh * 16 + blockIdx.y] = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
+// part: npart partial dots of sum_ij G0[i][j] X[j][i], written by the backward chain's last level
+// (SJob.dotx: one per wave of every output tile).
 // dX[i][j] = dXc[i][j] + G0[j][i]/c + sign(X_ij) (tie_c(i) dMc/nc + tie_r(j) dMr/nr),
 // dc = -sum(G0 o Z0)/c = -T/c^2,  dMc = dc * maxr, dMr = dc * maxc  (max ties share the gradient);
 // softmax != 0: out = X o (dX - rowsum(X o dX)) (the backward of A2 = softmax, X = A2), else out = dX.
@@ -528,7 +520,8 @@ __global__ __launch_bounds__(256) void pinv_c_dot_kernel(const bf16* __restrict_
 constexpr int APPLY_SUMS = 8;   // |X| sums per thread per kind in one burst (nbh <= 8); larger nbh loops
 __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __restrict__ X, const float* __restrict__ sums,
                                                              const float* __restrict__ maxima, const bf16* __restrict__ G0,
-                                                             long long plane, const float* __restrict__ part, int nbh,
+                                                             long long plane, const float* __restrict__ part, int npart,
+                                                             int nbh,
                                                              const float* __restrict__ dXc, int softmax,
                                                              float* __restrict__ out) {
   __shared__ float red[4][16];
@@ -571,7 +564,7 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
     sr[u] = sums[total + e];
   }
   const float mcl = lane < nbh ? maxima[lane] : -INFINITY, mrl = lane < nbh ? maxima[nbh + lane] : -INFINITY;
-  float ps = t < nbh * 16 ? part[t] : 0.f;
+  float ps = t < npart ? part[t] : 0.f;
   // global maxima (nbh <= 64: one lane per head), tie counts, the fixed-order partial-dot sum
   float mc = wave_max(mcl), mr = wave_max(mrl);
   for (int h = 64; h < nbh; ++h) { mc = fmaxf(mc, maxima[h]); mr = fmaxf(mr, maxima[nbh + h]); }
@@ -580,7 +573,7 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
   for (int u = 0; u < APPLY_SUMS; ++u)
     if (t + 256 * u < total) { nc += sc[u] == mc; nr += sr[u] == mr; }
   for (int e = t + 256 * APPLY_SUMS; e < total; e += 256) { nc += sums[e] == mc; nr += sums[total + e] == mr; }
-  for (int e = t + 256; e < nbh * 16; e += 256) ps += part[e];
+  for (int e = t + 256; e < npart; e += 256) ps += part[e];
   nc = wave_sum(nc); nr = wave_sum(nr); ps = wave_sum(ps);
   if (lane == 0) { red[wave][0] = nc; red[wave][1] = nr; red[wave][2] = ps; }
   __syncthreads();
@@ -669,6 +662,8 @@ struct ChainArgs {
   float* saved;     // FwdLayout
   float* work;      // backward workspace (G, dT5, dZa, dP, dT3, dXc, partial dots)
   int nbh, iters;
+  const float* X = nullptr;   // fp32 X: the backward's last level also writes the c-gradient dots
+  float* part = nullptr;      //   (per-wave partials of sum G0 o X^T) when set
 };
 
 // forward levels after L1 (S = X X^T + the |X| sums): A_0, B_0, A_1, B_1, ..., A_{it-1}, B_{it-1}, F
@@ -762,6 +757,7 @@ TM_HD SJob bwd_level_job(const ChainArgs& a, int lvl, int jn) {
       }
       SJob g = product(op(a.Xs, 1), op(dP, 1), G, 1.f);
       g.e1 = dZa; g.e1s = 1.f;
+      if (k == 0 && a.X) { g.dotx = a.X; g.dot_part = a.part; }   // G = G0: the c gradient's dot
       return g;
   }
 }
@@ -990,7 +986,7 @@ int pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* sa
 
 // workspace: G, dT5, dZa, dP, dT3 (split) + dX (fp32) + partial dots
 extern "C" long long tm_pinv_bwd_split_workspace_floats(int nbh) {
-  return 6LL * nbh * MAT + nbh * 16LL + 64;
+  return 6LL * nbh * MAT + nbh * 16LL * 8 + 64;
 }
 
 // dZ: the gradient w.r.t. Z_iters as split planes, placed by the caller at the start of `work`
@@ -1007,12 +1003,13 @@ extern "C" int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int it
   bf16* G = (bf16*)work;
   float* dXc = work + 5 * mat;
   float* part = work + 6 * mat;
-  const ChainArgs c{(const bf16*)Xs, (float*)saved, work, nbh, iters};
+  ChainArgs c{(const bf16*)Xs, (float*)saved, work, nbh, iters};
+  c.X = X;      // the last level writes G0 and the c gradient's per-wave dots sum G0 o X^T
+  c.part = part;
   if (int rc = run_levels(c, 1, plane, maxima, F.team_ctr(nbh, 1), st)) return rc;
-  // Z_0 = X^T / c: the c gradient's partial sums, then the transpose term, the max-tie terms and the softmax
-  pinv_c_dot_kernel<<<dim3(nbh, 16), 256, 0, st>>>(G, plane, X, part);
-  TM_CHECK_LAUNCH();
-  pinv_apply_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, F.sums(), maxima, G, plane, part, nbh, dXc, softmax, out);
+  // Z_0 = X^T / c: the transpose term, the max-tie terms and the softmax
+  pinv_apply_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, F.sums(), maxima, G, plane, part, nbh * 16 * 8, nbh, dXc,
+                                                        softmax, out);
   TM_CHECK_LAUNCH();
   return 0;
 }
