@@ -284,7 +284,7 @@ TM_DEV void abssums(const SLaunch& L, int head, int which, float* red) {
 // TEAM: the tile runs inside the persistent chain kernel (pinv_team_kernel): every operand it
 // reads was written by another workgroup of the same XCD in this launch, so the LDS-DMA reads
 // bypass the CU's L1 (sc1, served by the XCD's L2) and so do the epilogue operand loads (nt).
-template <bool TEAM, int TEAM_POL = 16>
+template <bool TEAM, int TEAM_POL = 16, bool DOT = false>
 TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* maxima, int head, int tile,
                        char* smem, unsigned long long* stamp_out, int dbg_) {
   constexpr int DMA_POL = TEAM ? TEAM_POL : 0;   // cache policy of the LDS-DMA: sc1 in the team kernel
@@ -322,9 +322,10 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
   const bool epi = tid < 512;  // the 512 threads that each own one 8-element piece of the 64x64 tile
   if (e1p && epi) eload(e1p, e1f, e1raw);
   if (e2p && epi) eload(e2p, e2f, e2raw);
-  // the transposed dotx piece of this thread's 8 outputs: dotx[col + e][row]
+  // the transposed dotx piece of this thread's 8 outputs: dotx[col + e][row] (DOT: a separate
+  // instantiation for the one launch that carries it, so the other levels keep their registers)
   float dxv[8];
-  if (J.dotx && epi) {
+  if (DOT && J.dotx && epi) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) dxv[e] = J.dotx[hoff + (size_t)(n0 + lc + e) * NL + m0 + lr];
   }
@@ -456,7 +457,7 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
       for (int e = 0; e < 8; ++e) w[e] = c3e * e1v[e];
       store_split8(J.c3, plane, eoff, w);
     }
-    if (J.dotx) {
+    if (DOT && J.dotx) {
       float d = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) d = fmaf(v[e], dxv[e], d);
@@ -479,7 +480,7 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
 // blockIdx.y is the job.
 // AUX: the launch carries the A3 combine row (only the forward's last level; a separate
 // instantiation, so the other levels' code is not touched by the combine's registers)
-template <bool AUX>
+template <bool AUX, bool DOT = false>
 __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (AUX && blockIdx.y == (unsigned)L.njobs) {
@@ -506,7 +507,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   const int dbg_ = L.dbg;
   if (SPLIT_DBG == 5) return;
   unsigned long long* so = L.stamps ? L.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 * 8 : nullptr;
-  stage_tile<false>(J, nbh, L.plane, L.maxima, head, tile, smem, so, dbg_);
+  stage_tile<false, 16, DOT>(J, nbh, L.plane, L.maxima, head, tile, smem, so, dbg_);
 }
 
 // ---------------------------------------------------------------------------
@@ -851,7 +852,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_team_kernel(TeamArgs T) {
     const unsigned long long t_ready = T.stamps ? rstamp() : 0;
     if (T.stamps) so = T.stamps + (size_t)t_global_base(x, t) * 40;
 #endif
-    stage_tile<true, POL>(J, nbh, T.plane, T.maxima, head, tile, smem, so, 0);
+    stage_tile<true, POL, true>(J, nbh, T.plane, T.maxima, head, tile, smem, so, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tile stores have reached the L2
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -892,6 +893,9 @@ struct Launcher {
       grid.y += 1;
       tm_allow_smem(pinv_stage_kernel<true>, STAGE_LDS + EPI_LDS);
       pinv_stage_kernel<true><<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
+    } else if (L.j[L.njobs - 1].dotx) {   // the backward's last level: the c-gradient dot in its epilogue
+      tm_allow_smem(pinv_stage_kernel<false, true>, STAGE_LDS + EPI_LDS);
+      pinv_stage_kernel<false, true><<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
     } else {
       tm_allow_smem(pinv_stage_kernel<false>, STAGE_LDS + EPI_LDS);
       pinv_stage_kernel<false><<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
