@@ -78,11 +78,13 @@ struct SJob {
   float* cf;                                // optional fp32 copy of v
   bf16* c2; float c2_alpha, c2_diag, c2_e1; // optional split: c2_alpha*s + c2_diag*I + c2_e1*E1'
   bf16* c3; float c3_e1; int pad1;          // optional split: c3_e1 * E1'
-  // optional: per-wave partials of sum_ij v[i][j] * dotx[j][i] (dotx fp32, head-major like the
-  // output) at dot_part[((head * 16 + tile) * 8 + wave)] -- the c gradient's dot of the backward's
-  // last level, without a separate launch
-  const float* dotx; float* dot_part;
 };
+// The DOT stage-kernel instantiation (the backward's last level only) reads its job's e2 as
+// `dotx` (fp32, head-major like the output; that job has no E2 addend) and cf as `dot_part`: per-wave
+// partials of sum_ij v[i][j] dotx[j][i] at dot_part[(head * 16 + tile) * 8 + wave] -- the c
+// gradient's dot without a separate launch, and without growing every launch's kernel arguments.
+TM_DEV const float* job_dotx(const SJob& J) { return (const float*)J.e2; }
+TM_DEV float* job_dot_part(const SJob& J) { return J.cf; }
 
 struct SLaunch {
   SJob j[MAXJ];
@@ -286,7 +288,7 @@ TM_DEV void abssums(const SLaunch& L, int head, int which, float* red) {
 // bypass the CU's L1 (sc1, served by the XCD's L2) and so do the epilogue operand loads (nt).
 template <bool TEAM, int TEAM_POL = 16, bool DOT = false>
 TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* maxima, int head, int tile,
-                       char* smem, unsigned long long* stamp_out, int dbg_) {
+                       char* smem, unsigned long long* stamp_out, int dbg_, bool dj = false) {
   constexpr int DMA_POL = TEAM ? TEAM_POL : 0;   // cache policy of the LDS-DMA: sc1 in the team kernel
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -321,13 +323,15 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
   };
   const bool epi = tid < 512;  // the 512 threads that each own one 8-element piece of the 64x64 tile
   if (e1p && epi) eload(e1p, e1f, e1raw);
-  if (e2p && epi) eload(e2p, e2f, e2raw);
+  const bool dotj = DOT && dj;   // this job carries the c-gradient dot in e2 / cf (job_dotx)
+  if (!dotj && e2p && epi) eload(e2p, e2f, e2raw);
   // the transposed dotx piece of this thread's 8 outputs: dotx[col + e][row] (DOT: a separate
   // instantiation for the one launch that carries it, so the other levels keep their registers)
   float dxv[8];
-  if (DOT && J.dotx && epi) {
+  if (dotj && epi) {
+    const float* dotx = job_dotx(J);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dxv[e] = J.dotx[hoff + (size_t)(n0 + lc + e) * NL + m0 + lr];
+    for (int e = 0; e < 8; ++e) dxv[e] = dotx[hoff + (size_t)(n0 + lc + e) * NL + m0 + lr];
   }
   // per-head maxima for 1/c: one raw vector load per lane now, reduced in the epilogue
   const bool need_c = J.alpha_cpow || J.e1_cpow;
@@ -436,12 +440,12 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
 #pragma unroll
       for (int e = 0; e < 8; ++e) e1v[e] *= e1m;
     }
-    if (e2p) edecode(e2raw, e2f, e2v);
+    if (!dotj && e2p) edecode(e2raw, e2f, e2v);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = s[e] + e1s * e1v[e] + e2s * e2v[e];
     if (dg) v[row - col] += diag;
     if (J.c_f32) store_f8((float*)J.c, eoff, v); else store_split8((bf16*)J.c, plane, eoff, v);
-    if (J.cf) store_f8(J.cf, eoff, v);
+    if (!dotj && J.cf) store_f8(J.cf, eoff, v);
     if (J.c2) {
       float w[8];
       const float c2a = J.c2_alpha, c2e = J.c2_e1;
@@ -457,12 +461,12 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
       for (int e = 0; e < 8; ++e) w[e] = c3e * e1v[e];
       store_split8(J.c3, plane, eoff, w);
     }
-    if (DOT && J.dotx) {
+    if (dotj) {
       float d = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) d = fmaf(v[e], dxv[e], d);
       d = wave_sum(d);
-      if (lane == 0) J.dot_part[((size_t)head * 16 + tile) * 8 + wv] = d;
+      if (lane == 0) job_dot_part(J)[((size_t)head * 16 + tile) * 8 + wv] = d;
     }
   }
   if (st_on && wv < 4) {
@@ -507,7 +511,8 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
   const int dbg_ = L.dbg;
   if (SPLIT_DBG == 5) return;
   unsigned long long* so = L.stamps ? L.stamps + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 * 8 : nullptr;
-  stage_tile<false, 16, DOT>(J, nbh, L.plane, L.maxima, head, tile, smem, so, dbg_);
+  stage_tile<false, 16, DOT>(J, nbh, L.plane, L.maxima, head, tile, smem, so, dbg_,
+                             DOT && (int)blockIdx.y == L.njobs - 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -758,7 +763,7 @@ TM_HD SJob bwd_level_job(const ChainArgs& a, int lvl, int jn) {
       }
       SJob g = product(op(a.Xs, 1), op(dP, 1), G, 1.f);
       g.e1 = dZa; g.e1s = 1.f;
-      if (k == 0 && a.X) { g.dotx = a.X; g.dot_part = a.part; }   // G = G0: the c gradient's dot
+      if (k == 0 && a.X) { g.e2 = a.X; g.cf = a.part; }   // G = G0: the c gradient's dot (DOT launch)
       return g;
   }
 }
@@ -852,7 +857,8 @@ __global__ __launch_bounds__(NTHREADS) void pinv_team_kernel(TeamArgs T) {
     const unsigned long long t_ready = T.stamps ? rstamp() : 0;
     if (T.stamps) so = T.stamps + (size_t)t_global_base(x, t) * 40;
 #endif
-    stage_tile<true, POL, true>(J, nbh, T.plane, T.maxima, head, tile, smem, so, 0);
+    stage_tile<true, POL, true>(J, nbh, T.plane, T.maxima, head, tile, smem, so, 0,
+                                T.dir == 1 && lev == nlev - 1 && jn == 1 && T.c.X != nullptr);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tile stores have reached the L2
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -886,6 +892,7 @@ struct Launcher {
     L.stamps = g_split_stamps;
 #endif
   }
+  bool dot = false;   // the last job's e2 / cf carry the c-gradient dot (job_dotx / job_dot_part)
   void add(const SJob& j) { L.j[L.njobs++] = j; }
   int go(hipStream_t st) {
     dim3 grid(16 * L.nbh, L.njobs);
@@ -893,7 +900,7 @@ struct Launcher {
       grid.y += 1;
       tm_allow_smem(pinv_stage_kernel<true>, STAGE_LDS + EPI_LDS);
       pinv_stage_kernel<true><<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
-    } else if (L.j[L.njobs - 1].dotx) {   // the backward's last level: the c-gradient dot in its epilogue
+    } else if (dot) {   // the backward's last level: the c-gradient dot in its epilogue
       tm_allow_smem(pinv_stage_kernel<false, true>, STAGE_LDS + EPI_LDS);
       pinv_stage_kernel<false, true><<<grid, NTHREADS, STAGE_LDS + EPI_LDS, st>>>(L);
     } else {
@@ -929,6 +936,7 @@ int run_levels(const ChainArgs& c, int dir, long long plane, const float* maxima
     Launcher l(c.nbh, plane, maxima);
     const int nj = dir == 0 ? fwd_level_njobs(c.iters, lvl) : bwd_level_njobs(c.iters, lvl);
     for (int j = 0; j < nj; ++j) l.add(dir == 0 ? fwd_level_job(c, lvl, j) : bwd_level_job(c, lvl, j));
+    l.dot = dir == 1 && lvl == nlev - 1 && c.X != nullptr;
     if (a3 && dir == 0 && lvl == nlev - 1) l.L.a3 = *a3;   // the forward's last level: one 128-tile job
     if (int rc = l.go(st)) return rc;
   }
