@@ -80,8 +80,8 @@ struct SJob {
   bf16* c3; float c3_e1; int pad1;          // optional split: c3_e1 * E1'
 };
 // The DOT stage-kernel instantiation (the backward's last level only) reads its job's e2 as
-// `dotx` (fp32, head-major like the output; that job has no E2 addend) and cf as `dot_part`: per-wave
-// partials of sum_ij v[i][j] dotx[j][i] at dot_part[(head * 16 + tile) * 8 + wave] -- the c
+// `dotx` (fp32, head-major like the output; that job has no E2 addend) and cf as `dot_part`: the
+// workgroup's partial of sum_ij v[i][j] dotx[j][i] at dot_part[head * 16 + tile] -- the c
 // gradient's dot without a separate launch, and without growing every launch's kernel arguments.
 TM_DEV const float* job_dotx(const SJob& J) { return (const float*)J.e2; }
 TM_DEV float* job_dot_part(const SJob& J) { return J.cf; }
@@ -409,7 +409,11 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
     for (int r = 0; r < 16; ++r) ep[(wm * 32 + acc_row(r, h)) * EROW + wn * 32 + cc] = acc[r];
   }
   __syncthreads();  // the tile is in `ep`; every wave (producers too) takes one 8-element row piece
-  if (SPLIT_DBG == 3 || !epi) return;
+  __shared__ float dred[8];   // DOT: the 8 epilogue waves' partial dots
+  if (SPLIT_DBG == 3 || !epi) {
+    if (dotj && SPLIT_DBG != 3) __syncthreads();   // the one barrier the epilogue waves' dot sum takes
+    return;
+  }
   const float diag = J.diag, e1s = J.e1s, e2s = J.e2s;
   float ic = 1.f;
   if (need_c) ic = nbh <= 64 ? 1.f / (wave_max(mcv) * wave_max(mrv)) : inv_c(maxima, nbh);
@@ -466,7 +470,11 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
 #pragma unroll
       for (int e = 0; e < 8; ++e) d = fmaf(v[e], dxv[e], d);
       d = wave_sum(d);
-      if (lane == 0) job_dot_part(J)[((size_t)head * 16 + tile) * 8 + wv] = d;
+      if (lane == 0) dred[wv] = d;
+      __syncthreads();   // every wave of the workgroup (the non-epilogue ones at their return)
+      if (tid == 0)
+        job_dot_part(J)[(size_t)head * 16 + tile] =
+            ((dred[0] + dred[1]) + (dred[2] + dred[3])) + ((dred[4] + dred[5]) + (dred[6] + dred[7]));
     }
   }
   if (st_on && wv < 4) {
@@ -998,7 +1006,7 @@ int pinv_fwd_split(const float* X, const void* Xs, int nbh, int iters, float* sa
 
 // workspace: G, dT5, dZa, dP, dT3 (split) + dX (fp32) + partial dots
 extern "C" long long tm_pinv_bwd_split_workspace_floats(int nbh) {
-  return 6LL * nbh * MAT + nbh * 16LL * 8 + 64;
+  return 6LL * nbh * MAT + nbh * 16LL + 64;
 }
 
 // dZ: the gradient w.r.t. Z_iters as split planes, placed by the caller at the start of `work`
@@ -1020,7 +1028,7 @@ extern "C" int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int it
   c.part = part;
   if (int rc = run_levels(c, 1, plane, maxima, F.team_ctr(nbh, 1), st)) return rc;
   // Z_0 = X^T / c: the transpose term, the max-tie terms and the softmax
-  pinv_apply_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, F.sums(), maxima, G, plane, part, nbh * 16 * 8, nbh, dXc,
+  pinv_apply_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, F.sums(), maxima, G, plane, part, nbh * 16, nbh, dXc,
                                                         softmax, out);
   TM_CHECK_LAUNCH();
   return 0;
