@@ -152,7 +152,8 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
         ("a3_fwd", 2): ("a3_fwd_v2_kernel<0, 4> (+ A2 rows; combine inside pinv F launch)", a3f),
         ("a1_fwd", 1): ("a1_fwd_bf16_kernel", a1f),
         ("ppeg_fwd", 0): ("ppeg_stencil_kernel<false>", ppf),
-        ("ppeg_bwd", 0): ("ppeg_stencil_kernel<true> + ppeg_wgrad_kernel + ppeg_wgrad_reduce_kernel", ppb),
+        # (the weight-gradient slab sums ride in the deferred multi_reduce flush that follows)
+        ("ppeg_bwd", 0): ("ppeg_stencil_kernel<true> + ppeg_wgrad_kernel", ppb),
         ("conv_bwd", 1): ("conv_bwd_mfma_kernel", cvb),
         ("a3_bwd", 2): ("attn_bwd_bf16_kernel<0, 9> (fused dk / dv epilogue)", a3b_l2),
         ("a3_bwd", 1): ("attn_bwd_bf16_kernel<0, 9> (fused dk / dv epilogue)", a3b_l1),

@@ -255,12 +255,12 @@ int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const f
 long long tm_ppeg_bwd_workspace(int B, int G, int D);
 /* dout (nullable): also writes the padded to_out-dropout gradient of the TransLayer below from dx
  * (as tm_dropout_bwd_pad with the same dtype / n_pad / pad / p / seed / seed_ptr).  The weight
- * gradients are summed from the workspace straight into dw7..db3 (=); dwsum is not written (kept in
- * the signature for ABI stability, may be null) */
+ * gradients (=) are summed from the workspace's slabs by tm_splitk_reduce: deferred into rq when
+ * it is non-null (final after tm_reduce_flush), else summed before return */
 int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const float* wfold, float* dx,
-                float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
-                float* db3, int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
-                const uint64_t* seed_ptr, void* stream);
+                float* work, float* dw7, float* db7, float* dw5, float* db5, float* dw3, float* db3,
+                int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
+                const uint64_t* seed_ptr, tm_reduce_queue* rq, void* stream);
 
 /* ---- AttMIL gated attention pooling (attmil.hip) -- code/models/AttMIL.py:88-110 ----
  * Z [N, 2D] = H [Wv;Wu]^T + [bv;bu] (caller's GEMM), H [N, L], w [D] / b [1] = attention_weights,

@@ -114,7 +114,7 @@ _SIGS = {
     "tm_ppeg_fold": (I, [P, P, P, P, P, P, I, P, P, P]),
     "tm_ppeg_fwd": (I, [P, I, I, I, P, P, P, P]),
     "tm_ppeg_bwd_workspace": (L, [I, I, I]),
-    "tm_ppeg_bwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, P, I, P, I, I, Fl, U64, P, P]),
+    "tm_ppeg_bwd": (I, [P, P, I, I, I, P, P, P, P, P, P, P, P, P, I, P, I, I, Fl, U64, P, P, P]),
     "tm_gather_rows": (I, [I, P, I, P, P, P, P, I, P, P]),
     "tm_attmil_fwd_workspace": (L, [I, I]),
     "tm_attmil_fwd": (I, [P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P]),

@@ -20,6 +20,8 @@ __global__ void cast_many_kernel(tm_cast_table tab) {
   for (int e = 0; e < 4 && j + e < n; ++e) dst[j + e] = from_f<T>(src[j + e]);
 }
 
+constexpr int CAST_PIECES = 4;
+
 // The per-step preparation of the fused forward as ONE launch: blocks [0, cast_blocks) convert
 // the cast table (GEMM weights + the bag to T), the next ceil(49 D/256) blocks fold PPEG's
 // 7x7 + 5x5 + 3x3 + identity into one 7x7 kernel (code/models/TransMIL.py:72), and the last
@@ -35,30 +37,45 @@ __global__ void __launch_bounds__(256) step_prepare_kernel(tm_cast_table tab, lo
                                                            const float* __restrict__ cls, float* __restrict__ H,
                                                            int B, int S) {
   if (blockIdx.x < cast_blocks) {
-    // 4 elements per thread (offsets are multiples of 4, so a piece never straddles tensors); the
-    // tensor is found wave-uniformly -- scalar loads of the table, a wave on a tensor boundary
-    // walks the few tensors it touches -- and the piece moves as one 16-B load / one 4-T store
+    // CAST_PIECES 4-element pieces per lane (block b, piece k: elements from (b CAST_PIECES + k)
+    // 1024, a wave 256 of them), all loads issued before any store: 16 KB in flight per block.  The
+    // tensor is found wave-uniformly (scalar loads of the table); a wave span inside one aligned
+    // tensor moves as one 16-B load / one 4-T store per lane, the rare span across a tensor
+    // boundary or the table's end goes piece by piece
     const long long total = tab.offset[tab.count];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long wbase = ((long long)blockIdx.x * blockDim.x + wave * 64) * 4;
-    if (wbase >= total) return;
-    const long long i4 = wbase + 4 * (threadIdx.x & 63);
-    int t0 = 0;
-    while (t0 < tab.count - 1 && wbase >= tab.offset[t0 + 1]) ++t0;
-    for (int t = t0; t < tab.count && tab.offset[t] < wbase + 256; ++t) {  // wave-uniform t
-      if (i4 < tab.offset[t] || i4 >= tab.offset[t + 1]) continue;
-      const long long j = i4 - tab.offset[t];
-      const float* src = tab.src[t] + j;
-      T* dst = (T*)tab.dst[t] + j;
-      if (((uintptr_t)src % 16) == 0 && ((uintptr_t)dst % (4 * sizeof(T))) == 0) {
-        const f32x4 v = *(const f32x4*)src;
-        vec4<T> o;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    f32x4 v[CAST_PIECES];
+    T* dp[CAST_PIECES];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = from_f<T>(v[e]);
-        *(vec4<T>*)dst = o;
-      } else {
+    for (int k = 0; k < CAST_PIECES; ++k) {
+      dp[k] = nullptr;
+      const long long wbase = ((long long)blockIdx.x * CAST_PIECES + k) * 1024 + wave * 256;
+      if (wbase >= total) continue;
+      const long long i4 = wbase + 4 * lane;
+      int t0 = 0;
+      while (t0 < tab.count - 1 && wbase >= tab.offset[t0 + 1]) ++t0;
+      const bool aligned = ((uintptr_t)tab.src[t0] % 16) == 0 && ((uintptr_t)tab.dst[t0] % (4 * sizeof(T))) == 0;
+      if (aligned && tab.offset[t0 + 1] >= wbase + 256) {
+        const long long j = i4 - tab.offset[t0];
+        v[k] = *(const f32x4*)(tab.src[t0] + j);
+        dp[k] = (T*)tab.dst[t0] + j;
+        continue;
+      }
+      for (int t = t0; t < tab.count && tab.offset[t] < wbase + 256; ++t) {  // wave-uniform t
+        if (i4 < tab.offset[t] || i4 >= tab.offset[t + 1]) continue;
+        const long long j = i4 - tab.offset[t];
+        const float* src = tab.src[t] + j;
+        T* dst = (T*)tab.dst[t] + j;
         for (int e = 0; e < 4; ++e) dst[e] = from_f<T>(src[e]);
       }
+    }
+#pragma unroll
+    for (int k = 0; k < CAST_PIECES; ++k) {
+      if (!dp[k]) continue;
+      vec4<T> o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = from_f<T>(v[k][e]);
+      *(vec4<T>*)dp[k] = o;
     }
     return;
   }
@@ -342,7 +359,7 @@ extern "C" int tm_step_prepare(int dtype, const tm_cast_table* table, const floa
                "step_prepare: offsets must be a prefix sum of multiples of 4");
     off = table->offset[i + 1];
   }
-  const long long cast_blocks = ((off + 3) / 4 + 255) / 256;
+  const long long cast_blocks = (off + 1024 * CAST_PIECES - 1) / (1024 * CAST_PIECES);
   const long long blocks = cast_blocks + (w7 ? (49LL * D + 255) / 256 : 0) + 1;
   TM_DTYPE_DISPATCH(dtype, (step_prepare_kernel<T><<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(
                                *table, cast_blocks, w7, b7, w5, b5, w3, b3, D, wfold, bfold, counter, seed_out,

@@ -184,7 +184,8 @@ __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restri
   }
 }
 
-// grid (nchunk * ntr * ceil(ntc / WT), B), block 256; part: [B * ntr * ceil(ntc / WT)][D][50]
+// grid (nchunk * ntr * ceil(ntc / WT), B), block 256; part: Z = B * ntr * ceil(ntc / WT) slabs in four
+// regions [Z][D][49], [Z][D][25], [Z][D][9], [Z][D] (see the store loop)
 __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy_,
                                                         int S, int G, int D, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -251,44 +252,29 @@ __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict
     for (int dx = 0; dx < KS; ++dx) *(f32x4*)(o + dx * 4) = accw[dx];
   }
   __syncthreads();
-  float* dst = part + ((size_t)b * (gridDim.x / nchunk) + grp) * D * (NT + 1) + (size_t)chunk * CW * (NT + 1);
+  // four slab regions, each [Z][count] with Z = B * groups slabs (the deferred reduce sums a
+  // region's slabs straight into one gradient): the folded 7x7 taps (= dw7), their 5x5 and 3x3
+  // centres (the fold is a sum, so these are dw5 / dw3), and the bias sums (db7 = db5 = db3)
+  const size_t Z = (size_t)gridDim.y * (gridDim.x / nchunk), z = (size_t)b * (gridDim.x / nchunk) + grp;
+  float* p7 = part + z * D * NT;
+  float* p5 = part + Z * D * NT + z * D * 25;
+  float* p3 = part + Z * D * (NT + 25) + z * D * 9;
+  float* pb = part + Z * D * (NT + 34) + z * D;
   for (int e = tid; e < CW * (NT + 1); e += 256) {
     const int cl = e / (NT + 1), tp = e - cl * (NT + 1);          // channel of the chunk, tap (49 = bias)
-    const int q = cl >> 2, ce = cl & 3;
+    const int q = cl >> 2, ce = cl & 3, ch = chunk * CW + cl;
     const int trow = tp == NT ? 7 : tp / KS, dx = tp == NT ? 0 : tp - (tp / KS) * KS;
     float s = 0.f;
 #pragma unroll
     for (int pr = 0; pr < 4; ++pr) s += red[(((size_t)pr * 8 + trow) * NQ + q) * 28 + dx * 4 + ce];
-    dst[e] = s;
+    if (tp == NT) {
+      pb[ch] = s;
+      continue;
+    }
+    p7[(size_t)ch * NT + tp] = s;
+    if (trow >= 1 && trow <= 5 && dx >= 1 && dx <= 5) p5[(size_t)ch * 25 + (trow - 1) * 5 + dx - 1] = s;
+    if (trow >= 2 && trow <= 4 && dx >= 2 && dx <= 4) p3[(size_t)ch * 9 + (trow - 2) * 3 + dx - 2] = s;
   }
-}
-
-// unfold folded gradients: dw7 = dwf, dw5 = centre 5x5, dw3 = centre 3x3, db* = db
-// the weight-gradient partial slabs summed (in slab order, as tm_splitk_reduce) straight into the
-// unfolded gradients: thread i = (ch, t) of the [D][50] partial layout, t < 49 a tap of the folded
-// 7x7 kernel (its 5x5 / 3x3 centre taps also feed dw5 / dw3: the fold is a sum), t = 49 the bias
-__global__ __launch_bounds__(256) void ppeg_wgrad_reduce_kernel(const float* __restrict__ part, int slabs, int D,
-                                                                float* __restrict__ dw7, float* __restrict__ db7,
-                                                                float* __restrict__ dw5, float* __restrict__ db5,
-                                                                float* __restrict__ dw3, float* __restrict__ db3) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t count = (size_t)D * (NT + 1);
-  if (i >= (int)count) return;
-  constexpr int U = 12;
-  float s = 0.f;
-  for (int z0 = 0; z0 < slabs; z0 += U) {
-    float v[U];
-#pragma unroll
-    for (int k = 0; k < U; ++k) v[k] = part[(size_t)min(z0 + k, slabs - 1) * count + i];
-#pragma unroll
-    for (int k = 0; k < U; ++k) s += z0 + k < slabs ? v[k] : 0.f;
-  }
-  const int ch = i / (NT + 1), t = i - ch * (NT + 1);
-  if (t == NT) { db7[ch] = s; db5[ch] = s; db3[ch] = s; return; }
-  dw7[(size_t)ch * NT + t] = s;
-  const int dy = t / KS, dx = t - dy * KS;
-  if (dy >= 1 && dy <= 5 && dx >= 1 && dx <= 5) dw5[(size_t)ch * 25 + (dy - 1) * 5 + dx - 1] = s;
-  if (dy >= 2 && dy <= 4 && dx >= 2 && dx <= 4) dw3[(size_t)ch * 9 + (dy - 2) * 3 + dx - 2] = s;
 }
 
 }  // namespace
@@ -319,14 +305,14 @@ extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfo
 }
 
 extern "C" long long tm_ppeg_bwd_workspace(int B, int G, int D) {
-  return (long long)B * wgrad_groups(G) * D * (NT + 1) * (long long)sizeof(float);
+  return (long long)B * wgrad_groups(G) * D * (NT + 25 + 9 + 1) * (long long)sizeof(float);
 }
 
 // dy: [B,S,D] upstream gradient; x: PPEG input.  dx written (=); weight grads written.
 extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D, const float* wfold, float* dx,
-                           float* work, float* dwsum, float* dw7, float* db7, float* dw5, float* db5, float* dw3,
-                           float* db3, int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
-                           const uint64_t* seed_ptr, void* stream) {
+                           float* work, float* dw7, float* db7, float* dw5, float* db5, float* dw3, float* db3,
+                           int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
+                           const uint64_t* seed_ptr, tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(x && dy && dx && dx != dy && D % CW == 0 && G > 0 && B > 0, "ppeg_bwd: bad args");
   TM_REQUIRE(!dout || ((dtype == TM_BF16 || dtype == TM_F32) && n_pad >= pad + 1 + G * G && pad >= 0),
              "ppeg_bwd: bad dropout-pad output");
@@ -338,9 +324,17 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
   TM_CHECK_LAUNCH();
   ppeg_wgrad_kernel<<<dim3(wgrad_groups(G) * (D / CW), B), 256, WG_LDS, st>>>(x, dy, S, G, D, work);
   TM_CHECK_LAUNCH();
-  (void)dwsum;
-  ppeg_wgrad_reduce_kernel<<<(D * (NT + 1) + 255) / 256, 256, 0, st>>>(work, B * wgrad_groups(G), D, dw7, db7, dw5,
-                                                                     db5, dw3, db3);
-  TM_CHECK_LAUNCH();
-  return 0;
+  // the weight-gradient slabs summed in slab order into the unfolded gradients (deferred into the
+  // caller's queue when it has one: the flush that finalises the PPEG gradients is one launch)
+  const int Z = B * wgrad_groups(G);
+  const float* p5 = work + (size_t)Z * D * NT;
+  const float* p3 = p5 + (size_t)Z * D * 25;
+  const float* pb = p3 + (size_t)Z * D * 9;
+  int rc = tm_splitk_reduce(work, dw7, Z, (long long)D * NT, 1.0f, 0, rq, stream);
+  if (!rc) rc = tm_splitk_reduce(p5, dw5, Z, (long long)D * 25, 1.0f, 0, rq, stream);
+  if (!rc) rc = tm_splitk_reduce(p3, dw3, Z, (long long)D * 9, 1.0f, 0, rq, stream);
+  if (!rc) rc = tm_splitk_reduce(pb, db7, Z, D, 1.0f, 0, rq, stream);
+  if (!rc) rc = tm_splitk_reduce(pb, db5, Z, D, 1.0f, 0, rq, stream);
+  if (!rc) rc = tm_splitk_reduce(pb, db3, Z, D, 1.0f, 0, rq, stream);
+  return rc;
 }

@@ -843,17 +843,16 @@ class TransMILEngine:
             if li == 2:
                 dH1 = pool(B * S * D).view(B * S, D)
                 work = pool(_lib.query("tm_ppeg_bwd_workspace", B, geo.G, D) // 4)
-                dwsum = pool(D * 50)
                 # the stencil also writes layer 1's padded to_out-dropout gradient (its first step)
                 s1 = ctx["s1"]
                 dout1 = pool(B * geo.n * D, self.tdtype).view(B, geo.n, D)
-                with probe("ppeg_bwd"):
+                with probe("ppeg_bwd"), defer_reductions():
                     _lib.call("tm_ppeg_bwd", _p(ctx["H1"]), _p(dH), B, geo.G, D, _p(prm["wfold"]), _p(dH1),
-                              _p(work), _p(dwsum), _p(g["pos_layer.proj.weight"]), _p(g["pos_layer.proj.bias"]),
+                              _p(work), _p(g["pos_layer.proj.weight"]), _p(g["pos_layer.proj.bias"]),
                               _p(g["pos_layer.proj1.weight"]), _p(g["pos_layer.proj1.bias"]),
                               _p(g["pos_layer.proj2.weight"]), _p(g["pos_layer.proj2.bias"]), self.dt_code,
                               _p(dout1), geo.n, geo.pad, C.c_float(s1["drop_p"]), C.c_uint64(s1["seed"]),
-                              _p(s1["seed_dev"]), st)
+                              _p(s1["seed_dev"]), _rq(), st)
                 dH = dH1
                 flush_reductions()     # head, norm, layer2 and PPEG parameter gradients final
                 if ready is not None:

@@ -77,13 +77,12 @@ class _PPEGFn(torch.autograd.Function):
         G = ctx.G
         dx = torch.empty_like(x)
         work = torch.empty(_lib.query("tm_ppeg_bwd_workspace", B, G, D) // 4, device=x.device)
-        dwsum = torch.empty(D * 50, device=x.device)
         s7, s5, s3 = ctx.shapes
         dw7, dw5, dw3 = (torch.empty(s, device=x.device) for s in (s7, s5, s3))
         db7, db5, db3 = (torch.empty(D, device=x.device) for _ in range(3))
-        _lib.call("tm_ppeg_bwd", _p(x), _p(dy.float().contiguous()), B, G, D, _p(wf), _p(dx), _p(work), _p(dwsum),
-                  _p(dw7), _p(db7), _p(dw5), _p(db5), _p(dw3), _p(db3), F32, None, 0, 0, C.c_float(0.0),
-                  C.c_uint64(0), None, _stream())
+        _lib.call("tm_ppeg_bwd", _p(x), _p(dy.float().contiguous()), B, G, D, _p(wf), _p(dx), _p(work), _p(dw7),
+                  _p(db7), _p(dw5), _p(db5), _p(dw3), _p(db3), F32, None, 0, 0, C.c_float(0.0), C.c_uint64(0),
+                  None, None, _stream())
         return dx, None, dw7, db7, dw5, db5, dw3, db3
 
 
