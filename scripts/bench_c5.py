@@ -43,7 +43,11 @@ def main():
     ap.add_argument("--chunk", type=int, default=512)
     ap.add_argument("--graph", action="store_true", help="capture the step in a hipGraph")
     ap.add_argument("--layout", default="nhwc", choices=["nhwc", "nchw"])
-    ap.add_argument("--benchmark", action="store_true", help="torch.backends.cudnn.benchmark (MIOpen find)")
+    # MIOpen find (torch.backends.cudnn.benchmark) picks the 3x3 / stem convolution kernels by timing
+    # them once per shape before the timed region: eval encoder 98.9 -> 89.1 ms per 4096 tiles
+    # (profiles/r04p_c5_find.jsonl); --no-benchmark keeps MIOpen's immediate-mode heuristics
+    ap.add_argument("--benchmark", action=argparse.BooleanOptionalAction, default=True,
+                    help="torch.backends.cudnn.benchmark (MIOpen find)")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = a.benchmark
     from transmil_deepgraft_amd.encoder import ImageBagModel, retccl_resnet50

@@ -74,20 +74,45 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restri
   }
 }
 
+// The fp64 combine of the partial sums: a workgroup owns CB = min(C, 64) channels, its 1024 / CB
+// thread groups each sum every G-th part (G = number of groups) in fp64 with 8 parts' loads in
+// flight, then group 0 adds the groups' sums in group order -- a fixed order, so deterministic.
+// (One thread per channel walking all ~2 K parts serially was ~0.75 ms per call: one dependent
+// load round trip per part on 1-8 workgroups.)
+constexpr int kFinalThreads = 1024;
 template <typename T>
-__global__ __launch_bounds__(256) void bn_stats_final_kernel(const T* __restrict__ x, long long rows, int C,
-                                                             int nparts, const float* __restrict__ part,
-                                                             const float* __restrict__ gamma,
-                                                             const float* __restrict__ beta, float* running_mean,
-                                                             float* running_var, float momentum, float eps,
-                                                             float* __restrict__ scale, float* __restrict__ shift) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(kFinalThreads) void bn_stats_final_kernel(const T* __restrict__ x, long long rows, int C,
+                                                                       int nparts, const float* __restrict__ part,
+                                                                       const float* __restrict__ gamma,
+                                                                       const float* __restrict__ beta,
+                                                                       float* running_mean, float* running_var,
+                                                                       float momentum, float eps,
+                                                                       float* __restrict__ scale,
+                                                                       float* __restrict__ shift) {
+  __shared__ double red[2][kFinalThreads];
+  const int CB = C < 64 ? C : 64, G = kFinalThreads / CB;
+  const int cl = threadIdx.x % CB, grp = threadIdx.x / CB, c = blockIdx.x * CB + cl;
   double S = 0.0, Q = 0.0;
-  for (int g = 0; g < nparts; ++g) {
-    S += (double)part[((size_t)g * 2 + 0) * C + c];
-    Q += (double)part[((size_t)g * 2 + 1) * C + c];
+  constexpr int U = 8;
+  for (int g0 = grp; g0 < nparts; g0 += U * G) {
+    float sv[U], qv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int g = min(g0 + u * G, nparts - 1);
+      sv[u] = part[((size_t)g * 2 + 0) * C + c];
+      qv[u] = part[((size_t)g * 2 + 1) * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (g0 + u * G < nparts) { S += (double)sv[u]; Q += (double)qv[u]; }
   }
+  red[0][threadIdx.x] = S;
+  red[1][threadIdx.x] = Q;
+  __syncthreads();
+  if (grp != 0) return;
+  S = 0.0;
+  Q = 0.0;
+  for (int g = 0; g < G; ++g) { S += red[0][g * CB + cl]; Q += red[1][g * CB + cl]; }
   const double n = (double)rows, md = S / n;
   double var = Q / n - md * md;
   var = var > 0.0 ? var : 0.0;
@@ -178,13 +203,13 @@ extern "C" int tm_bn_train_stats(int dtype, const void* const* xs, const long lo
     nparts += np;
   }
   if (dtype == TM_BF16)
-    bn_stats_final_kernel<bf16><<<(C + 255) / 256, 256, 0, st>>>((const bf16*)xs[0], total, C, nparts, workspace,
-                                                                  gamma, beta, running_mean, running_var, momentum,
-                                                                  eps, scale, shift);
+    bn_stats_final_kernel<bf16><<<(C + 63) / 64, kFinalThreads, 0, st>>>((const bf16*)xs[0], total, C, nparts,
+                                                                          workspace, gamma, beta, running_mean,
+                                                                          running_var, momentum, eps, scale, shift);
   else
-    bn_stats_final_kernel<float><<<(C + 255) / 256, 256, 0, st>>>((const float*)xs[0], total, C, nparts, workspace,
-                                                                   gamma, beta, running_mean, running_var, momentum,
-                                                                   eps, scale, shift);
+    bn_stats_final_kernel<float><<<(C + 63) / 64, kFinalThreads, 0, st>>>((const float*)xs[0], total, C, nparts,
+                                                                           workspace, gamma, beta, running_mean,
+                                                                           running_var, momentum, eps, scale, shift);
   TM_CHECK_LAUNCH();
   return 0;
 }
