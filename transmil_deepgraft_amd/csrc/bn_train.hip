@@ -20,19 +20,32 @@ namespace {
 constexpr int kStatParts = 2048;     // row blocks of the statistics pass (fixed: partial slab size)
 constexpr int kMaxPieces = 64;       // row pieces one statistics call combines
 
+// the row pieces of one statistics call: piece p owns partial slots [pbeg[p], pbeg[p + 1])
+struct BnPieces {
+  const void* x[kMaxPieces];
+  long long rows[kMaxPieces];
+  int pbeg[kMaxPieces + 1];
+  int n;
+};
+
+// ONE launch over every piece (workgroup b = partial slot b): all ~2 K workgroups of the call are
+// in flight together, where one launch per piece put one 256-thread workgroup on each CU
 template <typename T>
-__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restrict__ x, const T* __restrict__ x0,
-                                                               long long rows, int C, long long rows_per_part,
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(BnPieces pcs, int C, long long rows_per_part,
                                                                float* __restrict__ part) {
   __shared__ float red[2][256 * 8];
+  int p = 0;
+  while (p < pcs.n - 1 && (int)blockIdx.x >= pcs.pbeg[p + 1]) ++p;   // workgroup-uniform
+  const T* __restrict__ x = (const T*)pcs.x[p];
+  const long long rows = pcs.rows[p];
   const int tpr = C >> 3;                      // threads per row (8 channels each), divides 256
   const int rpi = 256 / tpr;                   // rows per iteration
   const int c8 = (threadIdx.x % tpr) * 8, r0 = threadIdx.x / tpr;
-  const vec8<T> shv = load8(x0 + c8);          // shift: row 0 of the first piece
+  const vec8<T> shv = load8((const T*)pcs.x[0] + c8);   // shift: row 0 of the first piece
   float sh[8], s[8], q[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { sh[e] = to_f(shv[e]); s[e] = 0.f; q[e] = 0.f; }
-  const long long beg = (long long)blockIdx.x * rows_per_part;
+  const long long beg = (long long)(blockIdx.x - pcs.pbeg[p]) * rows_per_part;
   const long long end = beg + rows_per_part < rows ? beg + rows_per_part : rows;
   long long r = beg + r0;
   for (; r + 3LL * rpi < end; r += 4LL * rpi) {          // four rows in flight per thread
@@ -185,23 +198,24 @@ extern "C" int tm_bn_train_stats(int dtype, const void* const* xs, const long lo
     TM_REQUIRE(xs[p] && rows[p] > 0 && ((uintptr_t)xs[p] % 16) == 0, "bn_train_stats: piece (16-B aligned, rows > 0)");
     total += rows[p];
   }
+  TM_REQUIRE(dtype == TM_BF16 || dtype == TM_F32, "bn_train_stats: dtype");
   const long long per = (total + kStatParts - 1) / kStatParts;
   hipStream_t st = (hipStream_t)stream;
+  BnPieces pcs{};
   int nparts = 0;
   for (int p = 0; p < npieces; ++p) {
-    const int np = (int)((rows[p] + per - 1) / per);
-    if (dtype == TM_BF16)
-      bn_stats_partial_kernel<bf16><<<np, 256, 0, st>>>((const bf16*)xs[p], (const bf16*)xs[0], rows[p], C, per,
-                                                        workspace + 2LL * nparts * C);
-    else if (dtype == TM_F32)
-      bn_stats_partial_kernel<float><<<np, 256, 0, st>>>((const float*)xs[p], (const float*)xs[0], rows[p], C, per,
-                                                         workspace + 2LL * nparts * C);
-    else {
-      tm_set_error("bn_train_stats: dtype");
-      return 1;
-    }
-    nparts += np;
+    pcs.x[p] = xs[p];
+    pcs.rows[p] = rows[p];
+    pcs.pbeg[p] = nparts;
+    nparts += (int)((rows[p] + per - 1) / per);
   }
+  pcs.pbeg[npieces] = nparts;
+  pcs.n = npieces;
+  if (dtype == TM_BF16)
+    bn_stats_partial_kernel<bf16><<<nparts, 256, 0, st>>>(pcs, C, per, workspace);
+  else
+    bn_stats_partial_kernel<float><<<nparts, 256, 0, st>>>(pcs, C, per, workspace);
+  TM_CHECK_LAUNCH();
   if (dtype == TM_BF16)
     bn_stats_final_kernel<bf16><<<(C + 63) / 64, kFinalThreads, 0, st>>>((const bf16*)xs[0], total, C, nparts,
                                                                           workspace, gamma, beta, running_mean,
