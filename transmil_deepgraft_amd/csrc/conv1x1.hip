@@ -15,6 +15,7 @@
 
 #include <hipblaslt/hipblaslt.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -30,11 +31,16 @@ struct Device {
   void* ws = nullptr;
 };
 
+constexpr int kCand = 8;   // heuristic candidates timed once per shape (outside stream capture)
+
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, cd = nullptr;
   hipblasLtMatmulAlgo_t algo{};
   size_t ws = 0;
+  hipblasLtMatmulHeuristicResult_t cand[kCand];
+  int ncand = 0;
+  bool tuned = false;
 };
 
 using Key = std::tuple<int, int, int, int, int, long long, int, int>;   // dev dtype relu bias res rows cin cout
@@ -94,18 +100,66 @@ int make_plan(Device& d, int dtype, int relu, int has_bias, long long rows, int 
   const uint64_t wsb = kWorkspace;
   hipblasStatus_t s = hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES,
                                                             &wsb, sizeof(wsb));
-  hipblasLtMatmulHeuristicResult_t r[1];
   int n = 0;
   if (s == HIPBLAS_STATUS_SUCCESS)
-    s = hipblasLtMatmulAlgoGetHeuristic(d.handle, p->desc, p->a, p->b, p->cd, p->cd, pref, 1, r, &n);
+    s = hipblasLtMatmulAlgoGetHeuristic(d.handle, p->desc, p->a, p->b, p->cd, p->cd, pref, kCand, p->cand, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   LT_CHECK(s);
   if (n < 1) {
     tm_set_error("conv1x1: hipBLASLt found no algorithm for this shape/epilogue");
     return 3;
   }
-  p->algo = r[0].algo;
-  p->ws = r[0].workspaceSize;
+  p->ncand = n;
+  p->algo = p->cand[0].algo;
+  p->ws = p->cand[0].workspaceSize;
+  p->tuned = n == 1;
+  return 0;
+}
+
+// the first call of a shape outside stream capture times every heuristic candidate (one warm-up +
+// three timed runs each, on the call's own operands: y is rewritten by the real call after) and
+// keeps the fastest -- the hipBLASLt analogue of MIOpen find.  TM_CONV1X1_TUNE=0 keeps the
+// heuristic's first choice.
+bool tuning_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("TM_CONV1X1_TUNE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int tune(Device& d, Plan& p, const void* w, const void* xp, const void* rp, void* yp, float beta, hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return 0;   // next call
+  p.tuned = true;
+  if (!tuning_enabled()) return 0;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return 0;
+  if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return 0; }
+  const float alpha = 1.f;
+  float best = 3.4e38f;
+  int bi = 0;
+  for (int i = 0; i < p.ncand; ++i) {
+    const hipblasLtMatmulHeuristicResult_t& c = p.cand[i];
+    if (c.state != HIPBLAS_STATUS_SUCCESS || c.workspaceSize > kWorkspace) continue;
+    if (hipblasLtMatmul(d.handle, p.desc, &alpha, w, p.a, xp, p.b, &beta, rp, p.cd, yp, p.cd, &c.algo, d.ws,
+                        c.workspaceSize, st) != HIPBLAS_STATUS_SUCCESS)
+      continue;
+    (void)hipEventRecord(e0, st);
+    for (int k = 0; k < 3; ++k)
+      hipblasLtMatmul(d.handle, p.desc, &alpha, w, p.a, xp, p.b, &beta, rp, p.cd, yp, p.cd, &c.algo, d.ws,
+                      c.workspaceSize, st);
+    (void)hipEventRecord(e1, st);
+    float ms = 0.f;
+    if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms < best) {
+      best = ms;
+      bi = i;
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  p.algo = p.cand[bi].algo;
+  p.ws = p.cand[bi].workspaceSize;
   return 0;
 }
 
@@ -148,6 +202,7 @@ extern "C" int tm_conv1x1(int dtype, const void* x, const void* w, const void* b
     const char* xp = (const char*)x + (size_t)r0 * cin * esz;
     char* yp = (char*)y + (size_t)r0 * cout * esz;
     const char* rp = residual ? (const char*)residual + (size_t)r0 * cout * esz : yp;
+    if (!p.tuned) tune(*d, p, w, xp, rp, yp, beta, (hipStream_t)stream);
     LT_CHECK(hipblasLtMatmul(d->handle, p.desc, &alpha, w, p.a, xp, p.b, &beta, rp, p.cd, yp, p.cd, &p.algo, d->ws,
                              p.ws, (hipStream_t)stream));
   }
