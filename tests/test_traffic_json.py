@@ -38,3 +38,23 @@ def test_traffic_json_sites(tmp_path):
     assert sites["pinv_fwd"]["traffic_bytes"] == int((2 * 16 + 8) * kib)
     assert sites["pinv_fwd"]["dispatches"] == [4, 4]
     assert sites["ln_fwd:1"]["algorithmic_bytes"] > 0
+
+
+def test_committed_traffic_reaches_the_bench_on_the_gpu_box():
+    """bench.py's roofline.traffic reads profiles/traffic.json at run time on the GPU box: the file
+    must be committed for the bench workload and must not be excluded from the gpurun snapshot
+    (.gpurunignore patterns are tar excludes; an exclude of the whole profiles/ directory made the
+    round-3 / early round-4 bench lines carry traffic: null)."""
+    import fnmatch
+    sys.path.insert(0, ROOT)
+    import bench
+    rec = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))["sites"]
+    for site in ("pinv_fwd", "pinv_bwd", "ln_fwd:1", "a3_bwd:1"):
+        assert bench.measured_traffic(site, 8192, "bf16") == rec[site]["traffic_bytes"] > 0
+    pats = [l.strip() for l in open(os.path.join(ROOT, ".gpurunignore")) if l.strip() and not l.startswith("#")]
+    member = "./profiles/traffic.json"
+    for p in pats:
+        anchored = p.startswith("./")
+        hit = fnmatch.fnmatch(member, p) if anchored else fnmatch.fnmatch(os.path.basename(member), p)
+        hit = hit or (anchored and member.startswith(p.rstrip("/") + "/"))
+        assert not hit, f".gpurunignore pattern {p!r} drops {member}"
