@@ -54,7 +54,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)   # 20 warm-up, >= 200 timed steps
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--n", type=int, default=8192, help="patches per bag")
+    # --n-patches: the same option under a name torch.distributed.run does not take for its own
+    # (it reads a bare --n after the script name as an ambiguous abbreviation of --nnodes / --nproc...)
+    ap.add_argument("--n", "--n-patches", dest="n", type=int, default=8192, help="patches per bag")
     ap.add_argument("--classes", type=int, default=2)
     ap.add_argument("--features", type=int, default=512, choices=[512, 2048],
                     help="in_features: 512 (Linear+GELU _fc1, the metric's config) or 2048 (the RCC "
@@ -345,10 +347,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # TM_BENCH_BACKEND=gloo: a rehearsal of the N > 1 control flow on fewer GPUs than ranks (ranks
+    # share devices round-robin; gloo all-reduces the CUDA buckets; use with --eager, gloo does not
+    # capture).  The measured path is RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("TM_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -443,7 +454,9 @@ def main():
         return sum(xs) / len(xs) if xs else None
 
     hbm = None
-    if rank == 0 and not args.no_hbm_probe and args.features == 512:
+    if not args.no_hbm_probe and args.features == 512:
+        # every rank runs the probe steps: each step's gradient all-reduce is a collective, so a
+        # rank-0-only probe would leave rank 0 waiting in it at N > 1 (rank 0 reports the result)
         def probe_step(i):
             load(i)
             body()
@@ -535,6 +548,7 @@ def main():
                                                               threads=(out["cpu_baseline"]["cores"],))
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier()      # rank 0's CPU baselines / print done before any rank tears down
         dist.destroy_process_group()
 
 

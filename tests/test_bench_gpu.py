@@ -48,3 +48,25 @@ def test_bench_graph_step_equals_eager_optimization_step(K):
     assert moved
     bad = [n for n in pa if not torch.equal(pa[n], pb[n])]
     assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_two_rank_bench_control_flow_completes():
+    """bench.py at N = 2 (torch.distributed.run, two ranks sharing this GPU through the gloo
+    rehearsal backend, eager): the timed loop, the post-timed probes (HBM sites, pseudo-inverse
+    roofline) and the teardown run their gradient all-reduces on EVERY rank, so the run ends and
+    rank 0 prints one JSON line with n_gpus = 2 (a rank-0-only probe step left rank 0 waiting in
+    its all-reduce)."""
+    import json
+    import subprocess
+    env = dict(os.environ, TM_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29517", "bench.py", "--gpus", "2", "--eager",
+           "--n-patches", "1024", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "dp2"
+    assert d["hbm_roofline"], "the HBM probe ran on every rank and rank 0 reported it"
