@@ -452,3 +452,38 @@ def test_fused_head_backward_equals_two_launch_path(train):
     bad = [n for n in grads[0] if not torch.equal(grads[0][n], grads[1][n])]
     assert not bad, bad
     assert all(torch.isfinite(v).all() for v in grads[0].values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,dtype", [(1, torch.float32), (3, torch.float32), (1, torch.bfloat16)])
+def test_graphed_optimization_step_equals_eager(K, dtype):
+    """GraphedOptimizationStep (one eager accumulation window, then one captured hipGraph per
+    phase replayed over static inputs) leaves the parameters bitwise equal to
+    TransMILTask.optimization_step on the same micro-batch sequence (train mode: dropout masks
+    drawn from the device counter in both), and returns the same losses."""
+    from transmil_deepgraft_amd.interface import GradAllReduce, GraphedOptimizationStep, TransMILTask
+    from transmil_deepgraft_amd.models import TransMIL
+
+    def build():
+        torch.manual_seed(11)
+        m = TransMIL(2, 512, 512).cuda().train().set_compute_dtype(dtype)
+        task = TransMILTask(m, accumulate_grad_batches=K)
+        return m, task, task.configure_optimizers()[0][0], GradAllReduce(m.parameters(), model=m)
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    bags = [torch.rand(1, 300, 512, device="cuda", generator=g) for _ in range(2)]
+    labels = [torch.tensor([j % 2], device="cuda") for j in range(2)]
+    n = 3 * K + 1
+    ma, ta, oa, ara = build()
+    gstep = GraphedOptimizationStep(ta, oa, ara)
+    la = [gstep((bags[i % 2], labels[i % 2], None)).clone() for i in range(n)]
+    assert gstep.graphs is not None
+    mb, tb, ob, arb = build()
+    lb = [tb.optimization_step((bags[i % 2], labels[i % 2], None), ob, allreduce=arb).clone() for i in range(n)]
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(la, lb)), (la, lb)
+    pa, pb = dict(ma.named_parameters()), dict(mb.named_parameters())
+    bad = [k for k in pa if not torch.equal(pa[k], pb[k])]
+    assert not bad, bad
+    with pytest.raises(ValueError):
+        gstep((torch.rand(1, 301, 512, device="cuda"), labels[0], None))
