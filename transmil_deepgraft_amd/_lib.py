@@ -191,8 +191,14 @@ def last_error() -> str:
     return lib().tm_last_error().decode()
 
 
+_FNS = {}
+
+
 def call(name: str, *args) -> None:
-    rc = getattr(lib(), name)(*args)
+    fn = _FNS.get(name)
+    if fn is None:
+        fn = _FNS[name] = getattr(lib(), name)
+    rc = fn(*args)
     if rc != 0:
         raise RuntimeError(f"{name} failed (rc={rc}): {last_error()}")
 

@@ -200,10 +200,16 @@ class TransMIL(nn.Module):
         if any(getattr(g, n, None) for n in ("_global_forward_hooks", "_global_forward_pre_hooks",
                                               "_global_backward_hooks", "_global_backward_pre_hooks")):
             return True
-        for m in self.modules():
-            if m is not self and (m._forward_hooks or m._forward_pre_hooks or m._backward_hooks
-                                  or getattr(m, "_backward_pre_hooks", None)):
+        # a plain stack walk of the submodule tree (Module.modules()' generator chain with its memo
+        # set was ~60 us of the eager step's host path)
+        stack = list(self._modules.values())
+        while stack:
+            m = stack.pop()
+            if m is None:
+                continue
+            if m._forward_hooks or m._forward_pre_hooks or m._backward_hooks or getattr(m, "_backward_pre_hooks", None):
                 return True
+            stack.extend(m._modules.values())
         return False
 
     def _forward_modules(self, x, return_attn):
