@@ -530,7 +530,8 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
 // dX[i][j] = dXc[i][j] + G0[j][i]/c + sign(X_ij) (tie_c(i) dMc/nc + tie_r(j) dMr/nr),
 // dc = -sum(G0 o Z0)/c = -T/c^2,  dMc = dc * maxr, dMr = dc * maxc  (max ties share the gradient);
 // softmax != 0: out = X o (dX - rowsum(X o dX)) (the backward of A2 = softmax, X = A2), else out = dX.
-// grid (nbh, 16), block 256: 16 rows of one head, thread = column j.
+// grid (nbh, 256 / APPLY_ROWS), block 256: APPLY_ROWS rows of one head, thread = column j.
+constexpr int APPLY_ROWS = 8;   // 256 workgroups at nbh = 8 (16 rows: 128, half the CUs idle)
 constexpr int APPLY_SUMS = 8;   // |X| sums per thread per kind in one burst (nbh <= 8); larger nbh loops
 __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __restrict__ X, const float* __restrict__ sums,
                                                              const float* __restrict__ maxima, const bf16* __restrict__ G0,
@@ -540,22 +541,23 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
                                                              float* __restrict__ out) {
   __shared__ float red[4][16];
   __shared__ float bc[4];
-  const int bh = blockIdx.x, i0 = blockIdx.y * 16, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int RB = APPLY_ROWS;
+  const int bh = blockIdx.x, i0 = blockIdx.y * RB, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const size_t hb = (size_t)bh * MAT;
   // every load is issued up front (one memory round trip): G0[t][i0..i0+15] (the transpose term of
   // column t, 32 contiguous bytes per plane), X and dXc rows i0..i0+15 at column t, this block's
   // row sums and column sum, the per-head maxima (lane h), the |X| sums for the tie counts and the
   // partial dots (lane-strided, clamped, masked)
-  float g0[16], xv[16], dx[16];
+  static_assert(RB == 8, "one 16-B piece per plane of G0's transposed row");
+  float g0[RB], xv[RB], dx[RB];
   {
     const size_t o = hb + (size_t)t * NL + i0;
-    const bf16x8 h0 = *(const bf16x8*)(G0 + o), h1 = *(const bf16x8*)(G0 + o + 8);
-    const bf16x8 l0 = *(const bf16x8*)(G0 + plane + o), l1 = *(const bf16x8*)(G0 + plane + o + 8);
+    const bf16x8 h0 = *(const bf16x8*)(G0 + o), l0 = *(const bf16x8*)(G0 + plane + o);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { g0[e] = (float)h0[e] + (float)l0[e]; g0[8 + e] = (float)h1[e] + (float)l1[e]; }
+    for (int e = 0; e < 8; ++e) g0[e] = (float)h0[e] + (float)l0[e];
   }
 #pragma unroll
-  for (int ii = 0; ii < 16; ++ii) {
+  for (int ii = 0; ii < RB; ++ii) {
     const size_t off = hb + (size_t)(i0 + ii) * NL + t;
     xv[ii] = X[off];
     dx[ii] = dXc[off];
@@ -563,9 +565,9 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
   const float* rs = sums + (size_t)bh * NL;
   const float* cs = sums + (size_t)(nbh + bh) * NL;
   const float csv = cs[t];
-  float rsv[16];
+  float rsv[RB];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < RB / 4; ++q) {
     const f32x4 v = *(const f32x4*)(rs + i0 + 4 * q);
     rsv[4 * q] = v[0]; rsv[4 * q + 1] = v[1]; rsv[4 * q + 2] = v[2]; rsv[4 * q + 3] = v[3];
   }
@@ -602,25 +604,25 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
   const float dMc = dc * mr / bc[0], dMr = dc * mc / bc[1];
   const float tie_r = csv == mr ? dMr : 0.f;
 #pragma unroll
-  for (int ii = 0; ii < 16; ++ii) {
+  for (int ii = 0; ii < RB; ++ii) {
     const float sg = xv[ii] > 0.f ? 1.f : (xv[ii] < 0.f ? -1.f : 0.f);
     const float tie_c = rsv[ii] == mc ? dMc : 0.f;
     dx[ii] = dx[ii] + g0[ii] * ic + sg * (tie_c + tie_r);
   }
   if (!softmax) {
 #pragma unroll
-    for (int ii = 0; ii < 16; ++ii) out[hb + (size_t)(i0 + ii) * NL + t] = dx[ii];
+    for (int ii = 0; ii < RB; ++ii) out[hb + (size_t)(i0 + ii) * NL + t] = dx[ii];
     return;
   }
   __syncthreads();
 #pragma unroll
-  for (int ii = 0; ii < 16; ++ii) {
+  for (int ii = 0; ii < RB; ++ii) {
     const float d = wave_sum(xv[ii] * dx[ii]);
     if (lane == 0) red[wave][ii] = d;
   }
   __syncthreads();
 #pragma unroll
-  for (int ii = 0; ii < 16; ++ii) {
+  for (int ii = 0; ii < RB; ++ii) {
     const float rd = (red[0][ii] + red[1][ii]) + (red[2][ii] + red[3][ii]);
     out[hb + (size_t)(i0 + ii) * NL + t] = xv[ii] * (dx[ii] - rd);
   }
@@ -1028,7 +1030,7 @@ extern "C" int tm_pinv_bwd_split(const float* X, const void* Xs, int nbh, int it
   c.part = part;
   if (int rc = run_levels(c, 1, plane, maxima, F.team_ctr(nbh, 1), st)) return rc;
   // Z_0 = X^T / c: the transpose term, the max-tie terms and the softmax
-  pinv_apply_bwd_kernel<<<dim3(nbh, 16), 256, 0, st>>>(X, F.sums(), maxima, G, plane, part, nbh * 16, nbh, dXc,
+  pinv_apply_bwd_kernel<<<dim3(nbh, NL / APPLY_ROWS), 256, 0, st>>>(X, F.sums(), maxima, G, plane, part, nbh * 16, nbh, dXc,
                                                         softmax, out);
   TM_CHECK_LAUNCH();
   return 0;
