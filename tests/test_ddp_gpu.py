@@ -71,8 +71,14 @@ def test_rccl_allreduce_inside_captured_graph(overlap):
     import torch.distributed as dist
     from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
     import gc
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
-                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    for attempt in range(5):   # a port free at probe time can be taken before the store binds it
+        try:
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                    device_id=torch.device("cuda", torch.cuda.current_device()))
+            break
+        except dist.DistNetworkError:
+            if attempt == 4:
+                raise
     graph = ar = None
     try:
         a, b = _model(3), _model(3)
