@@ -59,9 +59,13 @@ def test_two_rank_bench_control_flow_completes():
     its all-reduce)."""
     import json
     import subprocess
+    import socket
+    with socket.socket() as sk:        # a free port, not a fixed one (the box is shared)
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
     env = dict(os.environ, TM_BENCH_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29517", "bench.py", "--gpus", "2", "--eager",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--eager",
            "--n-patches", "1024", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr[-3000:]
