@@ -531,7 +531,7 @@ __global__ __launch_bounds__(NTHREADS) void pinv_stage_kernel(SLaunch L) {
 // dc = -sum(G0 o Z0)/c = -T/c^2,  dMc = dc * maxr, dMr = dc * maxc  (max ties share the gradient);
 // softmax != 0: out = X o (dX - rowsum(X o dX)) (the backward of A2 = softmax, X = A2), else out = dX.
 // grid (nbh, 256 / APPLY_ROWS), block 256: APPLY_ROWS rows of one head, thread = column j.
-constexpr int APPLY_ROWS = 8;   // 256 workgroups at nbh = 8 (16 rows: 128, half the CUs idle)
+constexpr int APPLY_ROWS = 4;   // 512 workgroups at nbh = 8 (16 rows: 128, half the CUs idle)
 constexpr int APPLY_SUMS = 8;   // |X| sums per thread per kind in one burst (nbh <= 8); larger nbh loops
 __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __restrict__ X, const float* __restrict__ sums,
                                                              const float* __restrict__ maxima, const bf16* __restrict__ G0,
@@ -548,13 +548,19 @@ __global__ __launch_bounds__(256) void pinv_apply_bwd_kernel(const float* __rest
   // column t, 32 contiguous bytes per plane), X and dXc rows i0..i0+15 at column t, this block's
   // row sums and column sum, the per-head maxima (lane h), the |X| sums for the tie counts and the
   // partial dots (lane-strided, clamped, masked)
-  static_assert(RB == 8, "one 16-B piece per plane of G0's transposed row");
+  static_assert(RB == 4 || RB == 8, "one 8- or 16-B piece per plane of G0's transposed row");
   float g0[RB], xv[RB], dx[RB];
   {
     const size_t o = hb + (size_t)t * NL + i0;
-    const bf16x8 h0 = *(const bf16x8*)(G0 + o), l0 = *(const bf16x8*)(G0 + plane + o);
+    if constexpr (RB == 8) {
+      const bf16x8 h0 = *(const bf16x8*)(G0 + o), l0 = *(const bf16x8*)(G0 + plane + o);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) g0[e] = (float)h0[e] + (float)l0[e];
+      for (int e = 0; e < 8; ++e) g0[e] = (float)h0[e] + (float)l0[e];
+    } else {
+      const bf16x4 h0 = *(const bf16x4*)(G0 + o), l0 = *(const bf16x4*)(G0 + plane + o);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) g0[e] = (float)h0[e] + (float)l0[e];
+    }
   }
 #pragma unroll
   for (int ii = 0; ii < RB; ++ii) {
