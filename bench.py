@@ -17,6 +17,8 @@ Prints ONE JSON line on rank 0.  Extra objects:
                    forward chain (tm_pinv_fwd_split: 14 launches of pinv_stage_kernel, the
                    largest share of the step in profiles/r02_*_kernel_summary.txt), its
                    algorithmic flops / the HIP-event span of the call on its stream
+  gemm_roofline -- the dense projections (to_qkv, to_out, _fc1 and their backward products): per call
+                   site and layer, 2 M N K / the same probe's event span, against the dense bf16 peak
   hbm_roofline  -- the HBM-bound NystromAttention / PPEG / LayerNorm kernels (north_star: >= 50 %
                    of HBM roofline): per call site and layer, algorithmic bytes (every compulsory
                    tensor read or written once) / the HIP-event span of the
@@ -121,7 +123,20 @@ def roofline_model(site, n_patches, dtype_bytes):
     raise ValueError(site)
 
 
-HBM_SITES = ("ln_fwd", "landmarks", "a3_fwd", "a1_fwd", "ppeg_fwd", "ppeg_bwd", "conv_bwd", "a3_bwd")
+HBM_SITES = ("ln_fwd", "landmarks", "a3_fwd", "a1_fwd", "ppeg_fwd", "ppeg_bwd", "conv_bwd", "a1_bwd", "a3_bwd")
+
+# the dense d_model projections (code/models/TransMIL.py:26-34 to_qkv / to_out, :128-133 _fc1) and
+# their backward products: site -> (layers in call order, M, N, K as functions of (n', N patches))
+GEMM_SITES = {
+    "fc1_gemm": ((0,), lambda n, N: (N, 512, 512), "_fc1 Linear + GELU (+ grid-pad rows)"),
+    "qkv_gemm": ((1, 2), lambda n, N: (n, 1536, 512), "to_qkv (+ head-major scatter, q scale)"),
+    "out_gemm": ((1,), lambda n, N: (n, 512, 512), "to_out + bias + dropout + residual"),
+    "wgrad_out": ((1,), lambda n, N: (512, 512, n), "dW_out split-K (+ bias gradient)"),
+    "dmerged_gemm": ((1,), lambda n, N: (n, 512, 512), "dmerged = dout W_out"),
+    "wgrad_qkv": ((2, 1), lambda n, N: (1536, 512, n), "dW_qkv split-K"),
+    "dxn_gemm": ((2, 1), lambda n, N: (n, 512, 1536), "dxn = dqkv W_qkv"),
+    "wgrad_fc1": ((0,), lambda n, N: (512, 512, N), "dW_fc1 split-K (+ bias gradient)"),
+}
 
 
 def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
@@ -143,6 +158,8 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
     ppf = 2 * S * d * f4                             # H1 in, H2 out (fp32 residual stream)
     ppb = 3 * S * d * f4 + n * d * t                 # H1, dH in; dH1 out; layer 1's padded dropout gradient out
     cvb = 3 * n * d * t + n * d * f4 + heads * n * f4   # dmerged, merged, v in; dv (fp32), D1 out
+    # q, dO in (T); lse1, D1 in; k~, Y (T) in; dq out (T: the precision dqkv carries); dk~, dY out (fp32)
+    a1b = 2 * n * d * t + 2 * heads * n * f4 + 2 * lm * t + n * d * t + 2 * lm * f4
     a3b_small = 2 * lm * t + 2 * heads * m * f4 + lm * f4 + lm * f4   # q~, dW in, lse3, D3, dk~ in, dq~3 out
     a3b_l2 = 2 * n * d * t + 2 * n * d * t + a3b_small                # k, v in; dk, dv (into dqkv) out
     a3b_l1 = a3b_l2 + n * d * f4                                      # + the conv path's fp32 dv in
@@ -157,6 +174,8 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
         # (the weight-gradient slab sums ride in the deferred multi_reduce flush that follows)
         ("ppeg_bwd", 0): ("ppeg_stencil_kernel<true> + ppeg_wgrad_kernel", ppb),
         ("conv_bwd", 1): ("conv_bwd_mfma_kernel", cvb),
+        # the kernel alone; its dk~ / dY partial slabs are summed in the deferred flush that follows
+        ("a1_bwd", 1): ("attn_bwd_bf16_kernel<1, 8> (dk~ / dY slab sums in the deferred flush)", a1b),
         ("a3_bwd", 2): ("attn_bwd_bf16_kernel<0, 9> (fused dk / dv epilogue)", a3b_l2),
         ("a3_bwd", 1): ("attn_bwd_bf16_kernel<0, 9> (fused dk / dv epilogue)", a3b_l1),
     }
@@ -164,12 +183,14 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
 
 # layer of the k-th call of a site within one step (forward: layer 1 then 2; backward: 2 then 1)
 SITE_LAYERS = {"ln_fwd": (1, 2), "landmarks": (1, 2), "a3_fwd": (1, 2), "a1_fwd": (1,), "ppeg_fwd": (0,),
-               "ppeg_bwd": (0,), "conv_bwd": (1,), "a3_bwd": (2, 1)}
+               "ppeg_bwd": (0,), "conv_bwd": (1,), "a1_bwd": (1,), "a3_bwd": (2, 1)}
 
 
-def hbm_roofline(engine, run_step, steps, n_patches, dtype_bytes):
-    """Eager probe steps with every HBM site timed (spin ahead, empty event pair subtracted)."""
-    engine.probe.target = set(HBM_SITES)
+def probe_sites(engine, run_step, steps, sites):
+    """Eager probe steps with every site in ``sites`` timed: a GPU spin queued ahead of each probed
+    launch so its events bracket the kernel, the span of an empty event pair recorded just before it
+    subtracted.  Returns site -> [ms per call, in call order over the steps]."""
+    engine.probe.target = set(sites)
     engine.probe.spin_cycles = 2_000_000
     engine.probe.events.clear()
     engine.probe.names.clear()
@@ -182,6 +203,34 @@ def hbm_roofline(engine, run_step, steps, n_patches, dtype_bytes):
     for name, ev in zip(engine.probe.names, engine.probe.events):
         s, e, zs, ze = ev
         per.setdefault(name, []).append(s.elapsed_time(e) - zs.elapsed_time(ze))
+    return per
+
+
+def gemm_roofline(per, n_patches):
+    """The dense projections against the dense bf16 MFMA peak: algorithmic flops (2 M N K) / the
+    probe's median event span per call site and layer (the split-K products' slab sums run in the
+    deferred flush, not in this span)."""
+    import math
+    G = math.ceil(math.sqrt(n_patches))
+    n = (G * G + 1 + 255) // 256 * 256
+    out = []
+    for site, (layers, shape, what) in GEMM_SITES.items():
+        xs = per.get(site, [])
+        if not xs or len(xs) % len(layers):
+            continue
+        M, N, K = shape(n, n_patches)
+        flops = 2 * M * N * K
+        for k, layer in enumerate(layers):
+            v = sorted(xs[k::len(layers)])
+            ms = v[len(v) // 2]
+            tfs = flops / (ms / 1e3) / 1e12
+            out.append(dict(site=site, layer=layer, what=what, M=M, N=N, K=K, flops=flops, us=round(ms * 1e3, 2),
+                            achieved_tfs=round(tfs, 1), peak_tfs=BF16_PEAK_TFS, frac=round(tfs / BF16_PEAK_TFS, 4)))
+    return out
+
+
+def hbm_roofline(per, n_patches, dtype_bytes):
+    """HBM-bound sites: algorithmic bytes / the probe's median event span, against 8 TB/s."""
     model = hbm_model(n_patches, dtype_bytes)
     out = []
     for site in HBM_SITES:
@@ -453,14 +502,16 @@ def main():
         xs = [v for nm, v in samples if nm == site]
         return sum(xs) / len(xs) if xs else None
 
-    hbm = None
+    hbm = gemms = None
     if not args.no_hbm_probe and args.features == 512:
         # every rank runs the probe steps: each step's gradient all-reduce is a collective, so a
         # rank-0-only probe would leave rank 0 waiting in it at N > 1 (rank 0 reports the result)
         def probe_step(i):
             load(i)
             body()
-        hbm = hbm_roofline(engine, probe_step, 3, args.n, 2 if args.dtype == "bf16" else 4)
+        per = probe_sites(engine, probe_step, 3, set(HBM_SITES) | set(GEMM_SITES))
+        hbm = hbm_roofline(per, args.n, 2 if args.dtype == "bf16" else 4)
+        gemms = gemm_roofline(per, args.n) if args.dtype == "bf16" else None
 
     # the optimizer step alone (it is also inside every timed step): a graph of opt.step()
     # replayed 20 times between two events (after the timed region; it advances the state)
@@ -539,6 +590,7 @@ def main():
             "roofline": roof,
             "roofline_pinv_bwd": roofline_obj("pinv_bwd") if args.probe == "pinv_fwd" else None,
             "hbm_roofline": hbm,
+            "gemm_roofline": gemms,
             "optimizer_ms": round(opt_ms, 5) if opt_ms is not None else None,
         }
         if not args.no_cpu_baseline and world == 1:

@@ -11,7 +11,8 @@
  * Conventions (all entry points):
  *   - device pointers are caller-owned; nothing is allocated inside;
  *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
- *   - no host synchronisation, so every call is hipGraph-capturable;
+ *   - no host synchronisation, so every call is hipGraph-capturable -- with ONE documented
+ *     exception, tm_conv1x1_tune (a host-timed algorithm search, refused during capture);
  *   - deterministic: no float atomics, fixed reduction orders;
  *   - return 0 on success, 1 on a bad argument, 2 on a launch error;
  *     tm_last_error() returns the thread-local message.
@@ -313,9 +314,22 @@ int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int
 /* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
  * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout])
  * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.
- * bias / residual may be NULL; residual must not alias y.  Returns 3 on a hipBLASLt error. */
+ * bias / residual may be NULL; residual must not alias y.  workspace: caller-owned device scratch
+ * of ws_bytes, stream-ordered on `stream` (NULL / 0: workspace-free algorithms only; up to
+ * tm_conv1x1_workspace_bytes() is used).  Library state: a per-device hipBLASLt handle and a
+ * per-shape plan cache (host objects behind a mutex, immutable once built -- no device scratch is
+ * shared between calls).  No host synchronisation.  Returns 3 on a hipBLASLt error. */
+long long tm_conv1x1_workspace_bytes(void);
 int tm_conv1x1(int dtype, const void* x, const void* w, const void* bias, const void* residual, void* y,
-               long long rows, int cin, int cout, int relu, void* stream);
+               long long rows, int cin, int cout, int relu, void* workspace, long long ws_bytes, void* stream);
+/* THE EXCEPTION to "no host synchronisation": times every hipBLASLt heuristic candidate for this
+ * shape on the given operands (y is overwritten) and waits on timing events, then keeps the fastest
+ * for later tm_conv1x1 calls of the shape (the hipBLASLt analogue of MIOpen find).  Call once per
+ * shape, outside stream capture (refused with status 1 while `stream` is capturing); without it
+ * tm_conv1x1 uses the heuristic's first choice. */
+int tm_conv1x1_tune(int dtype, const void* x, const void* w, const void* bias, const void* residual, void* y,
+                    long long rows, int cin, int cout, int relu, void* workspace, long long ws_bytes,
+                    void* stream);
 /* Train-mode BatchNorm2d over a channels-last activation given as npieces (1..64) row pieces
  * xs[p] of [rows[p], C] (host arrays; C a power of two, 8..2048; nn.BatchNorm2d.forward in
  * training, code/models/ResNet.py:95-117 under model.train()): batch statistics over all pieces
@@ -403,6 +417,11 @@ typedef struct tm_optim_table {
   int reserved;
   long long offset[TM_OPTIM_MAX_TENSORS + 1];
   tm_optim_tensor t[TM_OPTIM_MAX_TENSORS];
+  /* device [count][2] fp32 (lr, weight_decay) read by the kernel in place of t[i].lr /
+   * t[i].weight_decay, or NULL.  A captured hipGraph replays the kernel arguments it was captured
+   * with; reading the hyper-parameters from device memory lets an LR scheduler (ReduceLROnPlateau,
+   * model_interface.py:862-877) act on a replayed step (the caller rewrites the buffer). */
+  const float* hyper;
 } tm_optim_table;
 long long tm_radam_counters_len(long long total_elements);
 int tm_radam_lookahead_step(const tm_optim_table* table, float* exp_avg, float* exp_avg_sq, float* slow,

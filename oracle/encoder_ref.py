@@ -26,6 +26,13 @@ BN_EPS = 1e-5
 
 
 def _bn(x, sd, pre):
+    given = sd.get("__stats_in__")
+    if given is not None and pre in given:
+        # train-mode BN whose batch statistics were taken over a larger batch than x (a subset of a
+        # bag's tiles normalised with the whole bag's mean / biased variance)
+        mean, var = given[pre]
+        return F.batch_norm(x, mean.to(x), var.to(x), sd[pre + ".weight"], sd[pre + ".bias"], training=False,
+                            eps=BN_EPS)
     return F.batch_norm(x, sd[pre + ".running_mean"], sd[pre + ".running_var"], sd[pre + ".weight"],
                         sd[pre + ".bias"], training=sd["__train__"], momentum=sd["__momentum__"], eps=BN_EPS)
 
@@ -42,13 +49,17 @@ def _bottleneck(x, sd, pre, stride):
 
 
 def features(tiles: torch.Tensor, state_dict: dict, dtype=torch.float64, train=False, momentum=0.1,
-             stats_out: dict | None = None) -> torch.Tensor:
+             stats_out: dict | None = None, stats_in: dict | None = None) -> torch.Tensor:
     """tiles [n, 3, 224, 224] -> features [n, 2048] (``dtype`` arithmetic on the CPU).  With
     ``train``: batch-statistics BatchNorm over all n tiles; the updated running statistics go into
-    ``stats_out`` (name -> tensor) when given."""
+    ``stats_out`` (name -> tensor) when given.  ``stats_in`` (BN module name, e.g. "layer1.0.bn2" ->
+    (mean, biased variance)): those BatchNorms normalise with the given batch statistics instead of
+    the n tiles' own (a subset of a bag whose statistics span the whole bag)."""
     sd = {k: v.detach().to("cpu", dtype).clone() for k, v in state_dict.items()
           if not k.endswith("num_batches_tracked")}
     sd["__train__"], sd["__momentum__"] = bool(train), momentum
+    sd["__stats_in__"] = None if stats_in is None else {
+        k: (m.detach().to("cpu", dtype), v.detach().to("cpu", dtype)) for k, (m, v) in stats_in.items()}
     x = tiles.detach().to("cpu", dtype)
     x = F.relu(_bn(F.conv2d(x, sd["conv1.weight"], stride=2, padding=3), sd, "bn1"))
     x = F.max_pool2d(x, 3, 2, 1)
@@ -57,5 +68,5 @@ def features(tiles: torch.Tensor, state_dict: dict, dtype=torch.float64, train=F
             stride = 2 if (li > 1 and bi == 0) else 1
             x = _bottleneck(x, sd, f"layer{li}.{bi}", stride)
     if stats_out is not None:
-        stats_out.update({k: v for k, v in sd.items() if k.endswith(("running_mean", "running_var"))})
+        stats_out.update({k: v for k, v in sd.items() if isinstance(k, str) and k.endswith(("running_mean", "running_var"))})
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)

@@ -165,3 +165,52 @@ def test_engine_binds_one_queue_per_backward_call_and_thread():
     assert seen[0][0] == seen[0][1] and seen[1][0] == seen[1][1]
     assert seen[(0, "after")] is None and seen[(1, "after")] is None
     assert E._rq().value is None
+
+
+def _strip_diag_blocks(text):
+    """The source without `#ifdef TM_DIAG ... #endif` blocks (the diagnostic build's code)."""
+    out, depth, diag = [], 0, []
+    for line in text.split("\n"):
+        s = line.strip()
+        if s.startswith("#if"):
+            depth += 1
+            diag.append(s.startswith("#ifdef TM_DIAG") or s.startswith("#if defined(TM_DIAG)"))
+            continue
+        if s.startswith("#endif"):
+            depth -= 1
+            diag.pop()
+            continue
+        if s.startswith("#else") and diag:
+            diag[-1] = not diag[-1] if diag[-1] else diag[-1]
+            continue
+        if not any(diag):
+            out.append(line)
+    return "\n".join(out)
+
+
+def test_only_the_documented_entry_point_synchronises():
+    """The header promises no host synchronisation and no library-owned device scratch, with ONE
+    documented exception: tm_conv1x1_tune (host-timed hipBLASLt algorithm search, refused during
+    capture).  No product source waits on the device or allocates device memory anywhere else
+    (TM_DIAG-only code excluded: the diagnostic library is not the product)."""
+    import glob
+    head = open(HEADER).read()
+    conventions = head[:head.index("#ifndef TRANSMIL_HIP_H")]
+    assert "ONE documented" in conventions and "tm_conv1x1_tune" in conventions
+    proto = head[head.index("int tm_conv1x1_tune("):]
+    assert "refused" in head[head.index("THE EXCEPTION"):head.index("int tm_conv1x1_tune(")]
+    assert proto
+    pat = re.compile(r"\b(hipDeviceSynchronize|hipStreamSynchronize|hipEventSynchronize|hipMemcpy|"
+                     r"hipMemcpyFromSymbol|hipMalloc|hipMallocManaged|hipHostMalloc)\s*\(")
+    hits = {}
+    for path in sorted(glob.glob(os.path.join(ROOT, "transmil_deepgraft_amd", "csrc", "*.hip")) +
+                       glob.glob(os.path.join(ROOT, "transmil_deepgraft_amd", "csrc", "*.h"))):
+        text = _strip_diag_blocks(open(path).read())
+        found = pat.findall(text)
+        if found:
+            hits[os.path.basename(path)] = found
+    assert hits == {"conv1x1.hip": ["hipEventSynchronize"]}, hits
+    src = open(os.path.join(ROOT, "transmil_deepgraft_amd", "csrc", "conv1x1.hip")).read()
+    # ... and that one wait sits in the tuning branch, which refuses a capturing stream
+    assert src.index("hipEventSynchronize") > src.index("if (tune && !p->tuned)")
+    assert "not during stream capture" in src

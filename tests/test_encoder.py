@@ -115,6 +115,39 @@ def test_encoder_oracle_pinned_by_reference_fixture():
     np.testing.assert_allclose(features(x, sd, torch.float32).numpy(), fx["feats"], rtol=1e-5, atol=1e-5)
 
 
+def test_library_calls_stay_below_2_31_elements():
+    """Every library convolution / pooling of the encoder is handed < 2^31 elements: the guard
+    refuses a 2675-tile stem input (its output is 2675 x 64 x 112 x 112 > 2^31 - 1) before it reaches
+    MIOpen, a 2674-tile one passes (meta tensors: shapes only, nothing is computed)."""
+    from transmil_deepgraft_amd import encoder as E
+    assert E.tile_elems_max(224, 224) == 64 * 112 * 112
+    cap = E.max_tiles_per_call(224, 224)
+    assert cap == 2674 and cap * 64 * 112 * 112 <= 2 ** 31 - 1 < (cap + 1) * 64 * 112 * 112
+    w = torch.empty(64, 3, 7, 7, device="meta")
+    y = E._lib_conv2d(torch.empty(cap, 3, 224, 224, device="meta"), w, stride=2, padding=3)
+    assert tuple(y.shape) == (cap, 64, 112, 112)
+    with pytest.raises(RuntimeError, match="2\\^31"):
+        E._lib_conv2d(torch.empty(cap + 1, 3, 224, 224, device="meta"), w, stride=2, padding=3)
+    with pytest.raises(RuntimeError, match="2\\^31"):
+        E._lib_max_pool(torch.empty(cap + 1, 64, 112, 112, device="meta"))
+    E._lib_max_pool(torch.empty(cap, 64, 112, 112, device="meta"))
+
+
+def test_train_pieces_respect_the_statistics_call_and_the_library_limit():
+    """Train-mode bag pieces: at least ``chunk`` tiles, at most 64 pieces per BatchNorm statistics
+    call (tm_bn_train_stats), never more than max_tiles_per_call() tiles; a bag no piece size can
+    serve raises instead of failing inside the statistics call."""
+    from transmil_deepgraft_amd.encoder import max_tiles_per_call, train_pieces
+    cap = max_tiles_per_call()
+    assert train_pieces(4096, 512) == 512                    # C5: 8 pieces
+    assert train_pieces(4096, 4096) == cap                   # chunk above the cap: clamped (2 pieces)
+    assert train_pieces(6, 2) == 2
+    assert train_pieces(40000, 512) == 625                   # 64 pieces of 625 tiles
+    assert train_pieces(64 * cap, 512) == cap
+    with pytest.raises(RuntimeError, match="64 pieces"):
+        train_pieces(64 * cap + 1, 512)
+
+
 C5_TILES = 4096     # BASELINE config C5: one slide of 4096 224x224 tiles
 
 
@@ -225,7 +258,8 @@ def test_conv1x1_epilogue_matches_torch(dtype, tol, rows, cin, cout, relu, res):
     b = torch.randn(cout, device="cuda", generator=g).to(dtype)
     r = torch.randn(rows, cout, device="cuda", generator=g).to(dtype) if res else None
     y = torch.full((rows, cout), float("nan"), device="cuda", dtype=dtype)
-    _lib.call("tm_conv1x1", _dtype_code(x), _p(x), _p(w), _p(b), _p(r), _p(y), rows, cin, cout, int(relu), _stream())
+    _lib.call("tm_conv1x1", _dtype_code(x), _p(x), _p(w), _p(b), _p(r), _p(y), rows, cin, cout, int(relu), None, 0,
+              _stream())
     ref = x.float() @ w.float().t() + b.float() + (r.float() if res else 0)
     ref = ref.clamp_min(0) if relu else ref
     torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
@@ -284,3 +318,69 @@ def test_bn_train_kernels_match_fp64(dtype, rows, C):
         got = y.permute(0, 2, 3, 1).reshape(rows, C).double()
         tol = 1e-5 if dtype == torch.float32 else 1e-2
         torch.testing.assert_close(got, ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+def test_c5_train_mode_bn_4096_tiles(monkeypatch):
+    """Config C5's encoder in train mode at its own size (4096 tiles, fp32; the reference's frozen
+    encoder under Lightning's model.train(), code/models/model_interface.py:237-247,303-309): the
+    bag runs in 8 pieces of 512 tiles (every library tensor < 2^31 elements) while every BatchNorm
+    normalises with the whole bag's statistics.
+      * each BatchNorm's scale / shift and running mean / variance against an fp64 restatement of
+        the batch statistics of that BatchNorm's actual input (all 4096 tiles, computed here from
+        the pieces in fp64): scale = gamma / sqrt(var + eps), shift = beta - mean * scale, running
+        statistics with momentum 0.1 and the unbiased variance;
+      * the features of 4 tiles spread over the bag against the fp64 oracle forward of those tiles
+        normalised with the same whole-bag statistics (oracle/encoder_ref.py, stats_in)."""
+    import torch.nn as nn
+    from oracle.encoder_ref import BN_EPS, features
+    from transmil_deepgraft_amd import encoder as E
+    torch.backends.cudnn.allow_tf32 = False
+    enc = _encoder(torch.float32)
+    sd0 = {k: v.clone() for k, v in enc.state_dict().items()}
+    enc = enc.cuda().train()
+    assert E.train_pieces(C5_TILES, enc.chunk) == 512
+    names = {id(m): n for n, m in enc.named_modules() if isinstance(m, nn.BatchNorm2d)}
+    rec = {}
+    orig = E._bn_train_stats
+
+    def spy(ys, bn, ws):
+        assert all(y.numel() <= E.LIB_MAX_ELEMS for y in ys)
+        C = ys[0].shape[1]
+        n = sum(y.numel() // C for y in ys)
+        mean = sum(y.double().sum(dim=(0, 2, 3)) for y in ys) / n
+        var = sum(((y.double() - mean.view(1, C, 1, 1)) ** 2).sum(dim=(0, 2, 3)) for y in ys) / n
+        rm0, rv0 = bn.running_mean.double().clone(), bn.running_var.double().clone()
+        st = orig(ys, bn, ws)
+        rec[names[id(bn)]] = dict(mean=mean, var=var, st=st.double().clone(), rm0=rm0, rv0=rv0,
+                                  rm1=bn.running_mean.double().clone(), rv1=bn.running_var.double().clone(), n=n,
+                                  g=bn.weight.double(), b=bn.bias.double())
+        return st
+
+    monkeypatch.setattr(E, "_bn_train_stats", spy)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    tiles = torch.randn(C5_TILES, 3, 224, 224, device="cuda", generator=g)
+    with torch.no_grad():
+        feats = enc(tiles)
+    torch.cuda.synchronize()
+    assert len(rec) == 53 and torch.isfinite(feats).all()
+    worst = {}
+    for name, r in rec.items():
+        assert r["n"] > 1 and r["n"] % C5_TILES == 0
+        scale = r["g"] / torch.sqrt(r["var"] + BN_EPS)
+        shift = r["b"] - r["mean"] * scale
+        rm = 0.9 * r["rm0"] + 0.1 * r["mean"]
+        rv = 0.9 * r["rv0"] + 0.1 * r["var"] * r["n"] / (r["n"] - 1)
+        errs = [((r["st"][0] - scale).abs().max() / scale.abs().max()).item(),
+                ((r["st"][1] - shift).abs().max() / shift.abs().max().clamp_min(1e-6)).item(),
+                ((r["rm1"] - rm).abs().max() / rm.abs().max().clamp_min(1e-6)).item(),
+                ((r["rv1"] - rv).abs().max() / rv.abs().max()).item()]
+        worst[name] = max(errs)
+    bad = {k: v for k, v in worst.items() if v > 1e-4}
+    assert not bad, bad
+    idx = torch.tensor([0, 1365, 2731, 4095])
+    stats = {name: (r["mean"], r["var"]) for name, r in rec.items()}
+    ref = features(tiles[idx.cuda()].cpu(), sd0, train=True, stats_in=stats)
+    got = feats[idx.cuda()].double().cpu()
+    err = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert err < 2e-3, err

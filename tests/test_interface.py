@@ -428,6 +428,56 @@ def test_grad_allreduce_param_unused_on_one_rank():
         assert res[r][2] is None
 
 
+def _mixed_path_worker(rank, world, port, out):
+    """Step 1: rank 0 is on the fused path (its gradients already ARE the bucket's views, as the
+    fused backward leaves them; its early part-0 reduce issued from the backward hook), rank 1 on
+    the module path with parameter 2 unused.  Step 2: the roles swap."""
+    import torch.distributed as dist
+    from transmil_deepgraft_amd.interface import GradAllReduce
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ps = [torch.nn.Parameter(torch.ones(5)) for _ in range(4)]
+
+    class Model:      # two bucket parts, like TransMIL.grad_bucket_parts
+        def grad_bucket_parts(self):
+            return [ps[:2], ps[2:]]
+
+    ar = GradAllReduce(ps, model=Model())
+    res = []
+    for step in range(2):
+        fused = rank == step
+        for i, p in enumerate(ps):
+            p.grad = None if (not fused and i == 2) else torch.full((5,), float(10 * step + 4 * rank + i))
+        if fused:
+            ar.bucket.bind()             # the fused backward writes straight into the views
+            ar.bucket.ready(0)           # and the hook issues part 0 before layer1's backward
+        ar()
+        res.append([None if p.grad is None else p.grad.clone() for p in ps])
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_ranks_on_different_paths():
+    """One rank on the fused path (bucket-owned gradients, early hook reduce), the other on the
+    module-by-module path with an unused parameter: no mismatched collective (the has-gradient
+    flags ride in the bucket's own all_reduce), every rank ends with the averaged gradient and the
+    module-path rank adopts it for the parameter it did not use (find_unused_parameters)."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    with mp.Manager() as mgr:
+        out = mgr.dict()
+        mp.spawn(_mixed_path_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    for step in range(2):
+        fused_rank = step
+        for i in range(4):
+            vals = [10 * step + 4 * r + i for r in range(2) if not (r != fused_rank and i == 2)]
+            expect = torch.full((5,), sum(vals) / 2.0)
+            for r in range(2):
+                torch.testing.assert_close(res[r][step][i], expect)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("train", [False, True])
 def test_fused_head_backward_equals_two_launch_path(train):
@@ -452,6 +502,67 @@ def test_fused_head_backward_equals_two_launch_path(train):
     bad = [n for n in grads[0] if not torch.equal(grads[0][n], grads[1][n])]
     assert not bad, bad
     assert all(torch.isfinite(v).all() for v in grads[0].values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [1, 3])
+def test_graphed_optimization_step_follows_lr_changes(K):
+    """An LR schedule acting on a graph-replayed step (configure_optimizers' ReduceLROnPlateau halves
+    lr; code/models/model_interface.py:862-877): lr halved in every group between two replayed steps
+    leaves the parameters bitwise equal to the eager optimization_step with the same change, and the
+    groups' lookahead_step counters equal the eager ones (the capture itself does not advance them)."""
+    from transmil_deepgraft_amd.interface import GradAllReduce, GraphedOptimizationStep, TransMILTask
+    from transmil_deepgraft_amd.models import TransMIL
+
+    def build():
+        torch.manual_seed(12)
+        m = TransMIL(2, 512, 512).cuda().train().set_compute_dtype(torch.bfloat16)
+        task = TransMILTask(m, accumulate_grad_batches=K)
+        return m, task, task.configure_optimizers()[0][0], GradAllReduce(m.parameters(), model=m)
+
+    g = torch.Generator(device="cuda").manual_seed(6)
+    bags = [torch.rand(1, 300, 512, device="cuda", generator=g) for _ in range(2)]
+    labels = [torch.tensor([j % 2], device="cuda") for j in range(2)]
+    n = 6 * K
+    change = {3 * K: 0.5, 5 * K: 0.25}          # micro-batch index -> lr multiplier applied before it
+
+    def run(step, opt):
+        out = []
+        for i in range(n):
+            if i in change:
+                for grp in opt.param_groups:
+                    grp["lr"] = 2e-4 * change[i]
+            out.append(step((bags[i % 2], labels[i % 2], None)).clone())
+        return out
+
+    ma, ta, oa, ara = build()
+    gstep = GraphedOptimizationStep(ta, oa, ara)
+    la = run(gstep, oa)
+    assert gstep.graphs is not None
+    mb, tb, ob, arb = build()
+    lb = run(lambda b: tb.optimization_step(b, ob, allreduce=arb), ob)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(la, lb))
+    pa, pb = dict(ma.named_parameters()), dict(mb.named_parameters())
+    bad = [k for k in pa if not torch.equal(pa[k], pb[k])]
+    assert not bad, bad
+    assert [grp["lookahead_step"] for grp in oa.param_groups] == [grp["lookahead_step"] for grp in ob.param_groups]
+    assert oa.param_groups[0]["lookahead_step"] == n // K
+
+
+def test_graphed_step_refuses_lr_change_it_cannot_replay():
+    """A non-fused optimizer bakes lr into the captured graph: a change after the capture raises
+    (the replayed graph would silently keep the old value)."""
+    from types import SimpleNamespace
+    from transmil_deepgraft_amd.interface import GraphedOptimizationStep
+    w = torch.nn.Parameter(torch.zeros(3))
+    opt = torch.optim.SGD([w], lr=0.1)
+    gs = GraphedOptimizationStep(SimpleNamespace(accumulate_grad_batches=1), opt)
+    gs._fingerprint = gs._hyper_fingerprint()
+    gs._before_step_replay()                  # unchanged: fine
+    opt.param_groups[0]["lr"] = 0.05
+    with pytest.raises(RuntimeError, match="lr / weight_decay changed"):
+        gs._before_step_replay()
 
 
 @pytest.mark.gpu

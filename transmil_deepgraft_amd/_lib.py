@@ -51,7 +51,7 @@ class OptimTensor(C.Structure):
 
 class OptimTable(C.Structure):
     _fields_ = [("count", I), ("reserved", I), ("offset", L * (OPTIM_MAX_TENSORS + 1)),
-                ("t", OptimTensor * OPTIM_MAX_TENSORS)]
+                ("t", OptimTensor * OPTIM_MAX_TENSORS), ("hyper", P)]
 
 
 CAST_MAX = 8
@@ -131,7 +131,9 @@ _SIGS = {
     "tm_dropout_bwd_pad": (I, [I, P, I, I, I, I, I, Fl, U64, P, P, P]),
     "tm_add_relu": (I, [I, P, P, P, L, P]),
     "tm_bias_act": (I, [I, P, P, L, I, I, P]),
-    "tm_conv1x1": (I, [I, P, P, P, P, P, L, I, I, I, P]),
+    "tm_conv1x1_workspace_bytes": (L, []),
+    "tm_conv1x1": (I, [I, P, P, P, P, P, L, I, I, I, P, L, P]),
+    "tm_conv1x1_tune": (I, [I, P, P, P, P, P, L, I, I, I, P, L, P]),
     "tm_bn_train_workspace": (L, [I]),
     "tm_bn_train_stats": (I, [I, P, P, I, I, P, P, P, P, Fl, Fl, P, P, P, L, P]),
     "tm_bn_apply": (I, [I, P, P, P, P, P, P, L, I, I, P]),

@@ -23,6 +23,8 @@
 // updates 4 consecutive elements with 16-B loads / stores; tensors whose param / grad pointers
 // are not 16-B aligned fall back to element-wise access.
 // HBM traffic per element: p, m, v read+write, g read = 28 B (+8 B slow on sync steps).
+// lr / weight decay per tensor come from the table, or from the device array tab.hyper when set (an
+// LR scheduler then acts on a captured, replayed step).
 #include "../../include/transmil_hip.h"
 #include "common.h"
 
@@ -82,7 +84,9 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
     for (int t = ti; t < tab.count && tab.offset[t] < wbase + 256; ++t) {  // wave-uniform t
       if (i0[u] >= tab.offset[t] && i0[u] < tab.offset[t + 1]) {
         const tm_optim_tensor& T = tab.t[t];
-        pc[u].param = T.param; grad = T.grad; pc[u].lr = T.lr; pc[u].wd = T.weight_decay;
+        pc[u].param = T.param; grad = T.grad;
+        pc[u].lr = tab.hyper ? tab.hyper[2 * t] : T.lr;
+        pc[u].wd = tab.hyper ? tab.hyper[2 * t + 1] : T.weight_decay;
         pc[u].j0 = i0[u] - tab.offset[t];
         pc[u].n = (int)min(4LL, T.numel - pc[u].j0);   // the tensor's padding tail: n < 4 (or <= 0)
       }

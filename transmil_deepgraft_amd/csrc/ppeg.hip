@@ -297,6 +297,9 @@ static int wgrad_groups(int G) {
 extern "C" int tm_ppeg_fwd(const float* x, int B, int G, int D, const float* wfold, const float* bfold, float* y,
                            void* stream) {
   TM_REQUIRE(x && y && x != y && D % CW == 0 && G > 0 && B > 0, "ppeg_fwd: bad args");
+  // the tile kernels address one bag's grid through a buffer resource with 32-bit byte counts /
+  // offsets: beyond 4 GiB per bag the hardware bounds check would turn loads into silent zeros
+  TM_REQUIRE((1LL + (long long)G * G) * D * 4 < (1LL << 32), "ppeg_fwd: (1+G*G)*D*4 must be < 2^32 bytes per bag");
   const int ntiles = ((G + TR - 1) / TR) * ((G + TC - 1) / TC);
   ppeg_stencil_kernel<false><<<dim3(ntiles * (D / CW), B), 256, ST_LDS, (hipStream_t)stream>>>(
       x, 1 + G * G, G, D, wfold, bfold, y, DropPad{});
@@ -314,6 +317,7 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
                            int dtype, void* dout, int n_pad, int pad, float p, uint64_t seed,
                            const uint64_t* seed_ptr, tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(x && dy && dx && dx != dy && D % CW == 0 && G > 0 && B > 0, "ppeg_bwd: bad args");
+  TM_REQUIRE((1LL + (long long)G * G) * D * 4 < (1LL << 32), "ppeg_bwd: (1+G*G)*D*4 must be < 2^32 bytes per bag");
   TM_REQUIRE(!dout || ((dtype == TM_BF16 || dtype == TM_F32) && n_pad >= pad + 1 + G * G && pad >= 0),
              "ppeg_bwd: bad dropout-pad output");
   hipStream_t st = (hipStream_t)stream;

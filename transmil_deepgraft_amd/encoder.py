@@ -23,9 +23,12 @@ Same module / parameter / buffer names as code/models/ResNet.py (ResNet :130-277
   run as written;
 * in eval mode tiles go through in chunks (``chunk`` tiles, default 512; per-tile math, so the
   chunking is exact) so the activation peak stays a few GB whatever the bag size; in train mode
-  the bag is held as pieces of ``chunk`` tiles while every BatchNorm's statistics span the whole
-  batch (tens of GB for a 4096-tile bag, well inside one GPU's HBM); the [B*bag, 2048] features
-  stay on the device for the fused TransMIL engine (no host round trip).
+  the bag is held as pieces of ``train_pieces(N, chunk)`` tiles while every BatchNorm's statistics
+  span the whole batch (tens of GB for a 4096-tile bag, well inside one GPU's HBM); the
+  [B*bag, 2048] features stay on the device for the fused TransMIL engine (no host round trip);
+* no library kernel is ever handed a tensor of 2^31 or more elements (``_lib_guard``; a whole
+  4096-tile bag is 3.3 G elements at the stem output): every path runs on pieces of at most
+  ``max_tiles_per_call()`` tiles or refuses the call.
 """
 from __future__ import annotations
 
@@ -88,9 +91,35 @@ def _conv1x1_gemm(x, w, b, relu, residual=None):
     if residual is not None and (residual.shape != y.shape or residual.dtype != y.dtype or
                                  not residual.is_contiguous(memory_format=cl)):
         raise RuntimeError("conv1x1: channels-last residual of the output's shape and dtype expected")
-    _lib.call("tm_conv1x1", _dtype_code(x), _p(x), _p(w.contiguous()), _p(b), _p(residual) if residual is not None else None,
-              _p(y), n * h * wd, c, cout, int(relu), _stream())
+    # stream-ordered scratch from the caching allocator (no library-global workspace)
+    ws_bytes = _conv1x1_ws_bytes()
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
+    args = (_dtype_code(x), _p(x), _p(w.contiguous()), _p(b), _p(residual) if residual is not None else None,
+            _p(y), n * h * wd, c, cout, int(relu), _p(ws), ws_bytes, _stream())
+    key = (x.device.index, x.dtype, n * h * wd, c, cout, bool(relu), b is not None, residual is not None)
+    if key not in _TUNED and _tuning_enabled() and not torch.cuda.is_current_stream_capturing():
+        # first call of a shape, outside capture: time hipBLASLt's candidates once (the ABI's one
+        # synchronising entry point, tm_conv1x1_tune); y is then written by the real call below
+        _lib.call("tm_conv1x1_tune", *args)
+        _TUNED.add(key)
+    _lib.call("tm_conv1x1", *args)
     return y
+
+
+_TUNED = set()
+_WS = []
+
+
+def _conv1x1_ws_bytes():
+    if not _WS:
+        from . import _lib
+        _WS.append(_lib.query("tm_conv1x1_workspace_bytes"))
+    return _WS[0]
+
+
+def _tuning_enabled():
+    import os
+    return os.environ.get("TM_CONV1X1_TUNE", "1") != "0"
 
 
 def _bias_act_(y, b, relu=True):
@@ -149,6 +178,69 @@ def _bn_apply_(y, st, residual=None, rst=None, relu=True):
 
 def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
+
+
+# Every library kernel of the encoder (MIOpen / CK convolutions, PyTorch pooling, hipBLASLt) is
+# handed tensors of at most 2^31 - 1 elements.  A whole 4096-tile bag is 3.3 G elements at the stem
+# and layer1 outputs; run in one piece (round 4, train mode) it ended in an illegal-address fault
+# inside the library path ("C5 encoder"), and an fp32 one-pass eval differed
+# from the piecewise run.  The bag is therefore always held in pieces of at most
+# max_tiles_per_call() tiles, and _lib_guard refuses anything larger before it reaches a library.
+LIB_MAX_ELEMS = 2 ** 31 - 1
+
+
+def tile_elems_max(h=224, w=224):
+    """The largest activation one h x w tile produces in RetCCL ResNet-50 (elements): the input, the
+    stem output (64 x ceil(h/2) x ceil(w/2)) or layer1's output (256 x ceil(h/4) x ceil(w/4))."""
+    h2, w2 = (h + 1) // 2, (w + 1) // 2
+    h4, w4 = (h2 + 1) // 2, (w2 + 1) // 2
+    return max(3 * h * w, 64 * h2 * w2, 256 * h4 * w4)
+
+
+def max_tiles_per_call(h=224, w=224):
+    """Tiles per library call that keep every activation under LIB_MAX_ELEMS (2674 at 224 x 224)."""
+    return max(1, LIB_MAX_ELEMS // tile_elems_max(h, w))
+
+
+def _lib_guard(*ts):
+    for t in ts:
+        if t is not None and t.numel() > LIB_MAX_ELEMS:
+            raise RuntimeError(f"encoder: a library call on {t.numel()} elements (shape {tuple(t.shape)}) exceeds "
+                               f"2^31 - 1; the bag must be held in pieces of <= max_tiles_per_call() tiles")
+
+
+def _conv_out_numel(x, w, stride, padding):
+    n, _, h, wd = x.shape
+    k = w.shape[2]
+    ho = (h + 2 * padding - k) // stride + 1
+    wo = (wd + 2 * padding - k) // stride + 1
+    return n * w.shape[0] * ho * wo
+
+
+def _lib_conv2d(x, w, b=None, stride=1, padding=0):
+    """F.conv2d (MIOpen / CK) with input and output sizes checked against LIB_MAX_ELEMS first."""
+    _lib_guard(x)
+    if _conv_out_numel(x, w, stride, padding) > LIB_MAX_ELEMS:
+        raise RuntimeError(f"encoder: convolution output of {_conv_out_numel(x, w, stride, padding)} elements "
+                           f"exceeds 2^31 - 1; hold the bag in pieces of <= max_tiles_per_call() tiles")
+    return F.conv2d(x, w, b, stride=stride, padding=padding)
+
+
+def _lib_max_pool(x):
+    _lib_guard(x)
+    return F.max_pool2d(x, 3, 2, 1)
+
+
+def train_pieces(n_tiles, chunk, h=224, w=224, max_pieces=64):
+    """Piece size of the train-mode bag: at least ``chunk`` tiles, enough that the statistics call
+    combines at most ``max_pieces`` pieces (tm_bn_train_stats), never more than
+    max_tiles_per_call(h, w).  Raises when no piece size satisfies both."""
+    cap = max_tiles_per_call(h, w)
+    size = min(max(chunk, -(-n_tiles // max_pieces)), cap)
+    if -(-n_tiles // size) > max_pieces:
+        raise RuntimeError(f"encoder: a {n_tiles}-tile train-mode bag needs more than {max_pieces} pieces of "
+                           f"<= {cap} tiles (tm_bn_train_stats combines at most {max_pieces})")
+    return size
 
 
 class RetCCLResNet50(nn.Module):
@@ -238,10 +330,10 @@ class RetCCLResNet50(nn.Module):
         f = self._folded
         w, b = f["stem"]
         if self.channels_last and x.is_cuda:
-            x = F.max_pool2d(_bias_act_(F.conv2d(x, w, None, stride=2, padding=3), b), 3, 2, 1)
+            x = _lib_max_pool(_bias_act_(_lib_conv2d(x, w, None, stride=2, padding=3), b))
             for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
                 y = _conv1x1_gemm(x, w1, b1, True)
-                y = _bias_act_(F.conv2d(y, w2, None, stride=s2, padding=1), b2)
+                y = _bias_act_(_lib_conv2d(y, w2, None, stride=s2, padding=1), b2)
                 if d is None:
                     idt = x
                 else:
@@ -250,19 +342,19 @@ class RetCCLResNet50(nn.Module):
                     idt = _conv1x1_gemm(xs, d[0], d[1], False)
                 x = _conv1x1_gemm(y, w3, b3, True, residual=idt)
             return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
-        x = F.max_pool2d(F.relu(F.conv2d(x, w, b, stride=2, padding=3)), 3, 2, 1)
+        x = _lib_max_pool(F.relu(_lib_conv2d(x, w, b, stride=2, padding=3)))
         for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
-            y = F.relu(F.conv2d(x, w1, b1))
-            y = F.relu(F.conv2d(y, w2, b2, stride=s2, padding=1))
-            y = F.conv2d(y, w3, b3)
-            idt = x if d is None else F.conv2d(x, d[0], d[1], stride=d[2])
+            y = F.relu(_lib_conv2d(x, w1, b1))
+            y = F.relu(_lib_conv2d(y, w2, b2, stride=s2, padding=1))
+            y = _lib_conv2d(y, w3, b3)
+            idt = x if d is None else _lib_conv2d(x, d[0], d[1], stride=d[2][0])
             x = F.relu(y + idt)
         return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
 
     def _forward_train_fused(self, x):
         """Train mode (batch-statistics BatchNorm, frozen parameters, no autograd) on the GPU.
-        The bag is held as pieces of ``chunk`` tiles (every convolution / pooling runs at the
-        piece size the eval path uses) while each BatchNorm's statistics span all pieces
+        The bag is held as pieces of ``train_pieces(N, chunk)`` tiles (every convolution / pooling
+        on one piece, < 2^31 elements) while each BatchNorm's statistics span all pieces
         (tm_bn_train_stats).  Convolutions without bias (1x1: hipBLASLt GEMM; 3x3 / stem: MIOpen),
         each BatchNorm one statistics pass + one apply pass fused with its ReLU, and bn3 + (BN'd
         downsample) identity + ReLU one pass (tm_bn_apply)."""
@@ -273,16 +365,17 @@ class RetCCLResNet50(nn.Module):
             self._cast_key = key
         w = self._cast
         ws = torch.empty(self._bn_ws_floats(), dtype=torch.float32, device=x.device)
-        xs = [_cl(F.conv2d(x[i:i + self.chunk], w["conv1.weight"], None, stride=2, padding=3))
-              for i in range(0, x.shape[0], self.chunk)]
+        piece = train_pieces(x.shape[0], self.chunk, x.shape[2], x.shape[3])
+        xs = [_cl(_lib_conv2d(x[i:i + piece], w["conv1.weight"], None, stride=2, padding=3))
+              for i in range(0, x.shape[0], piece)]
         st = _bn_train_stats(xs, self.bn1, ws)
-        xs = [F.max_pool2d(_bn_apply_(p, st), 3, 2, 1) for p in xs]
+        xs = [_lib_max_pool(_bn_apply_(p, st)) for p in xs]
         for si, stage in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
             for bi, blk in enumerate(stage):
                 pre = f"layer{si}.{bi}."
                 ys = [_conv1x1_gemm(p, w[pre + "conv1.weight"], None, False) for p in xs]
                 st = _bn_train_stats(ys, blk.bn1, ws)
-                ys = [_cl(F.conv2d(_bn_apply_(y, st), w[pre + "conv2.weight"], None, stride=blk.stride, padding=1))
+                ys = [_cl(_lib_conv2d(_bn_apply_(y, st), w[pre + "conv2.weight"], None, stride=blk.stride, padding=1))
                       for y in ys]
                 st = _bn_train_stats(ys, blk.bn2, ws)
                 ys = [_conv1x1_gemm(_bn_apply_(y, st), w[pre + "conv3.weight"], None, False) for y in ys]
@@ -326,10 +419,18 @@ class RetCCLResNet50(nn.Module):
             self.to(memory_format=torch.channels_last)
         grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         # train-mode BatchNorm normalises with the statistics of the whole [B*bag] batch the
-        # reference feeds model_ft in one call (model_interface.py:303-309): no chunking there
-        # (a 4096-tile bag's activations are tens of GB, well inside one GPU's HBM)
-        chunk = x.shape[0] if self.training else self.chunk
+        # reference feeds model_ft in one call (model_interface.py:303-309): the fused train path
+        # holds the bag in pieces whose statistics are combined; eval chunks are per-tile exact.
+        # No library call sees more than LIB_MAX_ELEMS elements on any path.
+        cap = max_tiles_per_call(x.shape[2], x.shape[3])
+        chunk = x.shape[0] if self.training else max(1, min(self.chunk, cap))
         fused_train = self.training and not grad and self.channels_last
+        if self.training and not fused_train and x.shape[0] > cap:
+            # nn.BatchNorm2d needs the whole batch in one module call; above the cap that call
+            # would hand the library > 2^31-element tensors
+            raise RuntimeError(f"encoder: train mode with autograd (or without channels-last) takes at most {cap} "
+                               f"tiles per call (the whole-batch BatchNorm would exceed 2^31 elements); got "
+                               f"{x.shape[0]}")
         autocast = self.training and not fused_train and dt == torch.bfloat16
         with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
             for s in range(0, x.shape[0], chunk):

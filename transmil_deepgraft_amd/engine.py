@@ -440,11 +440,11 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         # A1 product backward: dq (complete), dkl, dY
         qpw = 256 if n % 256 == 0 else 32
         work = pool(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, qpw) // 4)
-        with probe("a1_bwd"):
-            with defer_reductions():     # its dk~ and dY slab sums as one launch
+        with defer_reductions():     # its dk~ and dY slab sums as one launch
+            with probe("a1_bwd"):
                 _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t),
                           _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, _rq(), st)
-            flush_reductions()
+        flush_reductions()
     # Y = Z W
     dz = pool(mat).view(nbh, NL, NL)
     dw = pool(nbh * NL * DH).view(nbh, NL, DH)
@@ -534,8 +534,9 @@ def translayer_forward(H, geo: Geometry, prm, tdtype, dt_code, pool, drop_p, see
         _lib.call("tm_cls_out_fwd", dt_code, _p(merged), _p(prm["wo"]), _p(prm["bo"]), _p(H), B, n, pad, S, D,
                   C.c_float(drop_p), C.c_uint64(seed), _p(seed_dev), _p(Hout), st)
     else:
-        gemm(merged, prm["wo"], Hout, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=dt_code, c_dtype=F32,
-             bias=prm["bo"], drop_p=drop_p, seed=seed, seed_ptr=seed_dev, resid=H, rowmap=(n, pad, S, 0, 0, 0))
+        with probe("out_gemm"):
+            gemm(merged, prm["wo"], Hout, B * n, D, D, lda=D, ldb=D, ldc=D, dtype=dt_code, c_dtype=F32,
+                 bias=prm["bo"], drop_p=drop_p, seed=seed, seed_ptr=seed_dev, resid=H, rowmap=(n, pad, S, 0, 0, 0))
     saved = dict(xn=xn, mean=mean, rstd=rstd, qkv=qkv, merged=merged, core=state, seed=seed, seed_dev=seed_dev,
                  drop_p=drop_p, cls_only=cls_only)
     return Hout, saved
@@ -566,20 +567,22 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
             _lib.call("tm_dropout_bwd_pad", dt_code, _p(dH), B, S, n, pad, D, C.c_float(saved["drop_p"]),
                       C.c_uint64(saved["seed"]), _p(saved["seed_dev"]), _p(dout), st)
         # to_out: dWo = dout^T merged ; dbo = colsum(dout) ; dmerged = dout Wo
-        with defer_reductions():
+        with defer_reductions(), probe("wgrad_out"):
             weight_grad(dout, saved["merged"], grads["wo"], D, D, B * n, ldy=D, ldx=D, dtype=dt_code,
                         work_pool=pool, bias_out=grads["bo"])
         dmerged = pool(B * n * D, tdtype).view(B, n, D)
-        gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
+        with probe("dmerged_gemm"):
+            gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     dqkv = nystrom_core_backward(dmerged, saved["merged"], saved["qkv"], saved["core"], geo, prm["wconv"],
                                  tdtype, dt_code, pool, grads["wconv"], DH ** -0.5,
                                  cls_row=pad if saved["cls_only"] else None)
     # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
-    with defer_reductions():
+    with defer_reductions(), probe("wgrad_qkv"):
         weight_grad(dqkv, saved["xn"], grads["wqkv"], 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
                     work_pool=pool)
     dxn = pool(B * n * D, tdtype).view(B, n, D)
-    gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
+    with probe("dxn_gemm"):
+        gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
     # LayerNorm backward, accumulated into dH (residual branch already there)
     rpb = 8     # 2 rows per wave, both requested up front (the partials go through the deferred reduce)
     with defer_reductions():
@@ -763,8 +766,9 @@ class TransMILEngine:
                 H0v[:, N + 1:].copy_(xe[:, :geo.add])
         else:
             pre = pool(B * N * D).view(B * N, D)   # fp32 pre-activation for the GELU backward
-            gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
-                 bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
+            with probe("fc1_gemm"):
+                gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
+                     bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
         H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0], seed_dev)
         H2 = pool(B * geo.S * D).view(B * geo.S, D)
         with probe("ppeg_fwd"):
@@ -884,7 +888,7 @@ class TransMILEngine:
                   _p(g["cls_token"]), st)
         main, inner = self.fc1["main"], ctx["inner"]
         Fx = F if inner is None else prm["w0"].shape[0]
-        with defer_reductions():
+        with defer_reductions(), probe("wgrad_fc1"):
             weight_grad(dpre, ctx["xt"], g[main + ".weight"], D, Fx, B * N, ldy=D, ldx=Fx, dtype=self.dt_code,
                         work_pool=pool, bias_out=g[main + ".bias"])
         if inner is not None:

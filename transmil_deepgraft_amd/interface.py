@@ -134,9 +134,10 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
     moments and slow weights of every parameter live in three flat fp32 buffers, the
     step counters on the device, and the kernel reads each parameter/gradient through
     a pointer table passed by value (``tm_radam_lookahead_step``, csrc/optim.hip), so
-    the step is hipGraph-capturable.  ``lr`` / ``weight_decay`` are read per group
-    at each call (a captured graph keeps the values it was captured with, as a
-    capturable torch optimizer does)."""
+    the step is hipGraph-capturable.  ``lr`` / ``weight_decay`` reach the kernel through a
+    small device array (``tm_optim_table.hyper``) that every eager step -- and, before each
+    replay, ``GraphedOptimizationStep`` via ``refresh_hyper()`` -- rewrites from the groups, so an
+    LR scheduler (``configure_optimizers``' ReduceLROnPlateau) also acts on a replayed graph."""
 
     def __init__(self, params, lr=2e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
                  lookahead_alpha=0.5, lookahead_k=6):
@@ -177,7 +178,29 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
         self._offsets = [0]
         for p in plist:     # each tensor's flat state padded to a multiple of 4 (16-B vectors)
             self._offsets.append(self._offsets[-1] + (p.numel() + 3) // 4 * 4)
+        self._hyper = torch.zeros(len(plist), 2, dtype=torch.float32, device=dev)   # (lr, weight_decay)
+        self._hyper_host = None
         self._bind_state()
+
+    def _hyper_values(self):
+        vals = []
+        for g in self.param_groups:
+            for p in g["params"]:
+                if id(p) in self._index:
+                    vals.append((float(g["lr"]), float(g["weight_decay"])))
+        return vals
+
+    @torch.no_grad()
+    def refresh_hyper(self):
+        """Write the groups' current lr / weight_decay into the device array the update kernel reads
+        (a no-op when they have not changed).  Must run outside stream capture: a captured step
+        reads whatever the array holds when it is replayed."""
+        if self._params is None:
+            return
+        vals = self._hyper_values()
+        if vals != self._hyper_host:
+            self._hyper.copy_(torch.tensor(vals, dtype=torch.float32))
+            self._hyper_host = vals
 
     def _bind_state(self):
         for i, p in enumerate(self._params):
@@ -195,7 +218,10 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
         lib = self._lib
         if self._params is None:
             self._activate([p for p in self._all if p.grad is not None])
+        if not torch.cuda.is_current_stream_capturing():
+            self.refresh_hyper()
         tab = lib.OptimTable()
+        tab.hyper = self._hyper.data_ptr()
         tab.count = len(self._params)
         i = 0
         for g in self.param_groups:
@@ -242,6 +268,7 @@ class FusedRAdamLookahead(torch.optim.Optimizer):
                     return
                 self._activate(stateful)
             self._bind_state()
+            self._hyper_host = None
             for i, p in enumerate(self._params):
                 st = loaded.get(p, {})
                 a, b = self._offsets[i], self._offsets[i] + p.numel()
@@ -311,13 +338,21 @@ class GradBucket:
         self._off = {}
         self.ranges = []
         off = 0
-        for part in self.parts_params:
+        for i, part in enumerate(self.parts_params):
             start = off
             for p in part:
                 self._off[id(p)] = (off, p.numel())
                 off += (p.numel() + 15) // 16 * 16     # every view 64-B aligned (vector stores)
+            if i == len(self.parts_params) - 1:
+                # the has-gradient flags (one float per parameter) ride at the end of the last part, so
+                # the unused-parameter exchange is part of that part's all_reduce (no collective of its own)
+                self._flag_off = off
+                off += (len(self.params) + 15) // 16 * 16
             self.ranges.append((start, off))
         self.flat = torch.zeros(off, dtype=torch.float32, device=dev)
+        # > 0 on every rank that has not written them: averaging keeps them > 0 (see GradAllReduce)
+        self.flags = self.flat[self._flag_off:self._flag_off + len(self.params)]
+        self.flags.fill_(1.0)
         self.hooks = []
 
     def view(self, p):
@@ -361,8 +396,9 @@ class GradAllReduce:
 
     Replaces the Lightning DDP reducer (``strategy='ddp_find_unused_parameters_true'``,
     code/train.py:184).  On the fused path every TransMIL parameter receives a gradient each step,
-    so no unused-parameter search runs; on the module-by-module path a has-gradient mask is
-    all-reduced first and parameters used on another rank adopt the averaged gradient.  With ``model=`` (a TransMIL with
+    so no unused-parameter search runs; on the module-by-module path the rank's has-gradient flags
+    travel in the bucket's own all_reduce (a tail of the last part) and parameters used on another
+    rank adopt the averaged gradient.  With ``model=`` (a TransMIL with
     ``grad_bucket_parts``) the bucket has two parts: part 0 (head, norm, layer2, PPEG; 4.4 MB
     fp32) is final before layer1's backward is enqueued and, with ``overlap``, its RCCL
     all_reduce is issued right then on RCCL's stream, overlapping layer1 + _fc1 backward on
@@ -410,18 +446,16 @@ class GradAllReduce:
             self._works.clear()
             return
         owned = all(self.bucket.owns(p) for p in self.params if p.grad is not None)
-        adopt = []
+        local = None
         if not owned:
-            # gradients produced outside the fused backward (module-by-module path): bind them.
-            # As DDP's find_unused_parameters: a parameter without a gradient HERE but with one on
-            # another rank receives the averaged gradient (its zeroed slice summed with theirs), so
-            # the ranks' optimizer steps stay identical; one used on no rank keeps grad None.
-            self._works.clear()
+            # gradients produced outside the fused backward (module-by-module path): bind them, and
+            # write this rank's has-gradient flags into the bucket's flag tail.  Every rank issues
+            # the same all_reduces in the same order whichever path it took (the fused path's early
+            # part-0 reduce from the backward hook included), so ranks on different paths cannot
+            # mismatch collectives; the flags are summed with the gradients.
             local = [p.grad is not None for p in self.params]
             self.bucket.bind()
-            used = torch.tensor(local, dtype=torch.int32, device=self.flat.device)
-            dist.all_reduce(used, op=dist.ReduceOp.MAX, group=self.group)
-            adopt = [p for p, here, anywhere in zip(self.params, local, used.tolist()) if anywhere and not here]
+            self.bucket.flags.copy_(torch.tensor(local, dtype=torch.float32))
         for i in range(len(self.bucket.ranges)):
             if i not in self._works:
                 self._works[i] = dist.all_reduce(self.bucket.part(i), op=dist.ReduceOp.SUM, group=self.group,
@@ -430,8 +464,16 @@ class GradAllReduce:
             self._works[i].wait()       # the compute stream waits on RCCL's stream
         self._works.clear()
         self.flat.mul_(1.0 / self._world())
-        for p in adopt:
-            p.grad = self.bucket.view(p)
+        if local is not None:
+            # as DDP's find_unused_parameters: a parameter without a gradient HERE but with one on
+            # another rank receives the averaged gradient (its zeroed slice summed with theirs), so
+            # the ranks' optimizer steps stay identical; one used on no rank keeps grad None.  A rank
+            # on the fused path never writes its flags: they stay > 0 (1 at creation, then averages
+            # of positive and non-negative values), i.e. "used".  (Host read: module path only.)
+            used = (self.bucket.flags > 0).tolist()
+            for p, here, anywhere in zip(self.params, local, used):
+                if anywhere and not here:
+                    p.grad = self.bucket.view(p)
 
 
 class _CrossEntropyOneHot(torch.autograd.Function):
@@ -576,7 +618,13 @@ class GraphedOptimizationStep:
 
     One bag shape per instance (the reference's loaders sample bags to a fixed size); a batch of
     another shape raises.  Returns the training_step loss tensor of the replayed graph (a static
-    buffer: it is overwritten by the next call of the same phase)."""
+    buffer: it is overwritten by the next call of the same phase).
+
+    Learning rate / weight decay: with ``FusedRAdamLookahead`` the replayed update reads them from
+    a device array refreshed from the param groups before every replayed optimizer step, so an LR
+    scheduler keeps working; any other optimizer bakes the captured values into the graph, and a
+    change of a group's lr / weight_decay after the capture raises instead of being ignored.
+    ``lookahead_step`` of every group advances per replayed optimizer step as in the eager path."""
 
     def __init__(self, task: "TransMILTask", opt, allreduce=None):
         self.task, self.opt, self.allreduce = task, opt, allreduce
@@ -605,6 +653,8 @@ class GraphedOptimizationStep:
                 opt.step()
             return loss
 
+        self._fingerprint = self._hyper_fingerprint()
+        la_steps = [g.get("lookahead_step") for g in opt.param_groups]   # capture runs opt.step()'s host side
         pool = torch.cuda.graph_pool_handle()
         self.graphs = {}
         opt.zero_grad(set_to_none=True)        # the first capture takes the writing (=) path,
@@ -613,6 +663,28 @@ class GraphedOptimizationStep:
             with torch.cuda.graph(g, pool=pool):
                 self.loss[ph] = body(ph)
             self.graphs[ph] = g
+        for grp, v in zip(opt.param_groups, la_steps):     # ... without a step having run
+            if v is not None:
+                grp["lookahead_step"] = v
+
+    def _hyper_fingerprint(self):
+        return [(g.get("lr"), g.get("weight_decay")) for g in self.opt.param_groups]
+
+    def _before_step_replay(self):
+        """The host side of opt.step() that a replay does not run: the fused optimizer's device
+        hyper-parameters, the groups' lookahead_step counters; a non-fused optimizer whose lr /
+        weight decay changed since the capture raises (its graph holds the old values)."""
+        opt = self.opt
+        refresh = getattr(opt, "refresh_hyper", None)
+        if refresh is not None:
+            refresh()
+        elif self._hyper_fingerprint() != self._fingerprint:
+            raise RuntimeError("GraphedOptimizationStep: lr / weight_decay changed after the capture, and "
+                               f"{type(opt).__name__} bakes them into the captured graph (use FusedRAdamLookahead, "
+                               "or build a new GraphedOptimizationStep)")
+        for g in opt.param_groups:
+            if "lookahead_step" in g:
+                g["lookahead_step"] += 1
 
     def __call__(self, batch):
         bags, label = batch[0], batch[1]
@@ -629,6 +701,8 @@ class GraphedOptimizationStep:
                              f"{self.shape[1]}, got {tuple(bags.shape)} / {tuple(label.shape)}")
         task._micro += 1
         ph = self._phase(task._micro)
+        if ph == "last":
+            self._before_step_replay()
         self.x.copy_(bags)
         self.y.copy_(label)
         self.graphs[ph].replay()
