@@ -186,7 +186,7 @@ SITE_LAYERS = {"ln_fwd": (1, 2), "landmarks": (1, 2), "a3_fwd": (1, 2), "a1_fwd"
                "ppeg_bwd": (0,), "conv_bwd": (1,), "a1_bwd": (1,), "a3_bwd": (2, 1)}
 
 
-def probe_sites(engine, run_step, steps, sites):
+def probe_site_times(engine, run_step, steps, sites):
     """Eager probe steps with every site in ``sites`` timed: a GPU spin queued ahead of each probed
     launch so its events bracket the kernel, the span of an empty event pair recorded just before it
     subtracted.  Returns site -> [ms per call, in call order over the steps]."""
@@ -509,7 +509,7 @@ def main():
         def probe_step(i):
             load(i)
             body()
-        per = probe_sites(engine, probe_step, 3, set(HBM_SITES) | set(GEMM_SITES))
+        per = probe_site_times(engine, probe_step, 3, set(HBM_SITES) | set(GEMM_SITES))
         hbm = hbm_roofline(per, args.n, 2 if args.dtype == "bf16" else 4)
         gemms = gemm_roofline(per, args.n) if args.dtype == "bf16" else None
 
