@@ -115,22 +115,25 @@ def test_encoder_oracle_pinned_by_reference_fixture():
     np.testing.assert_allclose(features(x, sd, torch.float32).numpy(), fx["feats"], rtol=1e-5, atol=1e-5)
 
 
-def test_library_calls_stay_below_2_31_elements():
-    """Every library convolution / pooling of the encoder is handed < 2^31 elements: the guard
-    refuses a 2675-tile stem input (its output is 2675 x 64 x 112 x 112 > 2^31 - 1) before it reaches
-    MIOpen, a 2674-tile one passes (meta tensors: shapes only, nothing is computed)."""
+def test_library_calls_stay_below_2_gib():
+    """Every library convolution / pooling of the encoder is handed < 2 GiB per tensor (MIOpen's
+    implicit-GEMM NHWC kernels wrap 32-bit offsets beyond that: scripts/dev/c5_drift.py measured
+    wrong outputs for tiles >= 2674 of a one-pass 4096-tile fp32 bag).  The guard refuses a
+    669-tile fp32 stem input (its output, 669 x 64 x 112 x 112 x 4 B, reaches 2^31 bytes) before it
+    reaches MIOpen, a 668-tile one passes; bf16 doubles the cap (meta tensors: shapes only)."""
     from transmil_deepgraft_amd import encoder as E
     assert E.tile_elems_max(224, 224) == 64 * 112 * 112
-    cap = E.max_tiles_per_call(224, 224)
-    assert cap == 2674 and cap * 64 * 112 * 112 <= 2 ** 31 - 1 < (cap + 1) * 64 * 112 * 112
-    w = torch.empty(64, 3, 7, 7, device="meta")
-    y = E._lib_conv2d(torch.empty(cap, 3, 224, 224, device="meta"), w, stride=2, padding=3)
-    assert tuple(y.shape) == (cap, 64, 112, 112)
-    with pytest.raises(RuntimeError, match="2\\^31"):
-        E._lib_conv2d(torch.empty(cap + 1, 3, 224, 224, device="meta"), w, stride=2, padding=3)
-    with pytest.raises(RuntimeError, match="2\\^31"):
-        E._lib_max_pool(torch.empty(cap + 1, 64, 112, 112, device="meta"))
-    E._lib_max_pool(torch.empty(cap, 64, 112, 112, device="meta"))
+    for dt, esz, cap_expect in ((torch.float32, 4, 668), (torch.bfloat16, 2, 1337)):
+        cap = E.max_tiles_per_call(224, 224, esz)
+        assert cap == cap_expect and cap * 64 * 112 * 112 * esz <= 2 ** 31 - 1 < (cap + 1) * 64 * 112 * 112 * esz
+        w = torch.empty(64, 3, 7, 7, device="meta", dtype=dt)
+        y = E._lib_conv2d(torch.empty(cap, 3, 224, 224, device="meta", dtype=dt), w, stride=2, padding=3)
+        assert tuple(y.shape) == (cap, 64, 112, 112)
+        with pytest.raises(RuntimeError, match="2\\^31"):
+            E._lib_conv2d(torch.empty(cap + 1, 3, 224, 224, device="meta", dtype=dt), w, stride=2, padding=3)
+        with pytest.raises(RuntimeError, match="2\\^31"):
+            E._lib_max_pool(torch.empty(cap + 1, 64, 112, 112, device="meta", dtype=dt))
+        E._lib_max_pool(torch.empty(cap, 64, 112, 112, device="meta", dtype=dt))
 
 
 def test_train_pieces_respect_the_statistics_call_and_the_library_limit():
@@ -138,14 +141,16 @@ def test_train_pieces_respect_the_statistics_call_and_the_library_limit():
     call (tm_bn_train_stats), never more than max_tiles_per_call() tiles; a bag no piece size can
     serve raises instead of failing inside the statistics call."""
     from transmil_deepgraft_amd.encoder import max_tiles_per_call, train_pieces
-    cap = max_tiles_per_call()
-    assert train_pieces(4096, 512) == 512                    # C5: 8 pieces
-    assert train_pieces(4096, 4096) == cap                   # chunk above the cap: clamped (2 pieces)
+    cap4, cap2 = max_tiles_per_call(elem_bytes=4), max_tiles_per_call(elem_bytes=2)
+    assert train_pieces(4096, 512) == 512                          # C5 fp32: 8 pieces
+    assert train_pieces(4096, 1024, elem_bytes=2) == 1024          # C5 bf16 (bench_c5): 4 pieces
+    assert train_pieces(4096, 4096) == cap4                        # chunk above the cap: clamped
+    assert train_pieces(4096, 4096, elem_bytes=2) == cap2
     assert train_pieces(6, 2) == 2
-    assert train_pieces(40000, 512) == 625                   # 64 pieces of 625 tiles
-    assert train_pieces(64 * cap, 512) == cap
+    assert train_pieces(40000, 512, elem_bytes=2) == 625           # 64 pieces of 625 tiles
+    assert train_pieces(64 * cap4, 512) == cap4
     with pytest.raises(RuntimeError, match="64 pieces"):
-        train_pieces(64 * cap + 1, 512)
+        train_pieces(64 * cap4 + 1, 512)
 
 
 C5_TILES = 4096     # BASELINE config C5: one slide of 4096 224x224 tiles
@@ -185,8 +190,10 @@ def test_c5_full_bag_4096_tiles(enc_dtype, mil_dtype, rtol, ltol, gtol):
     got = whole[idx.cuda()].double().cpu()
     err = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
     assert err < rtol, err
-    # the bag goes through in the encoder's 512-tile chunks: the same kernels as 8 separate calls
-    # (one 4096-tile MIOpen batch picks other convolution algorithms: not compared bitwise)
+    # the bag goes through in the encoder's 512-tile chunks: the same kernels as 8 separate calls.
+    # (A one-pass 4096-tile batch is refused by encoder._lib_guard: MIOpen's NHWC implicit-GEMM
+    # kernel for layer2.0's stride-2 3x3 convolution returned wrong outputs for tiles >= 2674 of it,
+    # profiles/r05_c5_drift.json -- the round-4 one-pass drift.)
     assert torch.equal(whole, chunks)
 
     # TransMIL(2, 2048) on the GPU features against the fp64 oracle on the same features
@@ -339,13 +346,13 @@ def test_c5_train_mode_bn_4096_tiles(monkeypatch):
     enc = _encoder(torch.float32)
     sd0 = {k: v.clone() for k, v in enc.state_dict().items()}
     enc = enc.cuda().train()
-    assert E.train_pieces(C5_TILES, enc.chunk) == 512
+    assert E.train_pieces(C5_TILES, enc.chunk, elem_bytes=4) == 512
     names = {id(m): n for n, m in enc.named_modules() if isinstance(m, nn.BatchNorm2d)}
     rec = {}
     orig = E._bn_train_stats
 
     def spy(ys, bn, ws):
-        assert all(y.numel() <= E.LIB_MAX_ELEMS for y in ys)
+        assert all(y.numel() * y.element_size() <= E.LIB_MAX_BYTES for y in ys)
         C = ys[0].shape[1]
         n = sum(y.numel() // C for y in ys)
         mean = sum(y.double().sum(dim=(0, 2, 3)) for y in ys) / n

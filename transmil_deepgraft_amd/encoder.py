@@ -26,8 +26,9 @@ Same module / parameter / buffer names as code/models/ResNet.py (ResNet :130-277
   the bag is held as pieces of ``train_pieces(N, chunk)`` tiles while every BatchNorm's statistics
   span the whole batch (tens of GB for a 4096-tile bag, well inside one GPU's HBM); the
   [B*bag, 2048] features stay on the device for the fused TransMIL engine (no host round trip);
-* no library kernel is ever handed a tensor of 2^31 or more elements (``_lib_guard``; a whole
-  4096-tile bag is 3.3 G elements at the stem output): every path runs on pieces of at most
+* no library kernel is ever handed a tensor of 2 GiB or more (``_lib_guard``; a whole 4096-tile
+  bag is 3.3 G elements at the stem output, and MIOpen's implicit-GEMM NHWC kernels wrap 32-bit
+  offsets there: wrong outputs measured, see LIB_MAX_BYTES): every path runs on pieces of at most
   ``max_tiles_per_call()`` tiles or refuses the call.
 """
 from __future__ import annotations
@@ -181,12 +182,18 @@ def _cl(t):
 
 
 # Every library kernel of the encoder (MIOpen / CK convolutions, PyTorch pooling, hipBLASLt) is
-# handed tensors of at most 2^31 - 1 elements.  A whole 4096-tile bag is 3.3 G elements at the stem
-# and layer1 outputs; run in one piece (round 4, train mode) it ended in an illegal-address fault
-# inside the library path ("C5 encoder"), and an fp32 one-pass eval differed
-# from the piecewise run.  The bag is therefore always held in pieces of at most
-# max_tiles_per_call() tiles, and _lib_guard refuses anything larger before it reaches a library.
-LIB_MAX_ELEMS = 2 ** 31 - 1
+# handed tensors of less than 2 GiB.  Round 5 measured why (scripts/dev/c5_drift.py,
+# profiles/r05_c5_drift.json): fed a whole 4096-tile fp32 bag, MIOpen's implicit-GEMM NHWC forward
+# kernel for layer2.0's 3x3 / stride-2 convolution (igemm_fwd_gtcx35_nhwc_fp32_..._bt128x128x16)
+# returned WRONG outputs for every tile from 2674 on (per-tile relative error up to 0.35; tiles
+# 0-2673 bit-identical to the piecewise run, every other op of the network bit-identical) -- a
+# 32-bit offset wrapping where 2 x the input's elements (= its bf16 bytes) pass 2^31 although the
+# tensor itself has 1.6 G elements.  That is the round-4 one-pass drift (3.35e-3 on the features,
+# only on tiles >= 2674), and the same wrap in a bf16 kernel is the likely source of the round-4
+# train-mode illegal-address fault.  So the bag is always held in pieces of at most
+# max_tiles_per_call() tiles (668 fp32 / 1337 bf16 at 224 x 224), and _lib_guard refuses any
+# library tensor of 2 GiB or more before it reaches a library.
+LIB_MAX_BYTES = 2 ** 31 - 1
 
 
 def tile_elems_max(h=224, w=224):
@@ -197,16 +204,18 @@ def tile_elems_max(h=224, w=224):
     return max(3 * h * w, 64 * h2 * w2, 256 * h4 * w4)
 
 
-def max_tiles_per_call(h=224, w=224):
-    """Tiles per library call that keep every activation under LIB_MAX_ELEMS (2674 at 224 x 224)."""
-    return max(1, LIB_MAX_ELEMS // tile_elems_max(h, w))
+def max_tiles_per_call(h=224, w=224, elem_bytes=4):
+    """Tiles per library call that keep every activation under LIB_MAX_BYTES (224 x 224: 668 tiles
+    in fp32, 1337 in bf16)."""
+    return max(1, LIB_MAX_BYTES // (tile_elems_max(h, w) * elem_bytes))
 
 
 def _lib_guard(*ts):
     for t in ts:
-        if t is not None and t.numel() > LIB_MAX_ELEMS:
-            raise RuntimeError(f"encoder: a library call on {t.numel()} elements (shape {tuple(t.shape)}) exceeds "
-                               f"2^31 - 1; the bag must be held in pieces of <= max_tiles_per_call() tiles")
+        if t is not None and t.numel() * t.element_size() > LIB_MAX_BYTES:
+            raise RuntimeError(f"encoder: a library call on {t.numel() * t.element_size()} bytes (shape "
+                               f"{tuple(t.shape)}) reaches 2^31; the bag must be held in pieces of "
+                               f"<= max_tiles_per_call() tiles")
 
 
 def _conv_out_numel(x, w, stride, padding):
@@ -218,11 +227,11 @@ def _conv_out_numel(x, w, stride, padding):
 
 
 def _lib_conv2d(x, w, b=None, stride=1, padding=0):
-    """F.conv2d (MIOpen / CK) with input and output sizes checked against LIB_MAX_ELEMS first."""
+    """F.conv2d (MIOpen / CK) with input and output sizes checked against LIB_MAX_BYTES first."""
     _lib_guard(x)
-    if _conv_out_numel(x, w, stride, padding) > LIB_MAX_ELEMS:
+    if _conv_out_numel(x, w, stride, padding) * x.element_size() > LIB_MAX_BYTES:
         raise RuntimeError(f"encoder: convolution output of {_conv_out_numel(x, w, stride, padding)} elements "
-                           f"exceeds 2^31 - 1; hold the bag in pieces of <= max_tiles_per_call() tiles")
+                           f"reaches 2^31 bytes; hold the bag in pieces of <= max_tiles_per_call() tiles")
     return F.conv2d(x, w, b, stride=stride, padding=padding)
 
 
@@ -231,11 +240,11 @@ def _lib_max_pool(x):
     return F.max_pool2d(x, 3, 2, 1)
 
 
-def train_pieces(n_tiles, chunk, h=224, w=224, max_pieces=64):
+def train_pieces(n_tiles, chunk, h=224, w=224, elem_bytes=4, max_pieces=64):
     """Piece size of the train-mode bag: at least ``chunk`` tiles, enough that the statistics call
     combines at most ``max_pieces`` pieces (tm_bn_train_stats), never more than
-    max_tiles_per_call(h, w).  Raises when no piece size satisfies both."""
-    cap = max_tiles_per_call(h, w)
+    max_tiles_per_call(h, w, elem_bytes).  Raises when no piece size satisfies both."""
+    cap = max_tiles_per_call(h, w, elem_bytes)
     size = min(max(chunk, -(-n_tiles // max_pieces)), cap)
     if -(-n_tiles // size) > max_pieces:
         raise RuntimeError(f"encoder: a {n_tiles}-tile train-mode bag needs more than {max_pieces} pieces of "
@@ -365,7 +374,7 @@ class RetCCLResNet50(nn.Module):
             self._cast_key = key
         w = self._cast
         ws = torch.empty(self._bn_ws_floats(), dtype=torch.float32, device=x.device)
-        piece = train_pieces(x.shape[0], self.chunk, x.shape[2], x.shape[3])
+        piece = train_pieces(x.shape[0], self.chunk, x.shape[2], x.shape[3], x.element_size())
         xs = [_cl(_lib_conv2d(x[i:i + piece], w["conv1.weight"], None, stride=2, padding=3))
               for i in range(0, x.shape[0], piece)]
         st = _bn_train_stats(xs, self.bn1, ws)
@@ -421,15 +430,17 @@ class RetCCLResNet50(nn.Module):
         # train-mode BatchNorm normalises with the statistics of the whole [B*bag] batch the
         # reference feeds model_ft in one call (model_interface.py:303-309): the fused train path
         # holds the bag in pieces whose statistics are combined; eval chunks are per-tile exact.
-        # No library call sees more than LIB_MAX_ELEMS elements on any path.
-        cap = max_tiles_per_call(x.shape[2], x.shape[3])
-        chunk = x.shape[0] if self.training else max(1, min(self.chunk, cap))
+        # No library call sees a tensor of LIB_MAX_BYTES or more on any path (the module path under
+        # autocast keeps fp32 BatchNorm outputs: sized as fp32).
         fused_train = self.training and not grad and self.channels_last
+        esz = 2 if dt == torch.bfloat16 and (fused_train or not self.training) else 4
+        cap = max_tiles_per_call(x.shape[2], x.shape[3], esz)
+        chunk = x.shape[0] if self.training else max(1, min(self.chunk, cap))
         if self.training and not fused_train and x.shape[0] > cap:
             # nn.BatchNorm2d needs the whole batch in one module call; above the cap that call
             # would hand the library > 2^31-element tensors
             raise RuntimeError(f"encoder: train mode with autograd (or without channels-last) takes at most {cap} "
-                               f"tiles per call (the whole-batch BatchNorm would exceed 2^31 elements); got "
+                               f"tiles per call (the whole-batch BatchNorm would hand the library >= 2^31 bytes); got "
                                f"{x.shape[0]}")
         autocast = self.training and not fused_train and dt == torch.bfloat16
         with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
