@@ -160,6 +160,12 @@ int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_
                   const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
                   float* dq, float* work, float* dkl, float* dy, int accumulate, tm_reduce_queue* rq,
                   void* stream);
+/* bf16 only: tm_nys_a1_bwd with dq written as bf16(dq_scale * dq) into the q part of dqkv
+ * ([B][n][3*nh*64], bf16, the columns of each head) instead of fp32 [B*h][n][64] rows (half the
+ * bytes, no fp32 round trip); tm_nys_assemble_q_slab_inplace then adds the landmark term there. */
+int tm_nys_a1_bwd_dqkv(const void* q, const void* dmerged, const void* kl_t, const void* y_t, const float* lse1,
+                       const float* d1, int nbh, int nh, int n, void* dqkv, float dq_scale, float* work, float* dkl,
+                       float* dy, tm_reduce_queue* rq, void* stream);
 long long tm_nys_a3_bwd_workspace(int nbh, int n);
 /* d3 (here and in tm_nys_a3_bwd_fused): D = rowsum(dW o W) as [2][B*h][256] partials, the two
  * 32-column halves of dW (tm_bmm_job.Rd of the dW = Z^T dY product); the kernels sum them */
@@ -192,6 +198,9 @@ int tm_nys_a3_bwd_slabs(int nbh, int n);
  * (nh <= 8; slab [slabs][nbags*nh][256][64] fp32 as tm_nys_a3_bwd_fused(dql = NULL) leaves it) */
 int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, const float* dql, const float* slab, int slabs,
                            int nbags, int nh, int n, float scale, void* dqkv, void* stream);
+/* bf16, after tm_nys_a1_bwd_dqkv: q += scale * (dql + sum_p slab[p])[t/l]/l in place in dqkv */
+int tm_nys_assemble_q_slab_inplace(const float* dql, const float* slab, int slabs, int nbags, int nh, int n,
+                                   float scale, void* dqkv, void* stream);
 
 /* ---- pseudo-inverse + small fp32 batched products (pinv.hip) -------------
  * moore_penrose_iter_pinv of nystrom_attention (App. A eq. 7).

@@ -91,6 +91,7 @@ _SIGS = {
     "tm_nys_conv_bwd": (I, [I, P, P, P, P, I, I, I, P, P, P, P, P, P]),
     "tm_nys_a1_bwd_workspace": (L, [I, I, I]),
     "tm_nys_a1_bwd": (I, [I, P, P, P, P, P, P, I, I, I, I, P, P, P, P, I, P, P]),
+    "tm_nys_a1_bwd_dqkv": (I, [P, P, P, P, P, P, I, I, I, P, Fl, P, P, P, P, P]),
     "tm_nys_a3_bwd_workspace": (L, [I, I]),
     "tm_nys_a3_bwd": (I, [I, P, P, P, P, P, P, I, I, I, P, P, P, P, I, P, P]),
     "tm_nys_assemble_dqkv": (I, [I, P, P, P, P, P, I, I, I, Fl, P, P]),
@@ -98,6 +99,7 @@ _SIGS = {
     "tm_nys_assemble_q": (I, [I, P, I, P, P, I, I, I, Fl, P, P]),
     "tm_nys_a3_bwd_slabs": (I, [I, I]),
     "tm_nys_assemble_q_slab": (I, [I, P, I, P, P, I, I, I, I, Fl, P, P]),
+    "tm_nys_assemble_q_slab_inplace": (I, [P, P, I, I, I, I, Fl, P, P]),
     "tm_nys_attn_row": (I, [I, P, P, P, P, P, P, I, I, I, P, P]),
     "tm_bmm": (I, [C.POINTER(BmmJob), I, I, I, P]),
     "tm_pinv_saved_floats": (L, [I, I]),

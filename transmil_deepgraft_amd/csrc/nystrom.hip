@@ -1469,6 +1469,9 @@ struct BwdArgs {
   // [bag][n][3 nh 64]): k = dK + dk~[t / l] / l, v = dv (the conv backward's, read) + dV
   void* dqkv; const float* dkl; float inv_l; int l;
   int dv_lo, dv_hi;   // fused: rows of the conv backward's dv that are read (zero outside)
+  // bf16 A1 kernel: dqkv non-null = dq written as bf16(dq_scale * dq) into the q part of dqkv
+  // ([bag][q_total][3 nh 64], the columns of head bh % nh) instead of fp32 rows at dq
+  float dq_scale;
 };
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
@@ -1923,12 +1926,26 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
           *(f32x4*)(dst + (size_t)q * DH + d4) = v;
         }
       } else if (kq == 0) {
+        if (MODE == MODE_A1 && a.dqkv) {
+          // bf16 q rows of dqkv (half the bytes of the fp32 rows; the landmark term is added in place
+          // by tm_nys_assemble_q_slab_inplace)
+          const int bag = bh / nh, hh = bh % nh, ld = 3 * nh * DH;
+          bf16* qo = (bf16*)a.dqkv + ((size_t)bag * a.q_total + q_begin + c0) * ld + hh * DH + dt_q * 32 + r;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float v = acc[i];
+          for (int i = 0; i < 16; ++i) {
+            float v = acc[i];
 #pragma unroll
-          for (int g = 0; g < NKQ - 1; ++g) v += xch[g * 2048 + acc_row(i, h) * 64 + dt_q * 32 + r];
-          dst[(size_t)acc_row(i, h) * DH + dt_q * 32 + r] = v;
+            for (int g = 0; g < NKQ - 1; ++g) v += xch[g * 2048 + acc_row(i, h) * 64 + dt_q * 32 + r];
+            qo[(size_t)acc_row(i, h) * ld] = (bf16)(a.dq_scale * v);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float v = acc[i];
+#pragma unroll
+            for (int g = 0; g < NKQ - 1; ++g) v += xch[g * 2048 + acc_row(i, h) * 64 + dt_q * 32 + r];
+            dst[(size_t)acc_row(i, h) * DH + dt_q * 32 + r] = v;
+          }
         }
       }
       cstamp(c0, 6);
@@ -2099,8 +2116,10 @@ __global__ void assemble_q_kernel(const float* __restrict__ dq, int dq_row, cons
 // grid (256 landmarks, nbags), block 512: the workgroup's first QP dq pieces per thread are
 // requested first, then landmark j's slab row is summed (eight part groups, combined in a fixed
 // order) while they are in flight, then the l tokens of segment j are written.
+// INPLACE (bf16): the q rows already hold bf16(scale * dq) (tm_nys_a1_bwd_dqkv); the landmark term
+// scale * (dql + sum_p slab[p])[t / l] / l is added to them in place.
 constexpr int AQ_THREADS = 512, AQ_GROUPS = AQ_THREADS / 64, AQ_QP = 5;
-template <typename T>
+template <typename T, bool INPLACE = false>
 __global__ __launch_bounds__(AQ_THREADS) void assemble_q_slab_kernel(const float* __restrict__ dq, int dq_row,
                                                                      const float* __restrict__ dql,
                                                                      const float* __restrict__ slab, int slabs,
@@ -2115,13 +2134,24 @@ __global__ __launch_bounds__(AQ_THREADS) void assemble_q_slab_kernel(const float
     c = (it % pieces) * 8;
     return (((size_t)bag * nh + c / DH) * n + t) * DH + c % DH;
   };
+  auto load_q = [&](int it) -> f32x8 {
+    int t, c;
+    const size_t row = dq_row_of(it, t, c);
+    if constexpr (INPLACE) {
+      const vec8<T> v = load8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c);
+      f32x8 r;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r[e] = to_f(v[e]);
+      return r;
+    } else {
+      return (dq_row < 0 || t == dq_row) ? load8<float>(dq + row) : (f32x8){};
+    }
+  };
   f32x8 a[AQ_QP];
 #pragma unroll
   for (int u = 0; u < AQ_QP; ++u) {
     const int it = tid + AQ_THREADS * u;
-    int t, c;
-    const size_t row = it < items ? dq_row_of(it, t, c) : 0;
-    a[u] = (it < items && (dq_row < 0 || t == dq_row)) ? load8<float>(dq + row) : (f32x8){};
+    a[u] = it < items ? load_q(it) : (f32x8){};
   }
   {
     const int pc = tid & 63, g = tid >> 6;
@@ -2161,17 +2191,15 @@ __global__ __launch_bounds__(AQ_THREADS) void assemble_q_slab_kernel(const float
     (void)dq_row_of(it, t, c);
     vec8<T> out;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) out[e] = from_f<T>(scale * (av[e] + part[0][c + e]));
+    for (int e = 0; e < 8; ++e)
+      out[e] = INPLACE ? from_f<T>(av[e] + scale * part[0][c + e]) : from_f<T>(scale * (av[e] + part[0][c + e]));
     store8<T>(dqkv + ((size_t)bag * n + t) * (3 * inner) + c, out);
   };
 #pragma unroll
   for (int u = 0; u < AQ_QP; ++u)
     if (tid + AQ_THREADS * u < items) store(tid + AQ_THREADS * u, a[u]);
-  for (int it = tid + AQ_THREADS * AQ_QP; it < items; it += AQ_THREADS) {   // long segments (l > 40)
-    int t, c;
-    const size_t row = dq_row_of(it, t, c);
-    store(it, (dq_row < 0 || t == dq_row) ? load8<float>(dq + row) : (f32x8){});
-  }
+  for (int it = tid + AQ_THREADS * AQ_QP; it < items; it += AQ_THREADS)   // long segments (l > 40)
+    store(it, load_q(it));
 }
 
 }  // namespace
@@ -2410,12 +2438,38 @@ extern "C" long long tm_nys_a1_bwd_workspace(int nbh, int n, int queries_per_wg)
   return 2LL * slabs * nbh * NL * DH * (long long)sizeof(float);
 }
 
+namespace {
+int a1_bwd_impl(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t, const float* lse1,
+                const float* d1, int nbh, int nh, int n, int queries_per_wg, float* dq, void* dqkv, float dq_scale,
+                float* work, float* dkl, float* dy, int accumulate, tm_reduce_queue* rq, void* stream);
+}  // namespace
+
 extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t,
                              const float* lse1, const float* d1, int nbh, int nh, int n, int queries_per_wg,
                              float* dq, float* work, float* dkl, float* dy, int accumulate, tm_reduce_queue* rq,
                              void* stream) {
+  return a1_bwd_impl(dtype, q, dmerged, kl_t, y_t, lse1, d1, nbh, nh, n, queries_per_wg, dq, nullptr, 0.f, work, dkl,
+                     dy, accumulate, rq, stream);
+}
+
+// bf16 only: dq goes to the q part of dqkv as bf16(dq_scale * dq) (tm_nys_assemble_q_slab_inplace
+// then adds the landmark term in place)
+extern "C" int tm_nys_a1_bwd_dqkv(const void* q, const void* dmerged, const void* kl_t, const void* y_t,
+                                  const float* lse1, const float* d1, int nbh, int nh, int n, void* dqkv,
+                                  float dq_scale, float* work, float* dkl, float* dy, tm_reduce_queue* rq,
+                                  void* stream) {
+  TM_REQUIRE(dqkv && ((uintptr_t)dqkv % 16) == 0 && nbh % nh == 0, "a1_bwd_dqkv: dqkv");
+  return a1_bwd_impl(TM_BF16, q, dmerged, kl_t, y_t, lse1, d1, nbh, nh, n, 256, nullptr, dqkv, dq_scale, work, dkl,
+                     dy, 0, rq, stream);
+}
+
+namespace {
+int a1_bwd_impl(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t, const float* lse1,
+                const float* d1, int nbh, int nh, int n, int queries_per_wg, float* dq, void* dqkv, float dq_scale,
+                float* work, float* dkl, float* dy, int accumulate, tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(queries_per_wg % 32 == 0 && n % queries_per_wg == 0, "a1_bwd: queries_per_wg must divide n, x32");
   const bool split = dtype == TM_BF16 && queries_per_wg <= NL && NYS_VARIANT != 3;
+  TM_REQUIRE(!dqkv || split, "a1_bwd_dqkv: the bf16 split kernel only");
   const int nqc = split ? a1_bwd_split(nbh, n) : n / queries_per_wg;
   BwdArgs a{};
   a.q = q; a.q_bag = (long long)nh * n * DH; a.q_head = (long long)n * DH; a.q_row = DH;
@@ -2424,6 +2478,7 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
   a.v = y_t; a.v_bag = a.k_bag; a.v_head = a.k_head;
   a.lse = lse1; a.lse_bh = n; a.dd = d1; a.dd_bh = n;
   a.dq = dq; a.dq_bh = (long long)n * DH;
+  a.dqkv = dqkv; a.dq_scale = dq_scale;
   float* slab_k = work;
   float* slab_v = work + (size_t)nqc * nbh * NL * DH;
   a.dk = slab_k; a.dk_bh = (long long)NL * DH;
@@ -2445,6 +2500,7 @@ extern "C" int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, cons
   if (rc) return rc;
   return tm_splitk_reduce(slab_v, dy, nqc, cnt, 1.0f, 0, rq, stream);
 }
+}  // namespace
 
 // A3 backward: keys = k rows, values = v rows, queries = ql_t (256 landmarks), dO = dw_t.
 // dk written (=), dv accumulated (+=), dql accumulated from partial slabs.
@@ -2560,6 +2616,16 @@ extern "C" int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, co
   TM_DTYPE_DISPATCH(dtype, (assemble_q_slab_kernel<T><<<dim3(NL, nbags), AQ_THREADS, 0, (hipStream_t)stream>>>(
                                dq, dq_row, dql, slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL, nh, scale,
                                (T*)dqkv)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_nys_assemble_q_slab_inplace(const float* dql, const float* slab, int slabs, int nbags, int nh, int n,
+                                              float scale, void* dqkv, void* stream) {
+  TM_REQUIRE(n > 0 && n % NL == 0 && nh > 0 && nh <= 8 && slabs > 0, "assemble_q_slab_inplace: bad shape");
+  TM_REQUIRE(dql && slab && dqkv && ((uintptr_t)dqkv % 16) == 0, "assemble_q_slab_inplace: null / misaligned operand");
+  assemble_q_slab_kernel<bf16, true><<<dim3(NL, nbags), AQ_THREADS, 0, (hipStream_t)stream>>>(
+      nullptr, -1, dql, slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL, nh, scale, (bf16*)dqkv);
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -418,6 +418,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
     dk = pool(nbh * n * DH)
     dkl = pool(nbh * NL * DH).view(nbh, NL, DH)
     dy = pool(nbh * NL * DH).view(nbh, NL, DH)
+    dqkv_early = None
     fused = state["a2s"] is not None     # bf16 mode: the A3 backward writes the final k / v parts
     if cls_row is not None:
         # one non-zero query row: dq row, rank-1 dk~ / dY, the conv33 dv window (clsrow.hip); the
@@ -430,7 +431,10 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
                   _p(dwconv_out), st)
     else:
         # conv33 backward + D1
-        dq = pool(nbh * n * DH)
+        # bf16 mode: dq goes straight into the q part of dqkv as bf16 (tm_nys_a1_bwd_dqkv); the
+        # landmark term is added there in place at the end (tm_nys_assemble_q_slab_inplace)
+        dqkv_early = pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH) if fused else None
+        dq = None if fused else pool(nbh * n * DH)
         dv = pool(nbh * n * DH)
         d1 = pool(nbh * n)
         with defer_reductions(), probe("conv_bwd"):
@@ -442,8 +446,13 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         work = pool(_lib.query("tm_nys_a1_bwd_workspace", nbh, n, qpw) // 4)
         with defer_reductions():     # its dk~ and dY slab sums as one launch
             with probe("a1_bwd"):
-                _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t),
-                          _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, _rq(), st)
+                if fused:
+                    _lib.call("tm_nys_a1_bwd_dqkv", _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t), _p(state["lse1"]),
+                              _p(d1), nbh, nh, n, _p(dqkv_early), C.c_float(scale), _p(work), _p(dkl), _p(dy), _rq(), st)
+                else:
+                    _lib.call("tm_nys_a1_bwd", dt_code, _p(q), _p(dmerged), _p(state["kl_t"]), _p(y_t),
+                              _p(state["lse1"]), _p(d1), nbh, nh, n, qpw, _p(dq), _p(work), _p(dkl), _p(dy), 0, _rq(),
+                              st)
         flush_reductions()
     # Y = Z W
     dz = pool(mat).view(nbh, NL, NL)
@@ -487,7 +496,9 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
                   _p(da2), st)
         _lib.call("tm_softmax_bwd_rows256", _p(state["a2"]), _p(da2), _p(ds2), nbh * NL, st)
     dql = pool(nbh * NL * DH).view(nbh, NL, DH)
-    dqkv = pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH)
+    dqkv = None if cls_row is None and fused else pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH)
+    if dqkv is None:
+        dqkv = dqkv_early
     if fused:
         # dq~ (landmark path, without the A3 part) and the final dk~ (+= the A1 part) first; the
         # fused A3 backward then writes k / v of dqkv and dq~3; assemble_q writes q
@@ -498,8 +509,13 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
             # dql = NULL: the dq~3 partial slab stays in work3; assemble_q_slab sums it in place
             _lib.call("tm_nys_a3_bwd_fused", _p(state["ql_t"]), _p(dw_t), _p(k), _p(v), _p(state["lse3"]), _p(d3),
                       nbh, nh, n, _p(dv), lo, hi, _p(dkl), _p(work3), None, _p(dqkv), _rq(), st)
-        _lib.call("tm_nys_assemble_q_slab", dt_code, _p(dq), -1 if cls_row is None else cls_row, _p(dql),
-                  _p(work3), _lib.query("tm_nys_a3_bwd_slabs", nbh, n), geo.B, nh, n, C.c_float(scale), _p(dqkv), st)
+        slabs = _lib.query("tm_nys_a3_bwd_slabs", nbh, n)
+        if cls_row is None:
+            _lib.call("tm_nys_assemble_q_slab_inplace", _p(dql), _p(work3), slabs, geo.B, nh, n, C.c_float(scale),
+                      _p(dqkv), st)
+        else:
+            _lib.call("tm_nys_assemble_q_slab", dt_code, _p(dq), cls_row, _p(dql), _p(work3), slabs, geo.B, nh, n,
+                      C.c_float(scale), _p(dqkv), st)
         return dqkv
     bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL, E1=dql3, e1=1.0),
          bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
