@@ -596,27 +596,32 @@ TM_DEV void rd_frag(bf16x8& f, unsigned base, const unsigned (&kc)[4]) {
 
 // one 64-deep k-tile of one wave's 32 x 64 subtile: 4 k-steps of 2 MFMAs, the LDS reads of
 // step s+1 in flight while step s multiplies
-template <bool A_KS, bool B_KS>
+// SWAP: the products are issued as (B, A) -- acc[j] holds the TRANSPOSED 32 x 32 tile (lane l:
+// output row l & 31, 16 output columns per lane), the register layout gemm_pr_kernel stores from
+template <bool A_KS, bool B_KS, bool SWAP = false>
 TM_DEV void ring_tile_mma(f32x16 (&acc)[2], unsigned abase, unsigned b0, unsigned b1, const unsigned (&akc)[4],
                           const unsigned (&bkc0)[4], const unsigned (&bkc1)[4]) {
   constexpr int RS = (A_KS ? 2 : 1) + 2 * (B_KS ? 2 : 1);   // LDS reads per k-step
+  auto mm = [](f32x16& c, const bf16x8& a, const bf16x8& b) {
+    if constexpr (SWAP) mma16(c, b, a); else mma16(c, a, b);
+  };
   bf16x8 a[2], b[2][2];
   rd_frag<A_KS, 0>(a[0], abase, akc); rd_frag<B_KS, 0>(b[0][0], b0, bkc0); rd_frag<B_KS, 0>(b[0][1], b1, bkc1);
   rd_frag<A_KS, 1>(a[1], abase, akc); rd_frag<B_KS, 1>(b[1][0], b0, bkc0); rd_frag<B_KS, 1>(b[1][1], b1, bkc1);
   wait_lgkm<RS>();
-  mma16(acc[0], a[0], b[0][0]);
-  mma16(acc[1], a[0], b[0][1]);
+  mm(acc[0], a[0], b[0][0]);
+  mm(acc[1], a[0], b[0][1]);
   rd_frag<A_KS, 2>(a[0], abase, akc); rd_frag<B_KS, 2>(b[0][0], b0, bkc0); rd_frag<B_KS, 2>(b[0][1], b1, bkc1);
   wait_lgkm<RS>();
-  mma16(acc[0], a[1], b[1][0]);
-  mma16(acc[1], a[1], b[1][1]);
+  mm(acc[0], a[1], b[1][0]);
+  mm(acc[1], a[1], b[1][1]);
   rd_frag<A_KS, 3>(a[1], abase, akc); rd_frag<B_KS, 3>(b[1][0], b0, bkc0); rd_frag<B_KS, 3>(b[1][1], b1, bkc1);
   wait_lgkm<RS>();
-  mma16(acc[0], a[0], b[0][0]);
-  mma16(acc[1], a[0], b[0][1]);
+  mm(acc[0], a[0], b[0][0]);
+  mm(acc[1], a[0], b[0][1]);
   wait_lgkm<0>();
-  mma16(acc[0], a[1], b[1][0]);
-  mma16(acc[1], a[1], b[1][1]);
+  mm(acc[0], a[1], b[1][0]);
+  mm(acc[1], a[1], b[1][1]);
 }
 
 // diagnostics (variant 8 only): per-workgroup shader-clock stamps of the ring kernel, read by
@@ -979,6 +984,203 @@ __global__ __launch_bounds__(512) void gemm_persist_kernel(const bf16* __restric
 }
 
 // ---------------------------------------------------------------------------
+// Persistent ring GEMM with the epilogue straight from the accumulator registers (gemm_pr_kernel):
+// two 512-thread workgroups per CU (64 KB of LDS each: the 2-stage LDS-DMA ring and nothing else),
+// each walking its tiles t = blockIdx.x + i * gridDim.x (XCD-clustered, ptile_set) as ONE stream of
+// 64-deep k-steps.  What it removes, per tile, from the ring kernel's timeline (stamps,
+// scripts/dev/gemm_stamps2.py, profiles/r05c_gemm_stamps.txt -- QKV: first tile landed 2.8 k,
+// k-loop 10.6 k, accumulator staging 1.2 k, epilogue 2.6 k cycles per tile):
+//   * the first k-step of the next tile is already in flight while this tile's epilogue runs;
+//   * no LDS epilogue image: the products are issued transposed (ring_tile_mma<.., SWAP>), so each
+//     lane holds 16 output COLUMNS of one output row; one cross-half exchange (lanes l, l ^ 32)
+//     gives every lane 8 consecutive columns -> the epilogue works on 8-column row chunks as the
+//     staged one does (bias, pre-activation, GELU, dropout, residual, row map, QKV scatter) and
+//     stores 16 B (bf16) / 32 B (fp32) per lane with no barrier and no LDS round trip;
+//   * the two workgroups of a CU drift apart after their first tiles, so one's epilogue and first
+//     operand fill overlap the other's MFMA k-loop.
+// Chunk (j, p) of a lane: row m0 + 32 wm + (l & 31), columns n0 + 64 wn + 32 j + 16 p + 8 (l >> 5).
+constexpr int PR_NS = 2;
+[[maybe_unused]] constexpr int PR_LDS = PR_NS * STAGE_BYTES;   // 64 KB
+
+template <typename OutT, int KIND>
+TM_DEV void pr_epilogue_chunk(OutT* __restrict__ C, const tm_gemm_args& g, int m, int n, const float (&v)[8],
+                              uint64_t seed) {
+  const int ne = min(8, g.N - n);
+  if (ne <= 0 || m >= g.M) return;
+  float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (g.bias) {
+    if (ne == 8 && ((uintptr_t)g.bias & 15) == 0) { const f32x8 t8 = load8<float>(g.bias + n); for (int e = 0; e < 8; ++e) bv[e] = t8[e]; }
+    else { for (int e = 0; e < ne; ++e) bv[e] = g.bias[n + e]; }
+  }
+  if constexpr (KIND == EK_QKV) {   // 8 columns never straddle a head (dh % 8 == 0, checked on the host)
+    const int inner = g.nh * g.dh;
+    const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
+    const float qs = which == 0 ? g.qscale : 1.f;
+    const int bag = m / g.seq, t = m - bag * g.seq;
+    OutT* dst = C + ((((long long)which * g.nbags + bag) * g.nh + hh) * g.seq + t) * g.dh + d;
+    vec8<OutT> o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f<OutT>((v[e] * g.alpha + bv[e]) * qs);
+    store8<OutT>(dst, o);
+    return;
+  } else if constexpr (KIND == EK_PLAIN) {
+    vec8<OutT> o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f<OutT>(v[e] * g.alpha + bv[e]);
+    OutT* dst = C + (size_t)m * g.ldc + n;
+    if (ne == 8 && g.ldc % 8 == 0) store8<OutT>(dst, o);
+    else { for (int e = 0; e < ne; ++e) dst[e] = o[e]; }
+    return;
+  } else {
+    // runtime mode: row map (TransMIL grid duplication / padding skip), pre-activation, GELU,
+    // dropout, residual / accumulate -- the same per-element order as gemm_epilogue_rows
+    int row = m, dup = -1;
+    if (g.grp_in > 0) {
+      const int bag = m / g.grp_in, t = m - bag * g.grp_in - g.skip;
+      if (t < 0) return;
+      if (t < g.dup_n) dup = bag * g.grp_out + g.dup_off + t;
+      row = bag * g.grp_out + g.out_off + t;
+    }
+    const bool vec = ne == 8 && g.ldc % 8 == 0 && (!g.pre || g.ld_pre % 8 == 0);
+    const size_t off = (size_t)row * g.ldc + n;
+    float addr[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, addc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (g.resid) {
+      if (vec) { const f32x8 t8 = load8<float>(g.resid + off); for (int e = 0; e < 8; ++e) addr[e] = t8[e]; }
+      else { for (int e = 0; e < ne; ++e) addr[e] = g.resid[off + e]; }
+    }
+    if (g.accumulate) {
+      if (vec) { const vec8<OutT> t8 = load8<OutT>(C + off); for (int e = 0; e < 8; ++e) addc[e] = to_f(t8[e]); }
+      else { for (int e = 0; e < ne; ++e) addc[e] = to_f(C[off + e]); }
+    }
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = v[e] * g.alpha + bv[e];
+    vec8<OutT> pre8, out8;
+    if (g.pre) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pre8[e] = from_f<OutT>(x[e]);
+    }
+    if (g.gelu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+    }
+    if (g.drop_p > 0.f) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float u = dropout_u01(seed, (uint32_t)row, (uint32_t)(n + e));
+        x[e] = (u >= g.drop_p) ? x[e] * g.drop_scale : 0.f;
+      }
+    }
+    // as gemm_epilogue_rows: + residual, then + the stored C (accumulate), in that order
+    if (g.resid) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] += addr[e];
+    }
+    if (g.accumulate) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] += addc[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out8[e] = from_f<OutT>(x[e]);
+    if (vec) {
+      if (g.pre) store8<OutT>((OutT*)g.pre + (size_t)m * g.ld_pre + n, pre8);
+      store8<OutT>(C + off, out8);
+      if (dup >= 0) store8<OutT>(C + (size_t)dup * g.ldc + n, out8);
+    } else {
+      for (int e = 0; e < ne; ++e) {
+        if (g.pre) ((OutT*)g.pre)[(size_t)m * g.ld_pre + n + e] = pre8[e];
+        C[off + e] = out8[e];
+        if (dup >= 0) C[(size_t)dup * g.ldc + n + e] = out8[e];
+      }
+    }
+  }
+}
+
+template <typename OutT, bool B_KN, int KIND>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void gemm_pr_kernel(
+    const bf16* __restrict__ A, const bf16* __restrict__ B, OutT* __restrict__ C, tm_gemm_args g, int tiles_m,
+    int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;   // 4 (M) x 2 (N) waves of 32 x 64
+  const int ntiles = tiles_m * tiles_n;       // splits == 1 (host-checked)
+
+  unsigned akc[4], bkc0[4] = {0, 0, 0, 0}, bkc1[4] = {0, 0, 0, 0};
+  unsigned bks0 = 0, bks1 = 0;
+  kc_addrs(akc, wm * 32, lane);
+  if constexpr (B_KN) {
+    bks0 = ks_addr(wn * 64, lane) + STAGE_BYTES / 2;
+    bks1 = ks_addr(wn * 64 + 32, lane) + STAGE_BYTES / 2;
+  } else {
+    kc_addrs(bkc0, wn * 64, lane);
+    kc_addrs(bkc1, wn * 64 + 32, lane);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) { bkc0[s] += STAGE_BYTES / 2; bkc1[s] += STAGE_BYTES / 2; }
+  }
+  const unsigned ring = lds_u32(smem);
+  const uint64_t seed = (KIND == EK_ANY && g.drop_p > 0.f) ? effective_seed(g.seed, g.seed_ptr) : 0;
+
+  PTile is{}, cs{};
+  is.i = 0;
+  ptile_set(is, ntiles, tiles_m, tiles_n, g);
+  cs = is;
+  int issued = 0, done = 0;
+  auto issue = [&]() {
+    char* st = smem + (issued % PR_NS) * STAGE_BYTES;
+    const int k0 = is.kt * 64;
+    glds_tile<false>(st, A, g.lda, is.m0, g.M, k0, wave, lane);
+    glds_tile<B_KN>(st + STAGE_BYTES / 2, B, g.ldb, is.n0, g.N, k0, wave, lane);
+    ++issued;
+    if (++is.kt == is.nk) { ++is.i; ptile_set(is, ntiles, tiles_m, tiles_n, g); }
+  };
+  if (is.t < ntiles) issue();
+
+  f32x16 acc[2];
+  acc[0] = (f32x16){};
+  acc[1] = (f32x16){};
+  const int h = lane >> 5, r32 = lane & 31;
+  while (cs.t < ntiles) {
+    // step `done` landed once at most (issued - done - 1) younger steps (4 loads each) remain; after
+    // an epilogue none is younger, and the wait also retires that epilogue's stores
+    if (issued - done - 1 >= 1) wait_vm<4>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's pieces landed; every wave done with step done-1
+    asm volatile("" ::: "memory");
+    if (is.t < ntiles) issue();    // overwrites step done-1's slot (possibly the next tile's first step)
+    const unsigned sb = ring + (done % PR_NS) * STAGE_BYTES;
+    ring_tile_mma<false, B_KN, true>(acc, sb, (B_KN ? bks0 : 0) + sb, (B_KN ? bks1 : 0) + sb, akc, bkc0, bkc1);
+    ++done;
+    if (++cs.kt == cs.nk) {
+      // epilogue from registers: acc[j] lane l = row 32 wm + r32 (of the tile), columns
+      // 64 wn + 32 j + acc_row(i, h); the (l, l ^ 32) exchange gives 8 consecutive columns
+      const int m = cs.m0 + wm * 32 + r32;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const int q0 = 2 * p, q1 = 2 * p + 1;
+          float send[4], recv[4], v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) send[e] = h ? acc[j][4 * q0 + e] : acc[j][4 * q1 + e];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) recv[e] = __shfl_xor(send[e], 32, 64);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = h ? recv[e] : acc[j][4 * q0 + e];
+            v[4 + e] = h ? acc[j][4 * q1 + e] : recv[e];
+          }
+          pr_epilogue_chunk<OutT, KIND>(C, g, m, cs.n0 + wn * 64 + j * 32 + 16 * p + 8 * h, v, seed);
+        }
+      }
+      acc[0] = (f32x16){};
+      acc[1] = (f32x16){};
+      ++cs.i;
+      ptile_set(cs, ntiles, tiles_m, tiles_n, g);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Big-tile bf16 GEMM: 256 x TBN (256 or 128) per 512-thread workgroup.  A 128 x 128 tile moves
 // 32 KB of operands per 64-deep k-step for 2 MFLOP (64 flop/B): at 2.5 PF that needs ~39 TB/s of
 // L2 -> CU operand bandwidth, which the chip does not have (the 128-tile kernels above run at
@@ -1219,6 +1421,16 @@ inline bool use_ring160(const tm_gemm_args& g) {
   return t128 > cu && t160 <= cu;
 }
 
+// the persistent register-epilogue kernel (k-contiguous A, no split).  Diagnostic build: variant 11
+// wherever valid, 12 never.
+inline bool use_pr(const tm_gemm_args& g) {
+  if (g.a_trans || g.splits != 1 || g.K % 64 != 0 || g.mode == TM_EPI_SPLITK) return false;
+  if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
+  if (GEMM_VARIANT == 11) return true;
+  if (GEMM_VARIANT != 0) return false;
+  return false;   // product selection: set from the measured A/B (scripts/dev/gemm_pr_ab.py)
+}
+
 template <typename OutT>
 bool big_ok(const tm_gemm_args& g) {
   if (GEMM_VARIANT != 7) return false;
@@ -1266,6 +1478,26 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
 #undef TM_PERSIST_CASE
     }
 #endif
+    if (use_pr(g)) {
+      const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+      const int ntiles = tiles_m * tiles_n, cap = 2 * tm_cu_count();
+      const int nwg = ntiles < cap ? ntiles : cap;
+      const int kind = epilogue_kind(g);
+#define TM_PR(BKN, K)                                                                                \
+      {                                                                                              \
+        tm_allow_smem(gemm_pr_kernel<OutT, BKN, K>, PR_LDS);                                         \
+        gemm_pr_kernel<OutT, BKN, K><<<nwg, 512, PR_LDS, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g, \
+                                                              tiles_m, tiles_n);                     \
+      }
+      if (g.b_kn) {
+        if (kind == EK_PLAIN) TM_PR(true, EK_PLAIN) else if (kind == EK_QKV) TM_PR(true, EK_QKV) else TM_PR(true, EK_ANY)
+      } else {
+        if (kind == EK_PLAIN) TM_PR(false, EK_PLAIN) else if (kind == EK_QKV) TM_PR(false, EK_QKV) else TM_PR(false, EK_ANY)
+      }
+#undef TM_PR
+      TM_CHECK_LAUNCH();
+      return 0;
+    }
     if (use_ring160(g)) {
       constexpr size_t sm = 2 * R160_STAGE;
       const dim3 g160((g.N + BN - 1) / BN, (g.M + BM160 - 1) / BM160);
