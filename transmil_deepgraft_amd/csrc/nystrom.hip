@@ -1742,7 +1742,11 @@ TM_DEV bf16x8 frag_tr_rows(const bf16* S, int mb, int kb, int lane) {
 }
 TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) { return frag_tr_rows<BwdLay16::QROW>(S, mb, kb, lane); }
 
-template <int MODE, int NW = 8, int ST = 0>   // ST: diagnostic s_memtime stamps (g_a1_stamps): 1 phases, 2 one chunk
+// DQ2 (default): dQ = dS K by two waves, one 32-column d tile each over ALL the workgroup's keys in
+// one accumulation chain (no cross-wave partials through LDS, no third barrier per chunk; the other
+// waves go on to the next chunk's S / dP / dV / dK meanwhile).  DQ2 = 0: the earlier form (every
+// wave a key group's partial, summed through LDS by the group-0 waves; diagnostic build only).
+template <int MODE, int NW = 8, int ST = 0, int DQ2 = 1>   // ST: diagnostic s_memtime stamps (g_a1_stamps): 1 phases, 2 one chunk
 __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   using LY = std::conditional_t<NW == 9, BwdLay9, BwdLay16>;
   static_assert(NW == 8 || (NW == 9 && MODE == MODE_A3), "9-wave form: A3 even split only");
@@ -1799,14 +1803,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   // ---- one burst of loads: K rows (for K^T), Q / dO rows, K / V fragments, lse / D ----
   constexpr int QP = (LY::MAXQ * 8 + NT - 1) / NT;  // 16-B query-row pieces per thread (5 | 4)
   const int mykey = wave * 32;
-  bf16x8 kr[4], qr[QP], orow[QP], kf[4], vf[4];
+  bf16x8 qr[QP], orow[QP], kf[4], vf[4];
   // key rows past nk (a short workgroup of the even split): clamped loads, finite, and their dS
-  // columns are written as zeros, so they add nothing to dQ
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = tid + NT * j;  // 16-B piece: row c >> 3 (< 32 NW), d0 = (c & 7) * 8
-    kr[j] = load8(K + (size_t)min(c >> 3, nk - 1) * DH + (c & 7) * 8);
-  }
+  // columns are written as zeros, so they add nothing to dQ.  K^T is staged from the waves' own K
+  // fragments (no second read of the K rows)
 #pragma unroll
   for (int j = 0; j < QP; ++j) {
     const int c = tid + NT * j;
@@ -1829,10 +1829,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   stamp(1);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = tid + NT * j, row = c >> 3, d0 = (c & 7) * 8;
+  for (int st = 0; st < 4; ++st) {   // this lane's key mykey + r, d = 16 st + 8 h .. + 7
 #pragma unroll
-    for (int e = 0; e < 8; ++e) kt_s[(d0 + e) * KT_ROW + row] = kr[j][e];
+    for (int e = 0; e < 8; ++e) kt_s[(st * 16 + 8 * h + e) * KT_ROW + mykey + r] = kf[st][e];
   }
 #pragma unroll
   for (int j = 0; j < QP; ++j) {
@@ -1896,8 +1895,34 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
     for (int i = 0; i < 16; ++i) ds_s[acc_row(i, h) * DS_ROW + mykey + r] = from_f<bf16>(dp[i]);  // 0: idle wave
     __syncthreads();
     cstamp(c0, 3);
+    if constexpr (DQ2) {
+      // waves W0, W0 + 1 (SIMDs that do not host the 9-wave form's ninth wave): d tile wave - W0
+      constexpr int W0 = NW == 9 ? 1 : 0;
+      if (wave == W0 || wave == W0 + 1) {
+        const int dtq = wave - W0;
+        f32x16 acc = (f32x16){};
+        // (partly unrolled: fully unrolled, the hoisted operand reads spill the 9-wave form)
+#pragma unroll
+        for (int st = 0; st < 2 * NW; ++st) {
+          const int kk = st * 16 + 8 * h;
+          mma16(acc, load8(ds_s + r * DS_ROW + kk), load8(kt_s + (dtq * 32 + r) * KT_ROW + kk));
+        }
+        cstamp(c0, 4);
+        if (MODE == MODE_A1 && a.dqkv) {
+          const int bag = bh / nh, hh = bh % nh, ld = 3 * nh * DH;
+          bf16* qo = (bf16*)a.dqkv + ((size_t)bag * a.q_total + q_begin + c0) * ld + hh * DH + dtq * 32 + r;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) qo[(size_t)acc_row(i, h) * ld] = (bf16)(a.dq_scale * acc[i]);
+        } else {
+          float* dst = MODE == MODE_A1 ? a.dq + bh * a.dq_bh : a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;
+          dst += (size_t)(q_begin + c0) * DH + dtq * 32 + r;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dst[(size_t)acc_row(i, h) * DH] = acc[i];
+        }
+        cstamp(c0, 5);
+      }
+    } else {
     // dQ chunk [32 q x 64 d] = dS [32 x NK] . K [NK x 64]: this wave: d tile dt_q, keys 16 KQS kq ..
-    {
       f32x16 acc = (f32x16){};
       float* dst = MODE == MODE_A1 ? a.dq + bh * a.dq_bh : a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;
       dst += (size_t)(q_begin + c0) * DH;
@@ -2488,8 +2513,20 @@ int a1_bwd_impl(int dtype, const void* q, const void* dmerged, const void* kl_t,
   hipStream_t st = (hipStream_t)stream;
   if (split) {
     a.q_total = n;
-    tm_allow_smem(attn_bwd_bf16_kernel<MODE_A1>, BwdLay16::BYTES);
-    attn_bwd_bf16_kernel<MODE_A1><<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
+#ifdef TM_DIAG
+    if (NYS_VARIANT == 33 || NYS_VARIANT == 34) {   // diagnostic: stamps per wave (33 phases, 34 inside chunk 2)
+      auto kern = NYS_VARIANT == 33 ? attn_bwd_bf16_kernel<MODE_A1, 8, 1> : attn_bwd_bf16_kernel<MODE_A1, 8, 2>;
+      tm_allow_smem(kern, BwdLay16::BYTES);
+      kern<<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
+    } else if (NYS_VARIANT == 35) {   // diagnostic: the earlier cross-wave dQ form
+      tm_allow_smem(attn_bwd_bf16_kernel<MODE_A1, 8, 0, 0>, BwdLay16::BYTES);
+      attn_bwd_bf16_kernel<MODE_A1, 8, 0, 0><<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
+    } else
+#endif
+    {
+      tm_allow_smem(attn_bwd_bf16_kernel<MODE_A1>, BwdLay16::BYTES);
+      attn_bwd_bf16_kernel<MODE_A1><<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
+    }
   } else {
     TM_DTYPE_DISPATCH(dtype, (tm_allow_smem(attn_bwd_kernel<T, MODE_A1>, bwd_smem_bytes<T>()),
                               attn_bwd_kernel<T, MODE_A1><<<dim3(nqc, nbh), 512, bwd_smem_bytes<T>(), st>>>(a)));
@@ -2532,6 +2569,11 @@ void launch_a3_bwd_bf16(BwdArgs& a, int nbh, int n, hipStream_t st, int& slabs) 
     if (NYS_VARIANT == 31) {   // diagnostic: stamps inside query chunk 2
       tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9, 2>, BwdLay9::BYTES);
       attn_bwd_bf16_kernel<MODE_A3, 9, 2><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
+      return;
+    }
+    if (NYS_VARIANT == 35) {   // diagnostic: the earlier cross-wave dQ form
+      tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9, 0, 0>, BwdLay9::BYTES);
+      attn_bwd_bf16_kernel<MODE_A3, 9, 0, 0><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
       return;
     }
 #endif
