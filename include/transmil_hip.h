@@ -105,6 +105,14 @@ int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const float* gam
                      const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
                      int resid_cls_only, float* dx_accum, float* work, float* dgamma, float* dbeta,
                      tm_reduce_queue* rq, void* stream);
+/* tm_layernorm_bwd with a per-segment addend on dy: row t of bag b reads dy + seg_add[b][(pad + t) /
+ * seg_len] (+ seg_add[b][nseg] at t = 0, the class row); seg_add is [B][seg_rows][D] fp32 (the
+ * scale * Aq Wq rows of tm_cls_q_rows' products, seg_rows = 288, nseg = 256) */
+int tm_layernorm_bwd_seg(const void* dy, int dtype, const float* x, const float* gamma, const float* mean,
+                         const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
+                         int resid_cls_only, const float* seg_add, int seg_len, int nseg, int seg_rows,
+                         float* dx_accum, float* work, float* dgamma, float* dbeta, tm_reduce_queue* rq,
+                         void* stream);
 int tm_head_fwd(const float* h, int B, int S, int D, const float* gamma, const float* beta, float eps,
                 const float* W, const float* bias, int C, float* logits, float* xhat, float* rstd,
                 void* stream);
@@ -382,6 +390,17 @@ int tm_cls_head_out_bwd(int dtype, const float* prob, const long long* label, co
 int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, const void* v, const void* kl_t, const void* y_t,
                       const float* lse1, const float* wconv, int B, int nh, int n, int r, float* dq, float* dkl,
                       float* dy, float* dv, float* dwconv, void* stream);
+/* bf16 mode: layer 2's q enters the loss only through its landmark means q~ (App. A eq. 4) and the
+ * class row r, so dL/dq = dq~[t / l] / l on every row t plus the class row's own term, and the q
+ * part of to_qkv's backward is two small products instead of a dense q block in dqkv:
+ *   dWq = scale * Aq^T Xs,   dxn[t] += scale * (Aq Wq)[t / l] (+ row NL at t = r)
+ * (tm_bmm, then tm_layernorm_bwd_seg).  This writes their operands, [B][288][nh*64] fp32 each:
+ *   Aq rows j < 256: (dql + sum_p slab[p])[b*nh + h][j][d] / l at column h*64 + d (slab: the
+ *   nslabs [B*nh][256][64] partials tm_nys_a3_bwd_fused leaves in its work), row 256: dq[b*nh+h][r][d];
+ *   Xs rows j < 256: sum over the segment's rows of xn[b] (bf16 [B][n][nh*64], pad rows zero),
+ *   row 256: xn[b][r]; rows 257..287 of both: zeros (operand rows to a multiple of 32). */
+int tm_cls_q_rows(const float* dql, const float* slab, int nslabs, const float* dq, const void* xn, int B, int nh,
+                  int n, int r, float* Aq, float* Xs, void* stream);
 
 /* fp32 -> dtype copies of up to 8 tensors (per-step bf16 GEMM weight operands) in one launch;
  * offset[] = prefix sums of the element counts, offset[0] = 0 */

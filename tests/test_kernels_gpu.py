@@ -677,3 +677,33 @@ def test_assemble_q_slab_reduces_the_a3_partials(dtype, dq_row, B, n):
     tol = 1e-5 if dtype == torch.float32 else 8e-3
     assert _rel(got, ref) < tol
     assert (dqkv[:, :, nh * 64:] == 7).all()
+
+
+# ----------------------------------------------------------------------------- class-row q operands
+@pytest.mark.parametrize("B,n,nslabs", [(1, 8448, 32), (2, 1024, 5), (1, 256, 0)])
+def test_cls_q_rows_against_torch(B, n, nslabs):
+    """tm_cls_q_rows: Aq rows = (dql + sum of the slabs) / l per landmark, the class row's dq; Xs
+    rows = the segment sums of the bf16 LayerNorm output, the class row; zero rows past 257."""
+    L = _lib()
+    from transmil_deepgraft_amd.engine import _p, _stream, QROWS
+    nh, D, NL = 8, 512, 256
+    nbh, l, r = B * nh, n // 256, n // 3
+    g = torch.Generator(device="cpu").manual_seed(n + nslabs)
+    dql = torch.randn(nbh, NL, 64, generator=g).to(DEV)
+    slab = torch.randn(max(nslabs, 1), nbh, NL, 64, generator=g).to(DEV)
+    dq = torch.randn(nbh, n, 64, generator=g).to(DEV)
+    xn = torch.randn(B, n, D, generator=g).to(torch.bfloat16).to(DEV)
+    Aq = torch.full((B, QROWS, D), float("nan"), device=DEV)
+    Xs = torch.full((B, QROWS, D), float("nan"), device=DEV)
+    L.call("tm_cls_q_rows", _p(dql), _p(slab), nslabs, _p(dq), _p(xn), B, nh, n, r, _p(Aq), _p(Xs), _stream())
+    torch.cuda.synchronize()
+    tot = (dql.double() + slab[:nslabs].double().sum(0)) / l                     # [nbh][256][64]
+    ea = torch.zeros(B, QROWS, D, dtype=torch.float64)
+    ex = torch.zeros(B, QROWS, D, dtype=torch.float64)
+    for b in range(B):
+        ea[b, :NL] = tot[b * nh:(b + 1) * nh].permute(1, 0, 2).reshape(NL, D).cpu()
+        ea[b, NL] = dq[b * nh:(b + 1) * nh, r].reshape(D).double().cpu()
+        ex[b, :NL] = xn[b].double().view(NL, l, D).sum(1).cpu()
+        ex[b, NL] = xn[b, r].double().cpu()
+    assert _rel(Aq.cpu(), ea) < 1e-6 and _rel(Xs.cpu(), ex) < 1e-6
+    assert (Aq[:, NL + 1:] == 0).all() and (Xs[:, NL + 1:] == 0).all()

@@ -470,3 +470,31 @@ def test_last_layer_class_row_path_equals_dense(dtype, tol, train, monkeypatch):
         if err > tol:
             bad.append((name, err))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("N,B", [(8192, 1), (1000, 2)])
+def test_class_row_q_products_equal_dense_q_block(N, B, monkeypatch):
+    """bf16 class-row layer 2: the q part of to_qkv's backward as two small products on
+    tm_cls_q_rows' operands (dWq = scale Aq^T Xs, dxn += scale Aq Wq by segment in the LayerNorm
+    backward; engine.CLS_Q_ROWS) against the dense q block of dqkv through the K = 3D GEMMs:
+    logits bitwise (the forward is shared), every parameter gradient within 2e-2 of its largest
+    entry (the dense path rounds dq and the q part of dxn to bf16; the products keep fp32)."""
+    from transmil_deepgraft_amd import engine as E
+    _, ours = _pair(2, dtype=torch.bfloat16)
+    ours.train()
+    x = torch.from_numpy(bag_input(N, 512, 9 + N, B))
+    c0 = ours._dropout_counter.clone()
+    outs = []
+    for on in (True, False):
+        monkeypatch.setattr(E, "CLS_Q_ROWS", on)
+        ours._dropout_counter.copy_(c0)
+        ours.zero_grad(set_to_none=True)
+        outs.append(_ours_forward_backward(ours, x, 1, 2))
+    (lq, gq), (ld, gd) = outs
+    assert torch.equal(lq, ld)
+    bad = []
+    for name, g in gd.items():
+        err = ((gq[name].double() - g.double()).abs().max() / g.double().abs().max().clamp_min(1e-12)).item()
+        if err > 2e-2:
+            bad.append((name, err))
+    assert not bad, bad

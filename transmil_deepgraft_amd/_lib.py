@@ -73,6 +73,7 @@ _SIGS = {
     "tm_layernorm_fwd": (I, [P, P, P, Fl, I, I, I, I, I, I, P, P, P, P]),
     "tm_layernorm_bwd_workspace": (L, [I, I, I]),
     "tm_layernorm_bwd": (I, [P, I, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P]),
+    "tm_layernorm_bwd_seg": (I, [P, I, P, P, P, P, I, I, I, I, I, I, I, P, I, I, I, P, P, P, P, P, P]),
     "tm_head_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P]),
     "tm_head_bwd": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P]),
     "tm_head_ce_fwd": (I, [P, I, I, I, P, P, Fl, P, P, I, P, P, P, P, P, P, P, P, P]),
@@ -144,6 +145,7 @@ _SIGS = {
     "tm_cls_out_bwd": (I, [I, P, P, P, I, I, I, I, I, Fl, U64, P, P, P, P, P]),
     "tm_cls_head_out_bwd": (I, [I, P, P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, Fl, U64, P, P, P, P, P]),
     "tm_cls_a1_row_bwd": (I, [I, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P]),
+    "tm_cls_q_rows": (I, [P, P, I, P, P, I, I, I, I, P, P, P]),
     "tm_pad_rows": (I, [I, P, I, I, I, I, I, P, P]),
     "tm_fc1_gelu_bwd": (I, [I, P, P, I, I, I, I, I, P, P, P]),
     "tm_gelu_bwd": (I, [I, P, P, L, P, P]),

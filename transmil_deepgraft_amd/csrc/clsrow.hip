@@ -350,6 +350,80 @@ __global__ __launch_bounds__(256) void a1_row_bwd_kernel(const T* __restrict__ d
   }
 }
 
+// The q operands of the class-row layer's q-part products (bf16 mode; see tm_cls_q_rows in the
+// header).  Block (j, b), thread c = column (head c / 64, dim c % 64) of one operand row.
+constexpr int QROWS = NL + 32;   // rows per bag: NL landmark rows, the class row, zero rows to a multiple of 32
+// 512 threads, D = nh * 64 = 512 columns (host-checked).  Every load of the block is issued before
+// the first add (16-B pieces): slab rows as 4 slab groups x 128 threads x 4 columns, segment rows as
+// 8 row groups x 64 threads x 8 columns; the groups' partial sums are combined through LDS in a
+// fixed order.
+constexpr int QR_SLABS = 64;     // slabs per call (host-checked): 16 pieces per thread
+__global__ __launch_bounds__(512) void cls_q_rows_kernel(const float* __restrict__ dql, const float* __restrict__ slab,
+                                                         int nslabs, const float* __restrict__ dq,
+                                                         const bf16* __restrict__ xn, int nh, int n, int r,
+                                                         float* __restrict__ Aq, float* __restrict__ Xs) {
+  constexpr int D = 512;
+  __shared__ f32x4 sred[4][128];
+  __shared__ float xred[8][D];
+  const int j = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int l = n / NL;
+  float* aout = Aq + ((size_t)b * QROWS + j) * D;
+  float* xout = Xs + ((size_t)b * QROWS + j) * D;
+  if (j > NL) {   // zero operand rows (block-uniform)
+    aout[tid] = 0.f;
+    xout[tid] = 0.f;
+    return;
+  }
+  if (j == NL) {  // the class row
+    const int hh = tid >> 6, d = tid & 63;
+    aout[tid] = dq[(((size_t)b * nh + hh) * n + r) * DH + d];
+    xout[tid] = (float)xn[((size_t)b * n + r) * D + tid];
+    return;
+  }
+  // slab pieces: group g = tid / 128 takes slabs g, g + 4, ..; thread column c4 = 4 (tid % 128)
+  const int g = tid >> 7, c4 = (tid & 127) * 4, hh = c4 >> 6, d = c4 & 63;
+  const size_t ss = (size_t)gridDim.y * nh * NL * DH;
+  const size_t o = (((size_t)b * nh + hh) * NL + j) * DH + d;
+  f32x4 sp[QR_SLABS / 4];
+#pragma unroll
+  for (int i = 0; i < QR_SLABS / 4; ++i) {
+    const int p = g + 4 * i;
+    sp[i] = p < nslabs ? *(const f32x4*)(slab + p * ss + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  // segment rows: group g8 = tid / 64 takes rows g8, g8 + 8, ..; thread columns 8 (tid % 64)
+  const int g8 = tid >> 6, c8 = (tid & 63) * 8;
+  const bf16* xr = xn + ((size_t)b * n + (size_t)j * l) * D + c8;
+  constexpr int XR = 8;          // rows per group in one burst (l <= 64, host-checked)
+  bf16x8 xp[XR];
+#pragma unroll
+  for (int i = 0; i < XR; ++i) {
+    const int t = g8 + 8 * i;
+    xp[i] = t < l ? *(const bf16x8*)(xr + (size_t)t * D) : (bf16x8){};
+  }
+  f32x4 s = sp[0];
+#pragma unroll
+  for (int i = 1; i < QR_SLABS / 4; ++i) s += sp[i];
+  float x8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x8[e] = (float)xp[0][e];
+#pragma unroll
+  for (int i = 1; i < XR; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x8[e] += (float)xp[i][e];
+  sred[g][tid & 127] = s;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) xred[g8][c8 + e] = x8[e];
+  __syncthreads();
+  if (tid < 128) {
+    const f32x4 q = *(const f32x4*)(dql + o) + ((sred[0][tid] + sred[1][tid]) + (sred[2][tid] + sred[3][tid]));
+    *(f32x4*)(aout + c4) = q / (float)l;
+  }
+  float xs = xred[0][tid];
+#pragma unroll
+  for (int i = 1; i < 8; ++i) xs += xred[i][tid];
+  xout[tid] = xs;
+}
+
 }  // namespace
 
 #define TM_CLS_DISPATCH(dt, CALL)                                 \
@@ -425,6 +499,18 @@ extern "C" int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, 
   TM_CLS_DISPATCH(dtype, (a1_row_bwd_kernel<T><<<dim3(B * nh, 4), 256, 0, (hipStream_t)stream>>>(
                              (const T*)dmerged, (const T*)q, (const T*)v, (const T*)kl_t, (const T*)y_t, lse1, wconv,
                              B, nh, n, r, dq, dkl, dy, dv, dwconv)));
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_cls_q_rows(const float* dql, const float* slab, int nslabs, const float* dq, const void* xn, int B,
+                             int nh, int n, int r, float* Aq, float* Xs, void* stream) {
+  TM_REQUIRE(dql && dq && xn && Aq && Xs && B > 0 && nh * DH == 512 && (nslabs == 0 || slab),
+             "cls_q_rows: bad args (nh * 64 must be 512)");
+  TM_REQUIRE(n % NL == 0 && n / NL <= 64 && r >= 0 && r < n && nslabs >= 0 && nslabs <= QR_SLABS,
+             "cls_q_rows: bad row / n / slab count");
+  cls_q_rows_kernel<<<dim3(QROWS, B), 512, 0, (hipStream_t)stream>>>(dql, slab, nslabs, dq, (const bf16*)xn, nh, n, r,
+                                                                     Aq, Xs);
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -83,12 +83,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 // dx accumulated into dx_accum (fp32, [rows, D]); dy read from the padded layout.
 // Each block handles `rows_per_block` rows (4 waves interleaved) and writes one
 // partial row of dgamma / dbeta: part[2][nblocks][D].
-template <typename T, int VPL>
+// SEG: dy of row t (bag b) + seg[b][(pad + t) / len] (+ seg[b][nseg] at t = 0): the class-row
+// layer's q-part gradient rows (tm_layernorm_bwd_seg)
+struct SegAdd { const float* p; int len, nseg, rows; };
+template <typename T, int VPL, bool SEG = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ gamma, const float* __restrict__ mean,
                                                      const float* __restrict__ rstd, int rows, int S, int n_pad, int pad,
                                                      int rows_per_block, int resid_cls_only, float* __restrict__ dx_accum,
-                                                     float* __restrict__ part) {
+                                                     float* __restrict__ part, SegAdd sg = SegAdd{nullptr, 1, 0, 0}) {
   constexpr int D = VPL * 64;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float dg[VPL], db[VPL], gm[VPL];
@@ -97,10 +100,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
   // software pipeline: the next row's dy, x, mean/rstd and dx_accum are requested before
   // this row is processed (one HBM round trip in flight instead of one per row)
-  auto fetch = [&](int r, float (&g)[VPL], float (&xv)[VPL], float (&acc)[VPL], float& mu, float& rs) {
+  auto fetch = [&](int r, float (&g)[VPL], float (&xv)[VPL], float (&acc)[VPL], float& mu, float& rs,
+                   float (&sa)[VPL]) {
     const int rr = min(r, rows - 1);
     const int b = rr / S, t = rr % S;
     load_row_t<T, VPL>(g, dy + ((size_t)b * n_pad + pad + t) * D, lane);
+    if constexpr (SEG) {
+      load_row<VPL>(sa, sg.p + ((size_t)b * sg.rows + (pad + t) / sg.len) * D, lane);
+      if (t == 0) {   // the class row also carries its own q term (one row per bag: a waited load)
+        float sc[VPL];
+        load_row<VPL>(sc, sg.p + ((size_t)b * sg.rows + sg.nseg) * D, lane);
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) sa[i] += sc[i];
+      }
+    }
     load_row<VPL>(xv, x + (size_t)rr * D, lane);
     if (!resid_cls_only || t == 0) {
       load_row<VPL>(acc, dx_accum + (size_t)rr * D, lane);
@@ -111,13 +124,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     mu = mean[rr];
     rs = rstd[rr];
   };
-  float g[VPL], xv[VPL], dacc[VPL], mu, rs;
+  float g[VPL], xv[VPL], dacc[VPL], sa[VPL], mu, rs;
   int r = r0 + wave;
-  if (r < r1) fetch(r, g, xv, dacc, mu, rs);
+  if (r < r1) fetch(r, g, xv, dacc, mu, rs, sa);
   for (; r < r1; r += 4) {
-    float g2[VPL], xv2[VPL], dacc2[VPL], mu2 = 0.f, rs2 = 0.f;
+    float g2[VPL], xv2[VPL], dacc2[VPL], sa2[VPL], mu2 = 0.f, rs2 = 0.f;
     const bool more = r + 4 < r1;
-    if (more) fetch(r + 4, g2, xv2, dacc2, mu2, rs2);
+    if (more) fetch(r + 4, g2, xv2, dacc2, mu2, rs2, sa2);
+    if constexpr (SEG) {
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) g[i] += sa[i];
+    }
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
@@ -145,7 +162,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
     }
     if (more) {
 #pragma unroll
-      for (int i = 0; i < VPL; ++i) { g[i] = g2[i]; xv[i] = xv2[i]; dacc[i] = dacc2[i]; }
+      for (int i = 0; i < VPL; ++i) { g[i] = g2[i]; xv[i] = xv2[i]; dacc[i] = dacc2[i]; sa[i] = sa2[i]; }
       mu = mu2;
       rs = rs2;
     }
@@ -482,6 +499,28 @@ extern "C" int tm_layernorm_bwd(const void* dy, int dtype, const float* x, const
     TM_VPL_DISPATCH(D, (ln_bwd_kernel<float, VPL><<<nb, 256, 0, st>>>((const float*)dy, x, gamma, mean, rstd, rows,
                                                                       S, n_pad, pad, rows_per_block, resid_cls_only, dx_accum, work)));
   }
+  TM_CHECK_LAUNCH();
+  int rc = tm_splitk_reduce(work, dgamma, nb, D, 1.0f, 0, rq, stream);
+  if (rc) return rc;
+  return tm_splitk_reduce(work + (size_t)nb * D, dbeta, nb, D, 1.0f, 0, rq, stream);
+}
+
+extern "C" int tm_layernorm_bwd_seg(const void* dy, int dtype, const float* x, const float* gamma, const float* mean,
+                                    const float* rstd, int rows, int D, int S, int n_pad, int pad, int rows_per_block,
+                                    int resid_cls_only, const float* seg_add, int seg_len, int nseg, int seg_rows,
+                                    float* dx_accum, float* work, float* dgamma, float* dbeta, tm_reduce_queue* rq,
+                                    void* stream) {
+  TM_REQUIRE(dy && x && gamma && mean && rstd && dx_accum && work && dgamma && dbeta && seg_add,
+             "layernorm_bwd_seg: null arg");
+  TM_REQUIRE(rows_per_block > 0 && S > 0 && seg_len > 0 && nseg >= 0 && seg_rows > nseg, "layernorm_bwd_seg: bad args");
+  TM_REQUIRE((long long)(pad + S - 1) / seg_len < nseg && pad + S <= n_pad, "layernorm_bwd_seg: rows past the segments");
+  TM_REQUIRE(dtype == TM_BF16, "layernorm_bwd_seg: bf16 dy only");
+  const int nb = (rows + rows_per_block - 1) / rows_per_block;
+  hipStream_t st = (hipStream_t)stream;
+  const SegAdd sg{seg_add, seg_len, nseg, seg_rows};
+  TM_VPL_DISPATCH(D, (ln_bwd_kernel<bf16, VPL, true><<<nb, 256, 0, st>>>((const bf16*)dy, x, gamma, mean, rstd, rows, S,
+                                                                         n_pad, pad, rows_per_block, resid_cls_only,
+                                                                         dx_accum, work, sg)));
   TM_CHECK_LAUNCH();
   int rc = tm_splitk_reduce(work, dgamma, nb, D, 1.0f, 0, rq, stream);
   if (rc) return rc;

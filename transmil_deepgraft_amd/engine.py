@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -30,6 +31,10 @@ DH = 64         # dim_head
 TAPS = 33       # residual conv
 PINV_ITERS = 6
 LN_EPS = 1e-5
+QROWS = NL + 32  # rows per bag of tm_cls_q_rows' operands (landmarks, class row, zero rows to 32 | rows)
+# bf16 class-row layer: the q part of to_qkv's backward as two small products (TM_CLS_Q_ROWS=0: the
+# dense q block of dqkv, for A/B runs and the equivalence test)
+CLS_Q_ROWS = os.environ.get("TM_CLS_Q_ROWS", "1") != "0"
 
 
 class _Probe:
@@ -406,9 +411,11 @@ def nystrom_core_forward(qkv, geo: Geometry, wconv, tdtype, dt_code, pool, cls_r
 
 
 def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdtype, dt_code, pool,
-                          dwconv_out, scale, cls_row=None):
-    """Backward of nystrom_core_forward: returns dqkv [B, n, 3*h*64] (T); writes dwconv_out.
-    ``cls_row``: dmerged is [B, h*64], the only non-zero row (``cls_row``) of the dense gradient."""
+                          dwconv_out, scale, cls_row=None, xn=None):
+    """Backward of nystrom_core_forward: returns (dqkv [B, n, 3*h*64] (T), qrows); writes dwconv_out.
+    ``cls_row``: dmerged is [B, h*64], the only non-zero row (``cls_row``) of the dense gradient.
+    ``xn`` (bf16 class-row layer): the q block of dqkv is NOT written; qrows = (Aq, Xs), the
+    operands of the q part's two small products (tm_cls_q_rows), else qrows = None."""
     n, nbh, nh = geo.n, geo.nbh, geo.heads
     q, k, v = qkv[0], qkv[1], qkv[2]
     st = _stream()
@@ -513,15 +520,23 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         if cls_row is None:
             _lib.call("tm_nys_assemble_q_slab_inplace", _p(dql), _p(work3), slabs, geo.B, nh, n, C.c_float(scale),
                       _p(dqkv), st)
+        elif xn is not None:
+            qr = pool(2 * geo.B * QROWS * nh * DH)
+            Aq, Xs = qr[:geo.B * QROWS * nh * DH].view(geo.B, QROWS, nh * DH), qr[geo.B * QROWS * nh * DH:].view(
+                geo.B, QROWS, nh * DH)
+            with probe("cls_q_rows"):
+                _lib.call("tm_cls_q_rows", _p(dql), _p(work3), slabs, _p(dq), _p(xn), geo.B, nh, n, cls_row, _p(Aq),
+                          _p(Xs), st)
+            return dqkv, (Aq, Xs)
         else:
             _lib.call("tm_nys_assemble_q_slab", dt_code, _p(dq), cls_row, _p(dql), _p(work3), slabs, geo.B, nh, n,
                       C.c_float(scale), _p(dqkv), st)
-        return dqkv
+        return dqkv, None
     bmm([bmm_job(ds2, 0, state["kl"], 0, dql, NL, DH, NL, E1=dql3, e1=1.0),
          bmm_job(ds2, 1, state["ql"], 0, dkl, NL, DH, NL, E1=dkl, e1=1.0)], nbh, prec)
     _lib.call("tm_nys_assemble_dqkv", dt_code, _p(dq), _p(dql), _p(dk), _p(dkl), _p(dv), geo.B, nh, n,
               C.c_float(scale), _p(dqkv), st)
-    return dqkv
+    return dqkv, None
 
 
 # ----------------------------------------------------------------------------- TransLayer
@@ -589,24 +604,55 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
         dmerged = pool(B * n * D, tdtype).view(B, n, D)
         with probe("dmerged_gemm"):
             gemm(dout, prm["wo"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
-    dqkv = nystrom_core_backward(dmerged, saved["merged"], saved["qkv"], saved["core"], geo, prm["wconv"],
-                                 tdtype, dt_code, pool, grads["wconv"], DH ** -0.5,
-                                 cls_row=pad if saved["cls_only"] else None)
-    # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
-    with defer_reductions(), probe("wgrad_qkv"):
-        weight_grad(dqkv, saved["xn"], grads["wqkv"], 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
-                    work_pool=pool)
+    # bf16 class-row layer: q reaches the loss only through its landmark means and the class row, so
+    # the q part of to_qkv's backward runs as two small products on tm_cls_q_rows' operands
+    qrows_on = (CLS_Q_ROWS and saved["cls_only"] and dt_code == BF16 and saved["core"]["a2s"] is not None
+                and "wqkv_f32" in prm)
+    dqkv, qrows = nystrom_core_backward(dmerged, saved["merged"], saved["qkv"], saved["core"], geo, prm["wconv"],
+                                        tdtype, dt_code, pool, grads["wconv"], DH ** -0.5,
+                                        cls_row=pad if saved["cls_only"] else None,
+                                        xn=saved["xn"] if qrows_on else None)
     dxn = pool(B * n * D, tdtype).view(B, n, D)
+    rpb = 8     # LN backward: 2 rows per wave, both requested up front (the partials go through the deferred reduce)
+    if qrows is None:
+        # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
+        with defer_reductions(), probe("wgrad_qkv"):
+            weight_grad(dqkv, saved["xn"], grads["wqkv"], 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
+                        work_pool=pool)
+        with probe("dxn_gemm"):
+            gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
+        # LayerNorm backward, accumulated into dH (residual branch already there)
+        with defer_reductions():
+            work = pool(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4)
+            _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
+                      _p(saved["rstd"]), B * S, D, S, n, pad, rpb, int(saved["cls_only"]), _p(dH), _p(work),
+                      _p(grads["norm_w"]),
+                      _p(grads["norm_b"]), _rq(), st)
+        return
+    # k / v parts: dW_kv = dqkv_kv^T xn, dxn = dqkv_kv W_kv (K = 2D instead of 3D)
+    dkv = dqkv.view(B * n, 3 * D)[:, D:]
+    with defer_reductions(), probe("wgrad_qkv"):
+        weight_grad(dkv, saved["xn"], grads["wqkv"][D:], 2 * D, D, B * n, ldy=3 * D, ldx=D, dtype=dt_code,
+                    work_pool=pool)
     with probe("dxn_gemm"):
-        gemm(dqkv, prm["wqkv"], dxn, B * n, D, 3 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
-    # LayerNorm backward, accumulated into dH (residual branch already there)
-    rpb = 8     # 2 rows per wave, both requested up front (the partials go through the deferred reduce)
+        gemm(dkv, prm["wqkv"][D:], dxn, B * n, D, 2 * D, lda=3 * D, ldb=D, ldc=D, b_kn=1, dtype=dt_code)
+    # q part: dWq = scale Aq^T Xs ; G = scale Aq Wq (its rows added to dxn by segment in the LN backward)
+    Aq, Xs = qrows
+    scale = DH ** -0.5
+    wq = prm["wqkv_f32"][:D]
+    gwq = grads["wqkv"][:D]
+    G = pool(B * QROWS * D).view(B, QROWS, D)
+    with probe("cls_q_products"):
+        jobs = [bmm_job(Aq.view(B * QROWS, D), 0, wq, 0, G.view(B * QROWS, D), B * QROWS, D, D, alpha=scale),
+                bmm_job(Aq[0], 1, Xs[0], 0, gwq, D, D, QROWS, alpha=scale)]
+        bmm(jobs, 1, 1)
+        for b in range(1, B):   # K <= 512 per product: one bag at a time, accumulated
+            bmm([bmm_job(Aq[b], 1, Xs[b], 0, gwq, D, D, QROWS, alpha=scale, E1=gwq, e1=1.0)], 1, 1)
     with defer_reductions():
         work = pool(_lib.query("tm_layernorm_bwd_workspace", B * S, D, rpb) // 4)
-        _lib.call("tm_layernorm_bwd", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
-                  _p(saved["rstd"]), B * S, D, S, n, pad, rpb, int(saved["cls_only"]), _p(dH), _p(work),
-                  _p(grads["norm_w"]),
-                  _p(grads["norm_b"]), _rq(), st)
+        _lib.call("tm_layernorm_bwd_seg", _p(dxn), dt_code, _p(H_in), _p(prm["norm_w"]), _p(saved["mean"]),
+                  _p(saved["rstd"]), B * S, D, S, n, pad, rpb, int(saved["cls_only"]), _p(G), n // NL, NL, QROWS,
+                  _p(dH), _p(work), _p(grads["norm_w"]), _p(grads["norm_b"]), _rq(), st)
 
 
 # ----------------------------------------------------------------------------- whole model
@@ -712,6 +758,7 @@ class TransMILEngine:
             p[li] = {
                 "norm_w": params[pre + "norm.weight"], "norm_b": params[pre + "norm.bias"],
                 "wqkv": wqkv,
+                "wqkv_f32": params[pre + "attn.to_qkv.weight"].contiguous(),
                 "wo": wo,
                 "bo": params[pre + "attn.to_out.0.bias"],
                 "wconv": params[pre + "attn.res_conv.weight"].contiguous(),
@@ -989,8 +1036,8 @@ class NystromEngine:
         dmerged = pool(B * n * D, self.tdtype).view(B, n, D)
         gemm(dpad, ctx["wo_t"], dmerged, B * n, D, D, lda=D, ldb=D, ldc=D, b_kn=1, dtype=self.dt_code)
         dwconv = torch.empty_like(ctx["wconv"], dtype=torch.float32)
-        dqkv = nystrom_core_backward(dmerged, ctx["merged"], ctx["qkv"], ctx["core"], geo, ctx["wconv"],
-                                     self.tdtype, self.dt_code, pool, dwconv, DH ** -0.5)
+        dqkv, _ = nystrom_core_backward(dmerged, ctx["merged"], ctx["qkv"], ctx["core"], geo, ctx["wconv"],
+                                        self.tdtype, self.dt_code, pool, dwconv, DH ** -0.5)
         dwqkv = torch.empty(3 * D, D, dtype=torch.float32, device=dout.device)
         weight_grad(dqkv, ctx["xp"], dwqkv, 3 * D, D, B * n, ldy=3 * D, ldx=D, dtype=self.dt_code, work_pool=pool)
         dx = torch.empty(B, S, D, dtype=torch.float32, device=dout.device)
