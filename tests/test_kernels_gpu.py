@@ -680,7 +680,7 @@ def test_assemble_q_slab_reduces_the_a3_partials(dtype, dq_row, B, n):
 
 
 # ----------------------------------------------------------------------------- class-row q operands
-@pytest.mark.parametrize("B,n,nslabs", [(1, 8448, 32), (2, 1024, 5), (1, 256, 0)])
+@pytest.mark.parametrize("B,n,nslabs", [(1, 8448, 32), (2, 1024, 5), (1, 256, 0), (1, 33024, 70)])
 def test_cls_q_rows_against_torch(B, n, nslabs):
     """tm_cls_q_rows: Aq rows = (dql + sum of the slabs) / l per landmark, the class row's dq; Xs
     rows = the segment sums of the bf16 LayerNorm output, the class row; zero rows past 257."""

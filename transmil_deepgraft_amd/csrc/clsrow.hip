@@ -357,7 +357,7 @@ constexpr int QROWS = NL + 32;   // rows per bag: NL landmark rows, the class ro
 // the first add (16-B pieces): slab rows as 4 slab groups x 128 threads x 4 columns, segment rows as
 // 8 row groups x 64 threads x 8 columns; the groups' partial sums are combined through LDS in a
 // fixed order.
-constexpr int QR_SLABS = 64;     // slabs per call (host-checked): 16 pieces per thread
+constexpr int QR_SLABS = 64;     // slabs per burst: 16 pieces per thread
 __global__ __launch_bounds__(512) void cls_q_rows_kernel(const float* __restrict__ dql, const float* __restrict__ slab,
                                                          int nslabs, const float* __restrict__ dq,
                                                          const bf16* __restrict__ xn, int nh, int n, int r,
@@ -380,36 +380,38 @@ __global__ __launch_bounds__(512) void cls_q_rows_kernel(const float* __restrict
     xout[tid] = (float)xn[((size_t)b * n + r) * D + tid];
     return;
   }
-  // slab pieces: group g = tid / 128 takes slabs g, g + 4, ..; thread column c4 = 4 (tid % 128)
+  // slab pieces: group g = tid / 128 takes slabs g, g + 4, ..; thread column c4 = 4 (tid % 128);
+  // bursts of QR_SLABS slabs (one at the bench shape)
   const int g = tid >> 7, c4 = (tid & 127) * 4, hh = c4 >> 6, d = c4 & 63;
   const size_t ss = (size_t)gridDim.y * nh * NL * DH;
   const size_t o = (((size_t)b * nh + hh) * NL + j) * DH + d;
-  f32x4 sp[QR_SLABS / 4];
-#pragma unroll
-  for (int i = 0; i < QR_SLABS / 4; ++i) {
-    const int p = g + 4 * i;
-    sp[i] = p < nslabs ? *(const f32x4*)(slab + p * ss + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
-  // segment rows: group g8 = tid / 64 takes rows g8, g8 + 8, ..; thread columns 8 (tid % 64)
+  // segment rows: group g8 = tid / 64 takes rows g8, g8 + 8, ..; thread columns 8 (tid % 64);
+  // bursts of 64 rows (one at the bench shape, l = 33)
   const int g8 = tid >> 6, c8 = (tid & 63) * 8;
   const bf16* xr = xn + ((size_t)b * n + (size_t)j * l) * D + c8;
-  constexpr int XR = 8;          // rows per group in one burst (l <= 64, host-checked)
-  bf16x8 xp[XR];
+  constexpr int XR = 8;
+  f32x4 s = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float x8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p0 = 0, t0 = 0; p0 < nslabs || t0 < l; p0 += QR_SLABS, t0 += 8 * XR) {
+    f32x4 sp[QR_SLABS / 4];
 #pragma unroll
-  for (int i = 0; i < XR; ++i) {
-    const int t = g8 + 8 * i;
-    xp[i] = t < l ? *(const bf16x8*)(xr + (size_t)t * D) : (bf16x8){};
+    for (int i = 0; i < QR_SLABS / 4; ++i) {
+      const int p = p0 + g + 4 * i;
+      sp[i] = p < nslabs ? *(const f32x4*)(slab + p * ss + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    bf16x8 xp[XR];
+#pragma unroll
+    for (int i = 0; i < XR; ++i) {
+      const int t = t0 + g8 + 8 * i;
+      xp[i] = t < l ? *(const bf16x8*)(xr + (size_t)t * D) : (bf16x8){};
+    }
+#pragma unroll
+    for (int i = 0; i < QR_SLABS / 4; ++i) s += sp[i];
+#pragma unroll
+    for (int i = 0; i < XR; ++i)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x8[e] += (float)xp[i][e];
   }
-  f32x4 s = sp[0];
-#pragma unroll
-  for (int i = 1; i < QR_SLABS / 4; ++i) s += sp[i];
-  float x8[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) x8[e] = (float)xp[0][e];
-#pragma unroll
-  for (int i = 1; i < XR; ++i)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) x8[e] += (float)xp[i][e];
   sred[g][tid & 127] = s;
 #pragma unroll
   for (int e = 0; e < 8; ++e) xred[g8][c8 + e] = x8[e];
@@ -507,8 +509,7 @@ extern "C" int tm_cls_q_rows(const float* dql, const float* slab, int nslabs, co
                              int nh, int n, int r, float* Aq, float* Xs, void* stream) {
   TM_REQUIRE(dql && dq && xn && Aq && Xs && B > 0 && nh * DH == 512 && (nslabs == 0 || slab),
              "cls_q_rows: bad args (nh * 64 must be 512)");
-  TM_REQUIRE(n % NL == 0 && n / NL <= 64 && r >= 0 && r < n && nslabs >= 0 && nslabs <= QR_SLABS,
-             "cls_q_rows: bad row / n / slab count");
+  TM_REQUIRE(n % NL == 0 && r >= 0 && r < n && nslabs >= 0, "cls_q_rows: bad row / n / slab count");
   cls_q_rows_kernel<<<dim3(QROWS, B), 512, 0, (hipStream_t)stream>>>(dql, slab, nslabs, dq, (const bf16*)xn, nh, n, r,
                                                                      Aq, Xs);
   TM_CHECK_LAUNCH();
