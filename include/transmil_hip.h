@@ -328,6 +328,10 @@ int tm_add_relu(int dtype, const void* a, const void* b, void* y, long long coun
 /* y[r, c] = act(y[r, c] + bias[c]) in place over rows x C channels-last (C % 8 == 0; act = ReLU
  * when relu != 0): a 3x3 convolution's folded conv+BN bias + ReLU (ResNet.py:95-104) in one pass */
 int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int relu, void* stream);
+/* ResNet stem tail (ResNet.py:240-245, BN folded into the convolution's bias): out[N, OH, OW, C] =
+ * maxpool3x3/2 pad 1 (relu(y + bias)) over the raw channels-last bf16 stem output y[N, H, W, C],
+ * OH = (H - 1) / 2 + 1; one pass instead of the in-place bias + ReLU and a max-pool launch */
+int tm_bias_relu_maxpool(const void* y, const void* bias, void* out, int N, int H, int W, int C, void* stream);
 /* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
  * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout])
  * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.

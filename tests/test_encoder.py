@@ -391,3 +391,21 @@ def test_c5_train_mode_bn_4096_tiles(monkeypatch):
     got = feats[idx.cuda()].double().cpu()
     err = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
     assert err < 2e-3, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h", [(3, 112), (2, 15)])
+def test_stem_bias_relu_maxpool_equals_bias_act_then_pool(n, h):
+    """tm_bias_relu_maxpool against tm_bias_act + max_pool2d (the two-pass eval stem tail),
+    channels-last bf16, odd and even sizes: bitwise."""
+    import torch.nn.functional as F
+    from transmil_deepgraft_amd import encoder as E
+    g = torch.Generator(device="cpu").manual_seed(n * 100 + h)
+    y = (torch.randn(n, 64, h, h + 1, generator=g) * 2).to(torch.bfloat16).to("cuda")
+    y = y.contiguous(memory_format=torch.channels_last)
+    b = torch.randn(64, generator=g).to(torch.bfloat16).to("cuda")
+    ref = F.max_pool2d(E._bias_act_(y.clone(), b), 3, 2, 1)
+    out = E._stem_pool_(y, b)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape and out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out, ref)

@@ -387,6 +387,64 @@ extern "C" int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* str
   return 0;
 }
 
+// ResNet stem tail (code/models/ResNet.py:240-245: conv1 -> bn1 -> relu -> maxpool 3x3/2 pad 1) on
+// the raw stem convolution output, channels-last bf16: out = relu(max over the window of y + b)
+// (= max of relu(y + b): + b and ReLU are monotone), one thread per 8 channels of one output
+// pixel; the 9 window rows' 16-B pieces are loaded before the max (out-of-range taps skipped, as
+// the -inf padding of max_pool2d).
+__global__ __launch_bounds__(256) void bias_relu_maxpool_kernel(const bf16* __restrict__ y, const bf16* __restrict__ bias,
+                                                                bf16* __restrict__ out, long long npix, int H, int W,
+                                                                int OH, int OW, int C) {
+  const int cg = C / 8;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix * cg) return;
+  const int c8 = (int)(i % cg) * 8;
+  const long long pix = i / cg;
+  const int ow = (int)(pix % OW), oh = (int)((pix / OW) % OH);
+  const long long nimg = pix / ((long long)OW * OH);
+  const bf16* base = y + nimg * H * W * (long long)C + c8;
+  bf16x8 v[9];
+  bool ok[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int ih = 2 * oh - 1 + t / 3, iw = 2 * ow - 1 + t % 3;
+    ok[t] = ih >= 0 && ih < H && iw >= 0 && iw < W;
+    v[t] = ok[t] ? *(const bf16x8*)(base + ((long long)ih * W + iw) * C) : (bf16x8){};
+  }
+  float m[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    if (ok[t])
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)v[t][e]);
+  const bf16x8 b8 = *(const bf16x8*)(bias + c8);
+  bf16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    // the reference rounds y + b to bf16 before the ReLU / pool: same here (the max of the
+    // rounded sums equals the rounded sum of the max: rounding is monotone)
+    const float sb = (float)(bf16)(m[e] + (float)b8[e]);
+    o[e] = (bf16)fmaxf(sb, 0.f);
+  }
+  *(bf16x8*)(out + pix * C + c8) = o;
+}
+
+extern "C" int tm_bias_relu_maxpool(const void* y, const void* bias, void* out, int N, int H, int W, int C,
+                                    void* stream) {
+  TM_REQUIRE(y && bias && out && N > 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0, "bias_relu_maxpool: bad args");
+  TM_REQUIRE(((uintptr_t)y % 16) == 0 && ((uintptr_t)bias % 16) == 0 && ((uintptr_t)out % 16) == 0,
+             "bias_relu_maxpool: 16-B aligned buffers");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const long long npix = (long long)N * OH * OW;
+  const long long threads = npix * (C / 8);
+  bias_relu_maxpool_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const bf16*)y, (const bf16*)bias, (bf16*)out, npix, H, W, OH, OW, C);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int relu, void* stream) {
   TM_REQUIRE(y && bias && rows >= 0 && C > 0 && C % 8 == 0, "bias_act: bad args (C % 8 == 0)");
   TM_REQUIRE(((uintptr_t)y % 16) == 0 && ((uintptr_t)bias % 16) == 0, "bias_act: 16-B aligned buffers");

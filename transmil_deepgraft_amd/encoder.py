@@ -134,6 +134,21 @@ def _bias_act_(y, b, relu=True):
     return y
 
 
+def _stem_pool_(y, b):
+    """maxpool3x3/2(relu(y + b)) of the raw channels-last bf16 stem output in one HIP pass
+    (tm_bias_relu_maxpool; the same values as tm_bias_act + max_pool2d: + b, ReLU and bf16 rounding
+    are monotone, so they commute with the max)."""
+    from . import _lib
+    from .engine import _p, _stream
+    if not y.is_contiguous(memory_format=torch.channels_last):
+        y = y.contiguous(memory_format=torch.channels_last)
+    n, c, h, wd = y.shape
+    out = torch.empty(n, c, (h - 1) // 2 + 1, (wd - 1) // 2 + 1, dtype=y.dtype, device=y.device,
+                      memory_format=torch.channels_last)
+    _lib.call("tm_bias_relu_maxpool", _p(y), _p(b), _p(out), n, h, wd, c, _stream())
+    return out
+
+
 def _bn_train_stats(ys, bn, ws):
     """Train-mode BatchNorm statistics of a channels-last activation held as a list of bag pieces
     (tm_bn_train_stats: the statistics span every piece): returns fp32 [2, C] (scale, shift) and
@@ -339,7 +354,8 @@ class RetCCLResNet50(nn.Module):
         f = self._folded
         w, b = f["stem"]
         if self.channels_last and x.is_cuda:
-            x = _lib_max_pool(_bias_act_(_lib_conv2d(x, w, None, stride=2, padding=3), b))
+            y = _lib_conv2d(x, w, None, stride=2, padding=3)
+            x = _stem_pool_(y, b) if y.dtype == torch.bfloat16 else _lib_max_pool(_bias_act_(y, b))
             for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
                 y = _conv1x1_gemm(x, w1, b1, True)
                 y = _bias_act_(_lib_conv2d(y, w2, None, stride=s2, padding=1), b2)
