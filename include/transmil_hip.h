@@ -332,6 +332,10 @@ int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int
  * maxpool3x3/2 pad 1 (relu(y + bias)) over the raw channels-last bf16 stem output y[N, H, W, C],
  * OH = (H - 1) / 2 + 1; one pass instead of the in-place bias + ReLU and a max-pool launch */
 int tm_bias_relu_maxpool(const void* y, const void* bias, void* out, int N, int H, int W, int C, void* stream);
+/* the same with train-mode BatchNorm: each tap bf16(relu(y * scale + shift)) (tm_bn_apply's
+ * arithmetic, scale / shift fp32 [C] from tm_bn_train_stats), then the window max */
+int tm_bn_relu_maxpool(const void* y, const float* scale, const float* shift, void* out, int N, int H, int W, int C,
+                       void* stream);
 /* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
  * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout])
  * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.

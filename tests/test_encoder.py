@@ -409,3 +409,20 @@ def test_stem_bias_relu_maxpool_equals_bias_act_then_pool(n, h):
     torch.cuda.synchronize()
     assert out.shape == ref.shape and out.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+def test_stem_bn_relu_maxpool_equals_bn_apply_then_pool():
+    """tm_bn_relu_maxpool (train-mode stem: batch-statistics BN, some negative scales) against
+    tm_bn_apply + max_pool2d: bitwise."""
+    import torch.nn.functional as F
+    from transmil_deepgraft_amd import encoder as E
+    g = torch.Generator(device="cpu").manual_seed(5)
+    y = (torch.randn(2, 64, 30, 29, generator=g) * 2).to(torch.bfloat16).to("cuda")
+    y = y.contiguous(memory_format=torch.channels_last)
+    scale = torch.randn(64, generator=g).to("cuda")
+    shift = torch.randn(64, generator=g).to("cuda")
+    ref = F.max_pool2d(E._bn_apply_(y.clone(), (scale, shift)), 3, 2, 1)
+    out = E._stem_pool_bn_(y, (scale, shift))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)

@@ -392,9 +392,15 @@ extern "C" int tm_cast_f32_many(int dtype, const tm_cast_table* table, void* str
 // (= max of relu(y + b): + b and ReLU are monotone), one thread per 8 channels of one output
 // pixel; the 9 window rows' 16-B pieces are loaded before the max (out-of-range taps skipped, as
 // the -inf padding of max_pool2d).
+// AFFINE: train-mode BatchNorm instead of the folded bias: each tap is bf16(relu(y * scale + shift))
+// (tm_bn_apply's per-element arithmetic; the scale may be negative, so the affine map is applied
+// before the max), then the max of the window.
+template <bool AFFINE = false>
 __global__ __launch_bounds__(256) void bias_relu_maxpool_kernel(const bf16* __restrict__ y, const bf16* __restrict__ bias,
                                                                 bf16* __restrict__ out, long long npix, int H, int W,
-                                                                int OH, int OW, int C) {
+                                                                int OH, int OW, int C,
+                                                                const float* __restrict__ scale = nullptr,
+                                                                const float* __restrict__ shift = nullptr) {
   const int cg = C / 8;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= npix * cg) return;
@@ -414,6 +420,21 @@ __global__ __launch_bounds__(256) void bias_relu_maxpool_kernel(const bf16* __re
   float m[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+  if constexpr (AFFINE) {
+    float sc[8], sf[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { sc[e] = scale[c8 + e]; sf[e] = shift[c8 + e]; }
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      if (ok[t])
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)(bf16)fmaxf(fmaf((float)v[t][e], sc[e], sf[e]), 0.f));
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)m[e];
+    *(bf16x8*)(out + pix * C + c8) = o;
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 9; ++t)
     if (ok[t])
@@ -439,8 +460,22 @@ extern "C" int tm_bias_relu_maxpool(const void* y, const void* bias, void* out, 
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
   const long long npix = (long long)N * OH * OW;
   const long long threads = npix * (C / 8);
-  bias_relu_maxpool_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+  bias_relu_maxpool_kernel<false><<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
       (const bf16*)y, (const bf16*)bias, (bf16*)out, npix, H, W, OH, OW, C);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_bn_relu_maxpool(const void* y, const float* scale, const float* shift, void* out, int N, int H, int W,
+                                  int C, void* stream) {
+  TM_REQUIRE(y && scale && shift && out && N > 0 && H > 0 && W > 0 && C > 0 && C % 8 == 0,
+             "bn_relu_maxpool: bad args");
+  TM_REQUIRE(((uintptr_t)y % 16) == 0 && ((uintptr_t)out % 16) == 0, "bn_relu_maxpool: 16-B aligned buffers");
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const long long npix = (long long)N * OH * OW;
+  const long long threads = npix * (C / 8);
+  bias_relu_maxpool_kernel<true><<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const bf16*)y, nullptr, (bf16*)out, npix, H, W, OH, OW, C, scale, shift);
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -149,6 +149,18 @@ def _stem_pool_(y, b):
     return out
 
 
+def _stem_pool_bn_(y, st):
+    """maxpool3x3/2(relu(y * scale + shift)) with the stem BatchNorm's batch statistics in one HIP
+    pass (tm_bn_relu_maxpool; the same values as tm_bn_apply + max_pool2d)."""
+    from . import _lib
+    from .engine import _p, _stream
+    n, c, h, wd = y.shape
+    out = torch.empty(n, c, (h - 1) // 2 + 1, (wd - 1) // 2 + 1, dtype=y.dtype, device=y.device,
+                      memory_format=torch.channels_last)
+    _lib.call("tm_bn_relu_maxpool", _p(y), _p(st[0]), _p(st[1]), _p(out), n, h, wd, c, _stream())
+    return out
+
+
 def _bn_train_stats(ys, bn, ws):
     """Train-mode BatchNorm statistics of a channels-last activation held as a list of bag pieces
     (tm_bn_train_stats: the statistics span every piece): returns fp32 [2, C] (scale, shift) and
@@ -394,7 +406,10 @@ class RetCCLResNet50(nn.Module):
         xs = [_cl(_lib_conv2d(x[i:i + piece], w["conv1.weight"], None, stride=2, padding=3))
               for i in range(0, x.shape[0], piece)]
         st = _bn_train_stats(xs, self.bn1, ws)
-        xs = [_lib_max_pool(_bn_apply_(p, st)) for p in xs]
+        if x.dtype == torch.bfloat16:
+            xs = [_stem_pool_bn_(p, st) for p in xs]
+        else:
+            xs = [_lib_max_pool(_bn_apply_(p, st)) for p in xs]
         for si, stage in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
             for bi, blk in enumerate(stage):
                 pre = f"layer{si}.{bi}."
