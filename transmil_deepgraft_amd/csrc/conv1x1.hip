@@ -31,7 +31,7 @@ namespace {
 
 constexpr int kMaxDev = 16;
 constexpr long long kMaxRows = 1LL << 21;
-constexpr int kCand = 8;   // heuristic candidates (tm_conv1x1_tune times them)
+constexpr int kCand = 32;  // heuristic candidates (tm_conv1x1_tune times them)
 
 struct Plan {
   hipblasLtMatrixLayout_t a = nullptr, b = nullptr, cd = nullptr;
