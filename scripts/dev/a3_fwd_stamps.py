@@ -18,7 +18,14 @@ k = (torch.randn(nbh, n, 64, generator=g) * 0.3).to(torch.bfloat16).to(dev)
 v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16).to(dev)
 work = torch.empty(_lib.query("tm_nys_a3_workspace", nbh, n) // 4 + 16, device=dev)
 f = lambda: _lib.call("tm_nys_a3_fwd", BF16, _p(ql), _p(k), _p(v), nbh, n, _p(work), _p(None), _p(None), _stream())
-for var in (0, 32):
+if os.environ.get("A3_SIM2", "0") == "1":   # the bench's form: the fused A2 rows (tm_nys_a3_fwd_sim2)
+    kl = (torch.randn(nbh, 256, 64, generator=g) * 0.3).to(dev)
+    a2 = torch.empty(nbh, 256, 256, device=dev)
+    a2s = torch.empty(nbh, 256, 256, device=dev)
+    f = lambda: _lib.call("tm_nys_a3_fwd_sim2", _p(ql), _p(kl), _p(k), _p(v), nbh, n, _p(work), _p(a2), _p(a2s),
+                          _stream())
+STV = 32
+for var in (0, STV):
     _lib.lib().tm_debug_set_variant(1, var)
     for _ in range(3): f()
     torch.cuda.synchronize()

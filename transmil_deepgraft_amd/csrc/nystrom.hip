@@ -2308,6 +2308,11 @@ void launch_a3_fwd_v2(const float* ql, const void* k, const void* v, int nbh, in
     a3_fwd_v2_kernel<1><<<grid, 512, A3V_BYTES, st>>>(ql, kb, vb, n, P, po, pm, pl, s2);
     return;
   }
+  if (NYS_VARIANT == 32 && s2.a2 && P * 8 == NL) {   // the same with the fused A2 rows
+    tm_allow_smem(a3_fwd_v2_kernel<1, 4>, A3V_BYTES);
+    a3_fwd_v2_kernel<1, 4><<<grid, 512, A3V_BYTES, st>>>(ql, kb, vb, n, P, po, pm, pl, s2);
+    return;
+  }
 #endif
   if (s2.a2 && P * 8 == NL) {
     tm_allow_smem(a3_fwd_v2_kernel<0, 4>, A3V_BYTES);
