@@ -79,7 +79,15 @@ __global__ __launch_bounds__(OPT_THREADS) void radam_lookahead_kernel(tm_optim_t
     pc[u].n = 0;
     s4[u] = (f32x4){0.f, 0.f, 0.f, 0.f};
     if (wbase >= total) continue;
-    while (ti < tab.count - 1 && wbase >= tab.offset[ti + 1]) ++ti;
+    {   // the last tensor starting at or before wbase: a binary search (a linear walk from tensor 0
+        // was up to tab.count dependent scalar loads per wave ahead of its element loads)
+      int lo = ti, hi = tab.count - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab.offset[mid] <= wbase) lo = mid; else hi = mid - 1;
+      }
+      ti = lo;
+    }
     const float* grad = nullptr;
     for (int t = ti; t < tab.count && tab.offset[t] < wbase + 256; ++t) {  // wave-uniform t
       if (i0[u] >= tab.offset[t] && i0[u] < tab.offset[t + 1]) {
