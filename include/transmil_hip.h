@@ -336,6 +336,14 @@ int tm_bias_relu_maxpool(const void* y, const void* bias, void* out, int N, int 
  * arithmetic, scale / shift fp32 [C] from tm_bn_train_stats), then the window max */
 int tm_bn_relu_maxpool(const void* y, const float* scale, const float* shift, void* out, int N, int H, int W, int C,
                        void* stream);
+/* The whole eval-mode stem in one pass (code/models/ResNet.py:240-245, BN folded): out[N, PH, PW, 64]
+ * = maxpool3x3/2 pad 1(relu(conv7x7/2 pad 3(x, w) + bias)), x bf16 [N, 3, H, W] at element strides
+ * (sn, sc, sh, sw) (NCHW or channels-last),
+ * wp the folded weights packed bf16 [64][7][8][4] (w[o, c, ky, kx] at [o][ky][kx][c]; kx = 7 and
+ * c = 3 zero), bias bf16 [64]; CH = (H - 1) / 2 + 1, PH = (CH - 1) / 2 + 1 (same for W).  fp32
+ * accumulation, one bf16 rounding after the ReLU; the convolution output never reaches HBM. */
+int tm_stem_conv_pool(const void* x, const void* wp, const void* bias, void* out, int N, int H, int W, long long sn,
+                      long long sc, long long sh, long long sw, void* stream);
 /* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
  * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout])
  * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.

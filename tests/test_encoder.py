@@ -167,8 +167,8 @@ def test_c5_full_bag_4096_tiles(enc_dtype, mil_dtype, rtol, ltol, gtol):
     RetCCL ResNet-50 (eval, BN folded) -> TransMIL(2, 2048) (RCC _fc1 branch).
       * 16 tiles spread over the bag: encoder features against the fixture-pinned fp64 oracle
         (oracle/encoder_ref.py), per-tile relative L2 error < rtol;
-      * the whole-bag features (the encoder's internal 512-tile chunks) bit-identical to running
-        the 8 chunks of 512 tiles one by one;
+      * the whole-bag features (the encoder's internal 512-tile chunks) equal to running the 8
+        chunks of 512 tiles one by one (fp32 bitwise, bf16 within a rounding);
       * TransMIL logits / every parameter gradient on the GPU-computed features against the fp64
         TransMIL oracle on the same features (C2 tolerances for the mode);
       * one train step of the image model (dropout on, Lookahead(RAdam)) finite and moving."""
@@ -194,7 +194,16 @@ def test_c5_full_bag_4096_tiles(enc_dtype, mil_dtype, rtol, ltol, gtol):
     # (A one-pass 4096-tile batch is refused by encoder._lib_guard: MIOpen's NHWC implicit-GEMM
     # kernel for layer2.0's stride-2 3x3 convolution returned wrong outputs for tiles >= 2674 of it,
     # profiles/r05_c5_drift.json -- the round-4 one-pass drift.)
-    assert torch.equal(whole, chunks)
+    # fp32: bit-identical.  bf16: the hipBLASLt 1x1 algorithm of each shape is chosen by timing
+    # (tm_conv1x1_tune) and some candidates sum split-K / stream-K partials in a run-dependent order,
+    # so an M tile that straddles two images may round differently run to run (two adjacent tiles
+    # of 4096 seen, scripts/dev/c5_whole_vs_chunks.py); the chunking property is then held to a
+    # bf16 rounding instead -- the offset-wrap defect this guards against was a 0.12-0.35 error
+    diff = (whole - chunks).norm(dim=1) / chunks.norm(dim=1)
+    if enc_dtype == torch.float32:
+        assert torch.equal(whole, chunks), (whole != chunks).any(dim=1).nonzero().flatten().tolist()[:16]
+    else:
+        assert diff.max().item() < 1e-2, (diff.max().item(), diff.argmax().item())
 
     # TransMIL(2, 2048) on the GPU features against the fp64 oracle on the same features
     refm, ours = _pair(2, feat=2048, dtype=mil_dtype)
@@ -426,3 +435,27 @@ def test_stem_bn_relu_maxpool_equals_bn_apply_then_pool():
     out = E._stem_pool_bn_(y, (scale, shift))
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(2, 224, 224), (3, 61, 47), (1, 9, 16)])
+def test_stem_conv_pool_against_torch_fp32(n, h, w):
+    """tm_stem_conv_pool (the whole eval stem in one pass: conv 7x7/2 + folded bias + ReLU +
+    max-pool 3x3/2) against the fp32 torch ops on the same bf16 inputs, within one bf16 rounding of
+    the output; NCHW and channels-last inputs give the same bits; ragged sizes cover the partial
+    8 x 8 pooled blocks and the padding at every edge."""
+    import torch.nn.functional as F
+    from transmil_deepgraft_amd import encoder as E
+    g = torch.Generator(device="cpu").manual_seed(n * 1000 + h + w)
+    x = torch.randn(n, 3, h, w, generator=g).to(torch.bfloat16).to("cuda")
+    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(torch.bfloat16).to("cuda")
+    b = (torch.randn(64, generator=g) * 0.1).to(torch.bfloat16).to("cuda")
+    ref = F.max_pool2d(F.relu(F.conv2d(x.float(), wt.float(), b.float(), stride=2, padding=3)), 3, 2, 1)
+    wp = E._pack_stem(wt)
+    out = E._stem_conv_pool(x, wp, b)
+    out_cl = E._stem_conv_pool(x.contiguous(memory_format=torch.channels_last), wp, b)
+    torch.cuda.synchronize()
+    assert out.shape == ref.shape and out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out, out_cl)
+    err = (out.float() - ref).abs()
+    assert (err <= ref.abs() * 2 ** -8 + 1e-5).all(), err.max().item()

@@ -136,6 +136,7 @@ _SIGS = {
     "tm_bias_act": (I, [I, P, P, L, I, I, P]),
     "tm_bias_relu_maxpool": (I, [P, P, P, I, I, I, I, P]),
     "tm_bn_relu_maxpool": (I, [P, P, P, P, I, I, I, I, P]),
+    "tm_stem_conv_pool": (I, [P, P, P, P, I, I, I, L, L, L, L, P]),
     "tm_conv1x1_workspace_bytes": (L, []),
     "tm_conv1x1": (I, [I, P, P, P, P, P, L, I, I, I, P, L, P]),
     "tm_conv1x1_tune": (I, [I, P, P, P, P, P, L, I, I, I, P, L, P]),

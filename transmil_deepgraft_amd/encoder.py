@@ -204,6 +204,35 @@ def _bn_apply_(y, st, residual=None, rst=None, relu=True):
     return y
 
 
+def _stem_conv_pool(x, wp, b):
+    """The eval stem (BN folded) in one HIP pass: maxpool3x3/2(relu(conv7x7/2(x) + b)) from bf16
+    tiles at any strides to a channels-last bf16 [n, 64, PH, PW] (tm_stem_conv_pool; the
+    convolution output never reaches HBM)."""
+    from . import _lib
+    from .engine import _p, _stream
+    n, c, h, wd = x.shape
+    if c != 3 or x.dtype != torch.bfloat16 or wp.shape != (64, 224):
+        raise RuntimeError("stem_conv_pool: bf16 [n, 3, h, w] tiles and [64, 224] packed weights expected")
+    ch, cw = (h - 1) // 2 + 1, (wd - 1) // 2 + 1
+    out = torch.empty(n, 64, (ch - 1) // 2 + 1, (cw - 1) // 2 + 1, dtype=x.dtype, device=x.device,
+                      memory_format=torch.channels_last)
+    sn, sc, sh, sw = x.stride()
+    _lib.call("tm_stem_conv_pool", _p(x), _p(wp), _p(b), _p(out), n, h, wd, sn, sc, sh, sw, _stream())
+    return out
+
+
+def _pack_stem(w):
+    """Folded stem weights [64, 3, 7, 7] -> tm_stem_conv_pool's [64][ky][kx 8][c 4] (kx = 7, c = 3 zero)."""
+    wp = torch.zeros(64, 7, 8, 4, dtype=w.dtype, device=w.device)
+    wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    return wp.reshape(64, 224).contiguous()
+
+
+def _stem_fused_enabled():
+    import os
+    return os.environ.get("TM_STEM_FUSED", "1") != "0"
+
+
 def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
@@ -349,6 +378,8 @@ class RetCCLResNet50(nn.Module):
     def _fold_all(self):
         dt, cl = self.compute_dtype, self.channels_last
         f = {"stem": _fold(self.conv1, self.bn1, dt, cl), "blocks": []}
+        if dt == torch.bfloat16:
+            f["stem_packed"] = _pack_stem(f["stem"][0])
         for stage in (self.layer1, self.layer2, self.layer3, self.layer4):
             for blk in stage:
                 d = None
@@ -366,8 +397,11 @@ class RetCCLResNet50(nn.Module):
         f = self._folded
         w, b = f["stem"]
         if self.channels_last and x.is_cuda:
-            y = _lib_conv2d(x, w, None, stride=2, padding=3)
-            x = _stem_pool_(y, b) if y.dtype == torch.bfloat16 else _lib_max_pool(_bias_act_(y, b))
+            if "stem_packed" in f and x.dtype == torch.bfloat16 and _stem_fused_enabled():
+                x = _stem_conv_pool(x, f["stem_packed"], b)
+            else:
+                y = _lib_conv2d(_cl(x), w, None, stride=2, padding=3)
+                x = _stem_pool_(y, b) if y.dtype == torch.bfloat16 else _lib_max_pool(_bias_act_(y, b))
             for (w1, b1), (w2, b2, s2), (w3, b3), d in f["blocks"]:
                 y = _conv1x1_gemm(x, w1, b1, True)
                 y = _bias_act_(_lib_conv2d(y, w2, None, stride=s2, padding=1), b2)
@@ -477,8 +511,10 @@ class RetCCLResNet50(nn.Module):
         with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
             for s in range(0, x.shape[0], chunk):
                 xc = x[s:s + chunk].to(torch.float32 if autocast else dt)
-                xc = xc.contiguous(memory_format=torch.channels_last if self.channels_last
-                                   else torch.contiguous_format)
+                if not (not self.training and self.channels_last and dt == torch.bfloat16 and _stem_fused_enabled()):
+                    # (the fused eval stem reads the tiles at any strides: no channels-last copy)
+                    xc = xc.contiguous(memory_format=torch.channels_last if self.channels_last
+                                       else torch.contiguous_format)
                 if not self.training:
                     y = self._forward_folded(xc)
                 elif fused_train:
