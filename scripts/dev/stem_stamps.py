@@ -30,8 +30,9 @@ L.tm_debug_set_stem_variant(0)
 buf = (C.c_ulonglong * (4096 * 8))()
 assert L.tm_debug_stem_stamps(buf, 4096 * 8) == 0
 a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
+a = a[a[:, 0] != 0]
 d = a[:, 2:6] - a[:, 1:2]
-ph = np.diff(np.concatenate([np.zeros((4096, 1), np.int64), d], axis=1), axis=1)
+ph = np.diff(np.concatenate([np.zeros((len(a), 1), np.int64), d], axis=1), axis=1)
 print("cycles per phase (median / p90): staged, k loop, conv tile, pool")
 for i, nm in enumerate(["staged", "k loop", "conv tile", "pool"]):
     print(f"  {nm:10s} {np.median(ph[:, i]):8.0f} {np.percentile(ph[:, i], 90):8.0f}")
