@@ -344,6 +344,22 @@ int tm_bn_relu_maxpool(const void* y, const float* scale, const float* shift, vo
  * accumulation, one bf16 rounding after the ReLU; the convolution output never reaches HBM. */
 int tm_stem_conv_pool(const void* x, const void* wp, const void* bias, void* out, int N, int H, int W, long long sn,
                       long long sc, long long sh, long long sw, void* stream);
+/* The train-mode stem (batch-statistics bn1, code/models/model_interface.py:303-309 feeding the
+ * frozen encoder in train mode) in two passes over the tiles, the convolution recomputed instead of
+ * stored: tm_stem_bn_stats runs the convolution and reduces its bf16-rounded outputs per channel
+ * (per-workgroup count / mean / M2, merged in workgroup order in fp64: deterministic), then writes
+ * scale = gamma / sqrt(var + eps), shift = beta - mean * scale (biased variance) and updates the
+ * running statistics with the unbiased variance and the momentum (nn.BatchNorm2d);
+ * workspace >= tm_stem_bn_stats_workspace() doubles.  tm_stem_conv_pool_bn then writes
+ * maxpool(bf16(relu(bf16(conv) * scale + shift))) (tm_bn_apply's arithmetic).  N may be the whole
+ * bag: tiles are addressed with 64-bit bases. */
+long long tm_stem_bn_stats_workspace(void);
+int tm_stem_bn_stats(const void* x, const void* wp, int N, int H, int W, long long sn, long long sc, long long sh,
+                     long long sw, const float* gamma, const float* beta, float* running_mean, float* running_var,
+                     float momentum, float eps, float* scale, float* shift, double* workspace, long long ws_doubles,
+                     void* stream);
+int tm_stem_conv_pool_bn(const void* x, const void* wp, const float* scale, const float* shift, void* out, int N,
+                         int H, int W, long long sn, long long sc, long long sh, long long sw, void* stream);
 /* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
  * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout])
  * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.

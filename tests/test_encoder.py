@@ -459,3 +459,46 @@ def test_stem_conv_pool_against_torch_fp32(n, h, w):
     assert torch.equal(out, out_cl)
     err = (out.float() - ref).abs()
     assert (err <= ref.abs() * 2 ** -8 + 1e-5).all(), err.max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,h,w", [(5, 64, 72), (2, 224, 224), (3, 33, 17)])
+def test_stem_train_bn_passes_against_torch(n, h, w):
+    """Train-mode stem (tm_stem_bn_stats + tm_stem_conv_pool_bn, the conv recomputed instead of
+    stored): batch statistics of the bf16-rounded conv output against fp64 torch over every pixel of
+    every tile (scale / shift / running statistics), and the pooled output against the fp32 torch
+    ops with those statistics."""
+    import torch.nn as nn
+    import torch.nn.functional as F
+    from transmil_deepgraft_amd import encoder as E
+    g = torch.Generator(device="cpu").manual_seed(n * 7 + h + w)
+    x = torch.randn(n, 3, h, w, generator=g).to(torch.bfloat16).to("cuda")
+    wt = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).to(torch.bfloat16).to("cuda")
+    bn = nn.BatchNorm2d(64, momentum=0.1).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(64, generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(64, generator=g) * 0.1)
+        bn.running_mean.copy_(torch.randn(64, generator=g) * 0.1)
+    rm0, rv0 = bn.running_mean.clone().double(), bn.running_var.clone().double()
+    wp = E._pack_stem(wt)
+    st = E._stem_bn_stats(x, wp, bn)
+    out = E._stem_conv_pool_bn(x, wp, st)
+    torch.cuda.synchronize()
+    conv = F.conv2d(x.double(), wt.double(), stride=2, padding=3).to(torch.bfloat16).double()
+    mean = conv.mean(dim=(0, 2, 3))
+    var = conv.var(dim=(0, 2, 3), unbiased=False)
+    cnt = conv.numel() // 64
+    sc = bn.weight.double() / torch.sqrt(var + bn.eps)
+    sf = bn.bias.double() - mean * sc
+    torch.testing.assert_close(st[0].double(), sc, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(st[1].double(), sf, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(bn.running_mean.double(), 0.9 * rm0 + 0.1 * mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn.running_var.double(), 0.9 * rv0 + 0.1 * var * cnt / (cnt - 1), rtol=1e-5,
+                               atol=1e-6)
+    ref = F.max_pool2d(F.relu(conv.float() * st[0].view(1, 64, 1, 1) + st[1].view(1, 64, 1, 1)), 3, 2, 1)
+    assert out.shape == ref.shape and out.is_contiguous(memory_format=torch.channels_last)
+    err = (out.float() - ref).abs()
+    # one bf16 rounding of the output, plus a one-ulp tie flip of bf16(conv) where the summation
+    # order differs (scaled by |scale|)
+    tol = ref.abs() * 2 ** -8 + st[0].abs().view(1, 64, 1, 1) * conv.float().abs().amax() * 2 ** -8 + 1e-5
+    assert (err <= tol).all(), err.max().item()

@@ -45,7 +45,14 @@ constexpr int SBUF = SIMG_BYTES > SOUT_BYTES ? SIMG_BYTES : SOUT_BYTES;
 constexpr int SLDS = SW_BYTES + SBUF;                 // 66416: two workgroups per CU
 constexpr int STHREADS = 256;
 constexpr int IPIX = SIR * SIC, ITRIPS = (IPIX + STHREADS - 1) / STHREADS;
+constexpr int SRED_BYTES = 2 * 4 * 64 * 4;            // MODE 1: the 4 row groups' (sum, count) per channel
 static_assert(SMT == 8, "two pixel tiles per wave");
+
+// MODE 0: eval, folded bias.  MODE 1: train-mode statistics of the conv output (bf16-rounded, as a
+// materialised conv output would be): per workgroup a fixed-order (count, mean, M2) over the conv
+// pixels its regions own (rows 2P .. 2P+15, cols 2Q .. 2Q+13: each pixel once), no pooled output.
+// MODE 2: train-mode BatchNorm apply: each conv value bf16(relu(bf16(conv) * scale + shift)) (the
+// arithmetic of tm_bn_apply on the rounded conv output), then the pool.
 
 #ifdef TM_DIAG
 // diagnostics: per-workgroup clock stamps of wave 0 ([block][8]: realtime start, shader clock at
@@ -68,6 +75,8 @@ TM_DEV void stem_stamp(unsigned long long (&ts)[8], int slot, bool real = false)
 
 struct StemArgs {
   const bf16* x; const bf16* wp; const bf16* bias; bf16* out;
+  const float* scale; const float* shift;   // MODE 2: train-mode BatchNorm (batch statistics)
+  double* part;                             // MODE 1: [grid][64][3] (count, mean, M2) per workgroup
   long long sn;
   int H, W, sc, sh, sw;             // element strides inside one tile (< 2^31)
   unsigned tile_bytes;              // one tile's extent: the buffer resource of its loads
@@ -75,7 +84,7 @@ struct StemArgs {
   int nregions;
 };
 
-template <bool STAMP = false>
+template <int MODE, bool STAMP = false>
 __global__ __launch_bounds__(STHREADS, 2) void stem_conv_pool_kernel(StemArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -96,12 +105,20 @@ __global__ __launch_bounds__(STHREADS, 2) void stem_conv_pool_kernel(StemArgs a)
     if (i < WPIECES) *(bf16x8*)(wl + (i / (SK / 8)) * SWROW + (i % (SK / 8)) * 8) =
         *(const bf16x8*)(a.wp + (i / (SK / 8)) * SK + (i % (SK / 8)) * 8);
   }
-  // the lane's 32 bias values: output channel 32 u + 8 k + 4 g + e sits in acc[.][u][4 k + e]
-  float bv[2][16];
+  // the lane's 32 bias (MODE 0) / scale + shift (MODE 2) values: output channel 32 u + 8 k + 4 g + e
+  // sits in acc[.][u][4 k + e]
+  float bv[2][16], sv[2][16];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) bv[u][i] = (float)a.bias[32 * u + acc_row(i, g)];
+    for (int i = 0; i < 16; ++i) {
+      const int c = 32 * u + acc_row(i, g);
+      bv[u][i] = MODE == 0 ? (float)a.bias[c] : MODE == 2 ? a.scale[c] : 0.f;
+      sv[u][i] = MODE == 2 ? a.shift[c] : 0.f;
+    }
+  // MODE 1: the workgroup's running (count, mean, M2) of channel tid (threads 0..63), fp64
+  double wn = 0.0, wmean = 0.0, wm2 = 0.0;
+  float* red = (float*)(lds + SW_BYTES + SBUF);             // MODE 1 scratch [2][4][64]
 
   // a region's input window in registers: each channel value in its own register, every load a
   // raw buffer load whose out-of-image offsets point past the resource (the hardware returns 0: the
@@ -188,7 +205,12 @@ __global__ __launch_bounds__(STHREADS, 2) void stem_conv_pool_kernel(StemArgs a)
           for (int k = 0; k < 4; ++k) {
             bf16x4 o;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (bf16)fmaxf(acc[j][u][4 * k + e] + bv[u][4 * k + e], 0.f);
+            for (int e = 0; e < 4; ++e) {
+              const float v = acc[j][u][4 * k + e];
+              if constexpr (MODE == 0) o[e] = (bf16)fmaxf(v + bv[u][4 * k + e], 0.f);
+              else if constexpr (MODE == 1) o[e] = (bf16)v;
+              else o[e] = (bf16)fmaxf(fmaf((float)(bf16)v, bv[u][4 * k + e], sv[u][4 * k + e]), 0.f);
+            }
             *(bf16x4*)(cv + mpix[j] * SOROW + 32 * u + 8 * k + 4 * g) = o;
           }
       }
@@ -196,6 +218,40 @@ __global__ __launch_bounds__(STHREADS, 2) void stem_conv_pool_kernel(StemArgs a)
     __syncthreads();
     if (first) stem_stamp<STAMP>(ts, 4);
 
+    if constexpr (MODE == 1) {
+      // this region's pixels: local rows 1 .. 16, cols 1 .. 14 inside the image; thread = (channel,
+      // row group q: rows 1 + q, 5 + q, ..): sum and count, then the region mean, then M2 about it
+      const int c = tid & 63, q = tid >> 6;
+      const int cr0 = 2 * P0 - 1, cc0 = 2 * Q0 - 1;
+      const int lrh = min(2 * SPR, a.CH - 1 - cr0), lch = min(2 * SPC, a.CW - 1 - cc0);
+      float sum = 0.f;
+      int cnt = 0;
+      for (int lr = 1 + q; lr <= lrh; lr += 4)
+        for (int lc = 1; lc <= lch; ++lc) { sum += (float)cv[(lr * SCC + lc) * SOROW + c]; ++cnt; }
+      red[q * 64 + c] = sum;
+      red[256 + q * 64 + c] = (float)cnt;
+      __syncthreads();
+      float rs = 0.f, rc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { rs += red[k * 64 + c]; rc += red[256 + k * 64 + c]; }
+      const float rmean = rs / rc;
+      float m2 = 0.f;
+      for (int lr = 1 + q; lr <= lrh; lr += 4)
+        for (int lc = 1; lc <= lch; ++lc) {
+          const float d = (float)cv[(lr * SCC + lc) * SOROW + c] - rmean;
+          m2 = fmaf(d, d, m2);
+        }
+      __syncthreads();                                      // every thread has read red's sums
+      red[q * 64 + c] = m2;
+      __syncthreads();
+      if (q == 0) {
+        const double rm2 = (double)red[c] + (double)red[64 + c] + (double)red[128 + c] + (double)red[192 + c];
+        const double n = wn + (double)rc, delta = (double)rmean - wmean;     // Chan et al. merge
+        wmean += delta * (double)rc / n;
+        wm2 += rm2 + delta * delta * wn * (double)rc / n;
+        wn = n;
+      }
+    } else {
     // 3 x 3 / 2 max pool: thread = (pooled pixel, 16 channels).  Conv pixels outside the image
     // are skipped (max_pool2d's -inf padding); every value is a ReLU output >= 0, so the max of the
     // bf16 bit patterns as unsigned integers is the max of the values (no converts)
@@ -228,11 +284,20 @@ __global__ __launch_bounds__(STHREADS, 2) void stem_conv_pool_kernel(StemArgs a)
       *(u32x4*)q = o0;
       *(u32x4*)(q + 8) = o1;
     }
+    }
     __syncthreads();                                        // cv dead: the next region's pixels
     if (first) stem_stamp<STAMP>(ts, 5);
     first = false;
     if (rn < a.nregions) stage();
     __syncthreads();
+  }
+  if constexpr (MODE == 1) {
+    if (tid < 64) {
+      double* pp = a.part + ((size_t)blockIdx.x * 64 + tid) * 3;
+      pp[0] = wn;
+      pp[1] = wmean;
+      pp[2] = wm2;
+    }
   }
 #ifdef TM_DIAG
   if constexpr (STAMP) {
@@ -247,36 +312,107 @@ __global__ __launch_bounds__(STHREADS, 2) void stem_conv_pool_kernel(StemArgs a)
 #endif
 }
 
-}  // namespace
+// the statistics' combine: one thread per channel merges the workgroups' (count, mean, M2) in
+// workgroup order (fixed: deterministic), then nn.BatchNorm2d's train-mode outputs -- scale / shift
+// with the biased variance, running statistics with the unbiased one and the momentum
+__global__ __launch_bounds__(64) void stem_stats_final_kernel(const double* __restrict__ part, int nparts,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float* running_mean,
+                                                             float* running_var, float momentum, float eps,
+                                                             float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = threadIdx.x;
+  double n = 0.0, mean = 0.0, m2 = 0.0;
+  for (int b = 0; b < nparts; ++b) {
+    const double* pp = part + ((size_t)b * 64 + c) * 3;
+    const double nb = pp[0];
+    if (nb <= 0.0) continue;
+    const double tot = n + nb, delta = pp[1] - mean;
+    mean += delta * nb / tot;
+    m2 += pp[2] + delta * delta * n * nb / tot;
+    n = tot;
+  }
+  const double var = n > 0.0 ? m2 / n : 0.0;
+  const double sc = (double)gamma[c] / sqrt(var + (double)eps);
+  scale[c] = (float)sc;
+  shift[c] = (float)((double)beta[c] - mean * sc);
+  if (running_mean) running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+  if (running_var)
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * (n > 1.0 ? var * n / (n - 1.0) : var));
+}
 
-extern "C" int tm_stem_conv_pool(const void* x, const void* wp, const void* bias, void* out, int N, int H, int W,
-                                 long long sn, long long sc, long long sh, long long sw, void* stream) {
-  TM_REQUIRE(x && wp && bias && out && N > 0 && H > 0 && W > 0 && sn > 0 && sc > 0 && sh > 0 && sw > 0,
-             "stem_conv_pool: bad args");
-  TM_REQUIRE(((uintptr_t)wp % 16) == 0 && ((uintptr_t)out % 16) == 0 && ((uintptr_t)x % 2) == 0,
-             "stem_conv_pool: aligned buffers (weights / output 16 B)");
+int stem_setup(StemArgs& a, const void* x, const void* wp, int N, int H, int W, long long sn, long long sc,
+               long long sh, long long sw, int* grid) {
+  TM_REQUIRE(x && wp && N > 0 && H > 0 && W > 0 && sn > 0 && sc > 0 && sh > 0 && sw > 0, "stem: bad args");
+  TM_REQUIRE(((uintptr_t)wp % 16) == 0 && ((uintptr_t)x % 2) == 0, "stem: aligned buffers (weights 16 B)");
   const long long extent = 2 * sc + (long long)(H - 1) * sh + (long long)(W - 1) * sw + 1;   // elements
-  TM_REQUIRE(extent * 2 < (1ll << 31) - 16, "stem_conv_pool: one tile must span < 2 GiB");
-  StemArgs a;
-  a.x = (const bf16*)x; a.wp = (const bf16*)wp; a.bias = (const bf16*)bias; a.out = (bf16*)out;
+  TM_REQUIRE(extent * 2 < (1ll << 31) - 16, "stem: one tile must span < 2 GiB");
+  a = StemArgs{};
+  a.x = (const bf16*)x; a.wp = (const bf16*)wp;
   a.H = H; a.W = W; a.sn = sn; a.sc = (int)sc; a.sh = (int)sh; a.sw = (int)sw;
   a.tile_bytes = (unsigned)(extent * 2);
   a.CH = (H - 1) / 2 + 1; a.CW = (W - 1) / 2 + 1;            // conv 7x7 / 2, pad 3
   a.PH = (a.CH - 1) / 2 + 1; a.PW = (a.CW - 1) / 2 + 1;      // pool 3x3 / 2, pad 1
   a.nbr = (a.PH + SPR - 1) / SPR; a.nbc = (a.PW + SPC - 1) / SPC;
   const long long nreg = (long long)N * a.nbr * a.nbc;
-  TM_REQUIRE(nreg < (1ll << 31), "stem_conv_pool: too many tiles");
+  TM_REQUIRE(nreg < (1ll << 31), "stem: too many tiles");
   a.nregions = (int)nreg;
-  const int grid = (int)std::min<long long>(nreg, 2LL * tm_cu_count());
+  *grid = (int)std::min<long long>(nreg, 2LL * tm_cu_count());
+  return 0;
+}
+
+template <int MODE>
+int stem_launch(const StemArgs& a, int grid, void* stream) {
   if (TM_DIAG_VAR(g_stem_variant) == 1) {
-    tm_allow_smem(stem_conv_pool_kernel<true>, SLDS);
-    stem_conv_pool_kernel<true><<<(unsigned)grid, STHREADS, SLDS, (hipStream_t)stream>>>(a);
+    tm_allow_smem(stem_conv_pool_kernel<MODE, true>, SLDS + SRED_BYTES);
+    stem_conv_pool_kernel<MODE, true><<<(unsigned)grid, STHREADS, SLDS + SRED_BYTES, (hipStream_t)stream>>>(a);
   } else {
-    tm_allow_smem(stem_conv_pool_kernel<false>, SLDS);
-    stem_conv_pool_kernel<false><<<(unsigned)grid, STHREADS, SLDS, (hipStream_t)stream>>>(a);
+    tm_allow_smem(stem_conv_pool_kernel<MODE, false>, SLDS + SRED_BYTES);
+    stem_conv_pool_kernel<MODE, false><<<(unsigned)grid, STHREADS, SLDS + SRED_BYTES, (hipStream_t)stream>>>(a);
   }
   TM_CHECK_LAUNCH();
   return 0;
+}
+
+}  // namespace
+
+extern "C" int tm_stem_conv_pool(const void* x, const void* wp, const void* bias, void* out, int N, int H, int W,
+                                 long long sn, long long sc, long long sh, long long sw, void* stream) {
+  StemArgs a;
+  int grid = 0;
+  if (int rc = stem_setup(a, x, wp, N, H, W, sn, sc, sh, sw, &grid)) return rc;
+  TM_REQUIRE(bias && out && ((uintptr_t)out % 16) == 0, "stem_conv_pool: bias / 16-B aligned output");
+  a.bias = (const bf16*)bias; a.out = (bf16*)out;
+  return stem_launch<0>(a, grid, stream);
+}
+
+extern "C" long long tm_stem_bn_stats_workspace(void) { return 2LL * tm_cu_count() * 64 * 3; }
+
+extern "C" int tm_stem_bn_stats(const void* x, const void* wp, int N, int H, int W, long long sn, long long sc,
+                                long long sh, long long sw, const float* gamma, const float* beta,
+                                float* running_mean, float* running_var, float momentum, float eps, float* scale,
+                                float* shift, double* workspace, long long ws_doubles, void* stream) {
+  StemArgs a;
+  int grid = 0;
+  if (int rc = stem_setup(a, x, wp, N, H, W, sn, sc, sh, sw, &grid)) return rc;
+  TM_REQUIRE(gamma && beta && scale && shift && workspace, "stem_bn_stats: bad args");
+  TM_REQUIRE(ws_doubles >= (long long)grid * 64 * 3, "stem_bn_stats: workspace too small");
+  a.part = workspace;
+  if (int rc = stem_launch<1>(a, grid, stream)) return rc;
+  stem_stats_final_kernel<<<1, 64, 0, (hipStream_t)stream>>>(workspace, grid, gamma, beta, running_mean, running_var,
+                                                             momentum, eps, scale, shift);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int tm_stem_conv_pool_bn(const void* x, const void* wp, const float* scale, const float* shift, void* out,
+                                    int N, int H, int W, long long sn, long long sc, long long sh, long long sw,
+                                    void* stream) {
+  StemArgs a;
+  int grid = 0;
+  if (int rc = stem_setup(a, x, wp, N, H, W, sn, sc, sh, sw, &grid)) return rc;
+  TM_REQUIRE(scale && shift && out && ((uintptr_t)out % 16) == 0, "stem_conv_pool_bn: scale / shift / output");
+  a.scale = scale; a.shift = shift; a.out = (bf16*)out;
+  return stem_launch<2>(a, grid, stream);
 }
 
 #ifdef TM_DIAG

@@ -221,6 +221,45 @@ def _stem_conv_pool(x, wp, b):
     return out
 
 
+def _stem_bn_stats(x, wp, bn):
+    """Train-mode bn1 statistics of the stem convolution over the whole bag (tm_stem_bn_stats: the
+    convolution recomputed, never stored): returns fp32 [2, 64] (scale, shift) and updates the
+    module's running statistics as nn.BatchNorm2d does."""
+    from . import _lib
+    from .engine import _p, _stream
+    n, c, h, wd = x.shape
+    if c != 3 or x.dtype != torch.bfloat16:
+        raise RuntimeError("stem_bn_stats: bf16 [n, 3, h, w] tiles expected")
+    st = torch.empty(2, 64, dtype=torch.float32, device=x.device)
+    track = bn.track_running_stats and bn.running_mean is not None
+    if track:
+        bn.num_batches_tracked.add_(1)
+    m = bn.momentum if bn.momentum is not None else (1.0 / float(bn.num_batches_tracked.item()) if track else 0.0)
+    g = bn.weight.detach() if bn.weight is not None else torch.ones(64, device=x.device)
+    b = bn.bias.detach() if bn.bias is not None else torch.zeros(64, device=x.device)
+    ws = torch.empty(_lib.query("tm_stem_bn_stats_workspace"), dtype=torch.float64, device=x.device)
+    sn, sc, sh, sw = x.stride()
+    _lib.call("tm_stem_bn_stats", _p(x), _p(wp), n, h, wd, sn, sc, sh, sw, _p(g), _p(b),
+              _p(bn.running_mean) if track else None, _p(bn.running_var) if track else None, float(m),
+              float(bn.eps), _p(st[0]), _p(st[1]), _p(ws), ws.numel(), _stream())
+    return st
+
+
+def _stem_conv_pool_bn(x, wp, st):
+    """maxpool3x3/2(relu(bn1(conv7x7/2(x)))) with the batch statistics st in one pass
+    (tm_stem_conv_pool_bn): channels-last bf16 [n, 64, PH, PW]."""
+    from . import _lib
+    from .engine import _p, _stream
+    n, c, h, wd = x.shape
+    ch, cw = (h - 1) // 2 + 1, (wd - 1) // 2 + 1
+    out = torch.empty(n, 64, (ch - 1) // 2 + 1, (cw - 1) // 2 + 1, dtype=x.dtype, device=x.device,
+                      memory_format=torch.channels_last)
+    sn, sc, sh, sw = x.stride()
+    _lib.call("tm_stem_conv_pool_bn", _p(x), _p(wp), _p(st[0]), _p(st[1]), _p(out), n, h, wd, sn, sc, sh, sw,
+              _stream())
+    return out
+
+
 def _pack_stem(w):
     """Folded stem weights [64, 3, 7, 7] -> tm_stem_conv_pool's [64][ky][kx 8][c 4] (kx = 7, c = 3 zero)."""
     wp = torch.zeros(64, 7, 8, 4, dtype=w.dtype, device=w.device)
@@ -437,13 +476,21 @@ class RetCCLResNet50(nn.Module):
         w = self._cast
         ws = torch.empty(self._bn_ws_floats(), dtype=torch.float32, device=x.device)
         piece = train_pieces(x.shape[0], self.chunk, x.shape[2], x.shape[3], x.element_size())
-        xs = [_cl(_lib_conv2d(x[i:i + piece], w["conv1.weight"], None, stride=2, padding=3))
-              for i in range(0, x.shape[0], piece)]
-        st = _bn_train_stats(xs, self.bn1, ws)
-        if x.dtype == torch.bfloat16:
-            xs = [_stem_pool_bn_(p, st) for p in xs]
+        if x.dtype == torch.bfloat16 and _stem_fused_enabled():
+            # the stem in two hand-written passes over the tiles (statistics, then conv + BN + ReLU +
+            # pool): the 112 x 112 x 64 conv output is never stored
+            if "stem_packed" not in w:
+                w["stem_packed"] = _pack_stem(w["conv1.weight"])
+            st = _stem_bn_stats(x, w["stem_packed"], self.bn1)
+            xs = [_stem_conv_pool_bn(x[i:i + piece], w["stem_packed"], st) for i in range(0, x.shape[0], piece)]
         else:
-            xs = [_lib_max_pool(_bn_apply_(p, st)) for p in xs]
+            xs = [_cl(_lib_conv2d(_cl(x[i:i + piece]), w["conv1.weight"], None, stride=2, padding=3))
+                  for i in range(0, x.shape[0], piece)]
+            st = _bn_train_stats(xs, self.bn1, ws)
+            if x.dtype == torch.bfloat16:
+                xs = [_stem_pool_bn_(p, st) for p in xs]
+            else:
+                xs = [_lib_max_pool(_bn_apply_(p, st)) for p in xs]
         for si, stage in enumerate((self.layer1, self.layer2, self.layer3, self.layer4), start=1):
             for bi, blk in enumerate(stage):
                 pre = f"layer{si}.{bi}."
@@ -511,8 +558,9 @@ class RetCCLResNet50(nn.Module):
         with torch.set_grad_enabled(grad), torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
             for s in range(0, x.shape[0], chunk):
                 xc = x[s:s + chunk].to(torch.float32 if autocast else dt)
-                if not (not self.training and self.channels_last and dt == torch.bfloat16 and _stem_fused_enabled()):
-                    # (the fused eval stem reads the tiles at any strides: no channels-last copy)
+                if not ((not self.training or fused_train) and self.channels_last and dt == torch.bfloat16
+                        and _stem_fused_enabled()):
+                    # (the fused stem reads the tiles at any strides: no channels-last copy)
                     xc = xc.contiguous(memory_format=torch.channels_last if self.channels_last
                                        else torch.contiguous_format)
                 if not self.training:
