@@ -360,6 +360,9 @@ int tm_stem_bn_stats(const void* x, const void* wp, int N, int H, int W, long lo
                      void* stream);
 int tm_stem_conv_pool_bn(const void* x, const void* wp, const float* scale, const float* shift, void* out, int N,
                          int H, int W, long long sn, long long sc, long long sh, long long sw, void* stream);
+/* out[n, i, j, :] = x[n, s*i, s*j, :] for channels-last x [N, H, W, C] (bf16 / fp32, C * elem % 16
+ * == 0): the input of a stride-s 1x1 downsample convolution (code/models/ResNet.py:130-135). */
+int tm_subsample2d(int dtype, const void* x, void* out, int N, int H, int W, int C, int stride, void* stream);
 /* C5 encoder 1x1 convolution over channels-last rows (code/models/ResNet.py:95-117 conv1 / conv3
  * / downsample with BN folded): y[rows, cout] = act(x[rows, cin] . w[cout, cin]^T (+ bias[cout])
  * (+ residual[rows, cout])), one hipBLASLt GEMM with the bias / residual / ReLU epilogue.

@@ -502,3 +502,15 @@ def test_stem_train_bn_passes_against_torch(n, h, w):
     # order differs (scaled by |scale|)
     tol = ref.abs() * 2 ** -8 + st[0].abs().view(1, 64, 1, 1) * conv.float().abs().amax() * 2 ** -8 + 1e-5
     assert (err <= tol).all(), err.max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_subsample_equals_strided_copy(dtype):
+    """tm_subsample2d (the stride-2 downsample input) against x[:, :, ::2, ::2]: bitwise, odd size."""
+    from transmil_deepgraft_amd import encoder as E
+    x = torch.randn(3, 64, 15, 14, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    out = E._subsample(x, 2)
+    torch.cuda.synchronize()
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(out, x[:, :, ::2, ::2])

@@ -137,6 +137,7 @@ _SIGS = {
     "tm_bias_relu_maxpool": (I, [P, P, P, I, I, I, I, P]),
     "tm_bn_relu_maxpool": (I, [P, P, P, P, I, I, I, I, P]),
     "tm_stem_conv_pool": (I, [P, P, P, P, I, I, I, L, L, L, L, P]),
+    "tm_subsample2d": (I, [I, P, P, I, I, I, I, I, P]),
     "tm_stem_bn_stats_workspace": (L, []),
     "tm_stem_bn_stats": (I, [P, P, I, I, I, L, L, L, L, P, P, P, P, Fl, Fl, P, P, P, L, P]),
     "tm_stem_conv_pool_bn": (I, [P, P, P, P, P, I, I, I, L, L, L, L, P]),

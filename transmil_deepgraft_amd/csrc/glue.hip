@@ -480,6 +480,36 @@ extern "C" int tm_bn_relu_maxpool(const void* y, const float* scale, const float
   return 0;
 }
 
+// Strided spatial subsample of a channels-last activation (the input of a stride-s 1x1 downsample
+// convolution, code/models/ResNet.py:130-135): out[n, i, j, :] = x[n, s*i, s*j, :], one thread per
+// 16-B piece of a pixel's channels (the channel rows stay contiguous on both sides).
+__global__ __launch_bounds__(256) void subsample_kernel(const uint4* __restrict__ x, uint4* __restrict__ out,
+                                                        long long npix_out, int H, int W, int OH, int OW, int s,
+                                                        int pieces) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix_out * pieces) return;
+  const int q = (int)(i % pieces);
+  const long long pix = i / pieces;
+  const int ow = (int)(pix % OW), oh = (int)((pix / OW) % OH);
+  const long long n = pix / ((long long)OW * OH);
+  out[i] = x[((n * H + (long long)oh * s) * W + (long long)ow * s) * pieces + q];
+}
+
+extern "C" int tm_subsample2d(int dtype, const void* x, void* out, int N, int H, int W, int C, int stride,
+                              void* stream) {
+  TM_REQUIRE(x && out && N > 0 && H > 0 && W > 0 && C > 0 && stride > 0, "subsample2d: bad args");
+  const int esz = dtype == TM_BF16 ? 2 : 4;
+  TM_REQUIRE((C * esz) % 16 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0,
+             "subsample2d: 16-B channel rows and buffers");
+  const int OH = (H - 1) / stride + 1, OW = (W - 1) / stride + 1, pieces = C * esz / 16;
+  const long long npix = (long long)N * OH * OW;
+  const long long threads = npix * pieces;
+  subsample_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      (const uint4*)x, (uint4*)out, npix, H, W, OH, OW, stride, pieces);
+  TM_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int tm_bias_act(int dtype, void* y, const void* bias, long long rows, int C, int relu, void* stream) {
   TM_REQUIRE(y && bias && rows >= 0 && C > 0 && C % 8 == 0, "bias_act: bad args (C % 8 == 0)");
   TM_REQUIRE(((uintptr_t)y % 16) == 0 && ((uintptr_t)bias % 16) == 0, "bias_act: 16-B aligned buffers");
