@@ -124,8 +124,9 @@ def main():
         "mil_ms": round(t_mil * 1e3, 3),
         "roofline": {"bound": "mfma", "achieved": round(enc_tfs, 1), "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": round(enc_tfs / BF16_PEAK_TFS, 4), "traffic": None,
-                     "kernel": f"encoder ({a.encoder_mode} BN): MIOpen / CK 3x3 + stem convolutions, hipBLASLt 1x1 "
-                               "GEMMs (tm_conv1x1), HIP BatchNorm / bias passes",
+                     "kernel": f"encoder ({a.encoder_mode} BN): hand-written stem (conv + BN + ReLU + pool, "
+                               "tm_stem_*), MIOpen / CK 3x3 convolutions, hipBLASLt 1x1 GEMMs (tm_conv1x1), "
+                               "HIP BatchNorm / bias passes",
                      "algorithmic_flops": int(R50_GFLOP_PER_TILE * 1e9 * a.n), "ms": round(t_enc * 1e3, 3)},
         "cpu_baseline": cpu,
     }), flush=True)
