@@ -62,9 +62,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_rccl_allreduce_inside_captured_graph(overlap):
-    """init_process_group("nccl") at world size 1 with the collective forced: the whole step
+def _rccl_graph_body(overlap):
+    """(Run in a child process by test_rccl_allreduce_inside_captured_graph.)  init_process_group("nccl") at world size 1 with the collective forced: the whole step
     (forward, CE, fused backward whose part-0 hook issues the RCCL all_reduce mid-backward when
     ``overlap``, the wait + 1/world scale, fused RAdam+Lookahead) captured as ONE hipGraph and
     replayed, against the same steps run eagerly without any collective."""
@@ -129,6 +128,22 @@ def test_rccl_allreduce_inside_captured_graph(overlap):
         gc.collect()
         torch.cuda.synchronize()
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_rccl_allreduce_inside_captured_graph(overlap):
+    """_rccl_graph_body in a child process of its own: each parametrisation gets a fresh NCCL
+    process group (initialising and destroying one twice in a single process aborted the whole
+    pytest process once in a round-5 suite run -- a failure here now fails only this test)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = (f"import sys; sys.path.insert(0, {here!r}); sys.path.insert(0, {os.path.dirname(here)!r}); "
+            f"import test_ddp_gpu as T; T._rccl_graph_body({overlap!r}); print('RCCL_GRAPH_OK')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(here), capture_output=True, timeout=300)
+    out = (r.stdout + r.stderr).decode(errors="replace")
+    assert r.returncode == 0 and "RCCL_GRAPH_OK" in out, f"rc={r.returncode}\n{out[-4000:]}"
 
 
 @pytest.mark.parametrize("k,npatch", [(1, 700), (3, 700), (1, 8192)])
