@@ -2,7 +2,7 @@
 # Config C5 at its own size on one GPU: scripts/bench_c5.py (4096 tiles -> ResNet-50 -> TransMIL(2048),
 # train step) in eval-BN and train-BN encoder modes, then a rocprofv3 kernel trace of the eval run.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r04}

@@ -2,7 +2,7 @@
 # One measurement session on the GPU box: the default bench line, a kernel trace + stats of a
 # short bench, and the PMC passes (each step under its own time limit; the first failure ends it).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r02}

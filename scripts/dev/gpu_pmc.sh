@@ -1,8 +1,8 @@
 #!/bin/bash
 # rocprofv3 PMC counters (kernel trace only, no other tracing) for one microbench case.
-#   CASE="gemm qkv (NT" COUNTERS="SQ_WAVE_CYCLES SQ_WAIT_ANY ..." bash scripts/gpu_pmc.sh
+#   CASE="gemm qkv (NT" COUNTERS="SQ_WAVE_CYCLES SQ_WAIT_ANY ..." bash scripts/dev/gpu_pmc.sh
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 OUT=${PMC_OUT:-gpurun_out/pmc}

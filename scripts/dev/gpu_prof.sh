@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocprofv3 kernel-trace + stats of a short bench run (no PMC counters here).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 OUT=${PROF_OUT:-gpurun_out/prof}

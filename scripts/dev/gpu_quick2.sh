@@ -2,7 +2,7 @@
 # Quick GPU check: selected kernel tests (K), the whole-model parity tests, one bench line (+ rocprof
 # kernel stats when PROF=1).  Every GPU step has its own time limit; the first failure ends it.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 T="python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread"

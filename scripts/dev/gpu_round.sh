@@ -2,7 +2,7 @@
 # One GPU session: tests, then (only if no crash) a short bench.  Every GPU step
 # has its own time limit; a crash/timeout ends the script.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 TESTS="${TESTS:-tests}"
 timeout -k 10 900 python -u -m pytest $TESTS -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1

@@ -9,7 +9,7 @@
 #   c5       scripts/bench_c5.py (C5_ARGS=)                      -> c5.log
 #   pmc      PMC passes over the bench (scripts/gpu_pmc_bench.sh) -> pmc/
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r05}
 OUT=gpurun_out/$TAG

@@ -1,7 +1,7 @@
 #!/bin/bash
 # split pinv: tests, ablation microbench, and a kernel trace of the split forward / backward
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_pinv_split_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/t_split.log 2>&1

@@ -2,7 +2,7 @@
 # Diagnostic build stamp runs (libtransmil_hip_diag.so): per-phase s_memtime of the A3 forward and
 # backward at the bench shape.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 timeout -k 10 120 python scripts/dev/a3_fwd_stamps.py > gpurun_out/st_a3f.log 2>&1 || { tail -20 gpurun_out/st_a3f.log; exit 1; }
 cat gpurun_out/st_a3f.log

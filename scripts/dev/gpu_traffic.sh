@@ -2,7 +2,7 @@
 # HBM traffic of the bench's probed kernel from rocprofv3 PMC counters: one pass per
 # counter (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass), kernel-trace only.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
