@@ -1,13 +1,15 @@
 """A/B of attention-backward variants (diagnostic build, nys variants) on the bench shapes: the A1
 backward (tm_nys_a1_bwd_dqkv) and the fused A3 backward (tm_nys_a3_bwd_fused), 100 calls each per
-variant.  Run under `rocprofv3 --kernel-trace --stats`: each variant is its own template instance,
-so the kernel stats separate them.
+variant, then graph-replayed us per call of each (variants in the order given, twice).  Under
+`rocprofv3 --kernel-trace --stats` each variant is its own template instance, so the kernel stats
+separate them.
 
     TRANSMIL_HIP_LIB=transmil_deepgraft_amd/libtransmil_hip_diag.so python scripts/dev/attn_bwd_ab.py 0 36
 """
 import ctypes as C
 import os
 import sys
+import time
 
 sys.path.insert(0, os.getcwd())
 os.environ.setdefault("TRANSMIL_HIP_LIB", os.path.join(os.getcwd(), "transmil_deepgraft_amd", "libtransmil_hip_diag.so"))
@@ -58,5 +60,26 @@ for var in [int(x) for x in (sys.argv[1:] or ["0", "36"])]:
     else:
         print(f"variant {var}: max |diff| vs first variant (dqkv, dkl, dy, dql):",
               [f"{(a - b).abs().max().item():.3e}" for a, b in zip(out, ref)], flush=True)
+
+
+def timeit(fn, reps=50):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        for _ in range(reps):
+            fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    gr.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps * 1e6
+
+
+for rep in range(2):
+    for var in [int(x) for x in (sys.argv[1:] or ["0", "36"])]:
+        L.tm_debug_set_nys_variant(var)
+        print(f"variant {var}: A1 bwd {timeit(a1):.2f} us, A3 bwd {timeit(a3):.2f} us", flush=True)
 L.tm_debug_set_nys_variant(0)
 print("done", flush=True)

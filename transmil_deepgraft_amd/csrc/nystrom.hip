@@ -668,7 +668,82 @@ TM_DEV void attn_fwd_wave_il(const bf16* ks, const bf16* vt, const bf16x8 (&qf)[
   sum = l;
 }
 
-template <int VAR = 0>  // ablation: 1 no conv MFMAs, 2 no attention phase, 3 prologue only, 9 stamps
+// attn_fwd_wave_il with its LDS fragments software-pipelined one tile ahead (one wave per SIMD
+// has no partner wave to hide a read's latency: the il form waited on every key / value read
+// right before its MFMA).  Key fragments of tile kt + 1 and value fragments of tile kt + 1 are
+// issued before the MFMAs of tile kt; the max tree of tile kt - 1 and the exp / pack of tile
+// kt + 1 run beside them.  Same arithmetic, same order of every sum: bitwise the il results
+// (scripts/dev/fwd_pipe_ab.py: 14.4 -> 13.8 us per call at the bench shape).
+TM_DEV void attn_fwd_wave_pipe(const bf16* ks, const bf16* vt, const bf16x8 (&qf)[4], f32x16 (&o)[2], float& mx,
+                               float& sum, int lane) {
+  constexpr int KROW = Lay<bf16>::KROW;
+  const int r = lane & 31, h = lane >> 5;
+  f32x16 s[8];
+  float mk[8];
+  bf16x8 kf[2][4];
+#pragma unroll
+  for (int st = 0; st < 4; ++st) kf[0][st] = load8(ks + r * KROW + st * 16 + 8 * h);
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    if (kt < 7) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st) kf[(kt + 1) & 1][st] = load8(ks + ((kt + 1) * 32 + r) * KROW + st * 16 + 8 * h);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead (the scheduler sinks reads to their use)
+    s[kt] = (f32x16){};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) mma16(s[kt], kf[kt & 1][st], qf[st]);
+    if (kt > 0) mk[kt - 1] = tree_max16(s[kt - 1]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  mk[7] = tree_max16(s[7]);
+  float m = fmaxf(fmaxf(fmaxf(mk[0], mk[1]), fmaxf(mk[2], mk[3])), fmaxf(fmaxf(mk[4], mk[5]), fmaxf(mk[6], mk[7])));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  const float ml = m * LOG2E;
+  o[0] = (f32x16){};
+  o[1] = (f32x16){};
+  float lk[8];
+  bf16x8 vf[2][4], pf[2][2];
+#pragma unroll
+  for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) vf[0][2 * sp + dt] = value_frag<bf16>(vt, dt, 16 * sp, lane);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s[0][i] = __builtin_amdgcn_exp2f(fmaf(s[0][i], LOG2E, -ml));
+  lk[0] = tree_sum16(s[0]);
+  pf[0][0] = acc_as_operand<bf16>(s[0], 0);
+  pf[0][1] = acc_as_operand<bf16>(s[0], 1);
+#pragma unroll
+  for (int kt = 0; kt < 8; ++kt) {
+    const int b = kt & 1, nb = b ^ 1;
+    if (kt < 7) {
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) vf[nb][2 * sp + dt] = value_frag<bf16>(vt, dt, (kt + 1) * 32 + 16 * sp, lane);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) mma16(o[dt], vf[b][2 * sp + dt], pf[b][sp]);
+    if (kt < 7) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s[kt + 1][i] = __builtin_amdgcn_exp2f(fmaf(s[kt + 1][i], LOG2E, -ml));
+      lk[kt + 1] = tree_sum16(s[kt + 1]);
+      pf[nb][0] = acc_as_operand<bf16>(s[kt + 1], 0);
+      pf[nb][1] = acc_as_operand<bf16>(s[kt + 1], 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float l = ((lk[0] + lk[1]) + (lk[2] + lk[3])) + ((lk[4] + lk[5]) + (lk[6] + lk[7]));
+  l += __shfl_xor(l, 32, 64);
+  mx = m;
+  sum = l;
+}
+
+template <int VAR = 0>  // ablation: 1 no conv MFMAs, 2 no attention phase, 3 prologue only, 9 stamps,
+                        // 6 the earlier attention form (attn_fwd_wave_il: reads just in time)
 __global__ __launch_bounds__(256) void a1_fwd_bf16_kernel(const bf16* __restrict__ q, const bf16* __restrict__ v,
                                                           const bf16* __restrict__ kl_t, const bf16* __restrict__ y_t,
                                                           const float* __restrict__ wconv, int n, int nh, int wpg,
@@ -752,7 +827,8 @@ __global__ __launch_bounds__(256) void a1_fwd_bf16_kernel(const bf16* __restrict
         o[0] = (f32x16){}; o[1] = (f32x16){};
         mx = to_f(qf[0][0]);
       } else {
-        attn_fwd_wave_il(ks, vt, qf, o, mx, sum, lane);
+        if constexpr (VAR == 6) attn_fwd_wave_il(ks, vt, qf, o, mx, sum, lane);
+        else attn_fwd_wave_pipe(ks, vt, qf, o, mx, sum, lane);
       }
     }
     if (first) a1p_stamp<VAR>(2, wave);
@@ -1747,6 +1823,7 @@ TM_DEV bf16x8 frag_tr_acc(const bf16* S, int mb, int kb, int lane) { return frag
 // waves go on to the next chunk's S / dP / dV / dK meanwhile).  DQ2 = 0: the earlier form (every
 // wave a key group's partial, summed through LDS by the group-0 waves; diagnostic build only).
 template <int MODE, int NW = 8, int ST = 0, int DQ2 = 1>   // ST: diagnostic s_memtime stamps (g_a1_stamps): 1 phases, 2 one chunk
+                                                           // DQ2 = 2: the DQ2 chain with its reads just in time
 __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
   using LY = std::conditional_t<NW == 9, BwdLay9, BwdLay16>;
   static_assert(NW == 8 || (NW == 9 && MODE == MODE_A3), "9-wave form: A3 even split only");
@@ -1901,11 +1978,32 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
       if (wave == W0 || wave == W0 + 1) {
         const int dtq = wave - W0;
         f32x16 acc = (f32x16){};
-        // (partly unrolled: fully unrolled, the hoisted operand reads spill the 9-wave form)
+        if constexpr (DQ2 == 1) {
+          // software-pipelined: the operand reads of k-steps st + 2, st + 3 are issued before the
+          // MFMAs of st, st + 1 (left to itself the compiler sinks each pair of reads to its MFMAs and
+          // waits on them: A1 backward 38.5 -> 37.7 us, A3 32.9 -> 32.6, bitwise the same)
+          constexpr int NS = 2 * NW;
+          const bf16* da = ds_s + r * DS_ROW + 8 * h;
+          const bf16* kb = kt_s + (dtq * 32 + r) * KT_ROW + 8 * h;
+          bf16x8 fa[4], fb[4];
+#pragma unroll
+          for (int st = 0; st < 2; ++st) { fa[st] = load8(da + st * 16); fb[st] = load8(kb + st * 16); }
+#pragma unroll
+          for (int st = 0; st < NS; st += 2) {
+#pragma unroll
+            for (int u = 2; u < 4; ++u)
+              if (st + u < NS) { fa[(st + u) & 3] = load8(da + (st + u) * 16); fb[(st + u) & 3] = load8(kb + (st + u) * 16); }
+            __builtin_amdgcn_sched_barrier(0);
+            mma16(acc, fa[st & 3], fb[st & 3]);
+            if (st + 1 < NS) mma16(acc, fa[(st + 1) & 3], fb[(st + 1) & 3]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        } else {   // DQ2 == 2 (diagnostic build): the reads just in time
 #pragma unroll
         for (int st = 0; st < 2 * NW; ++st) {
           const int kk = st * 16 + 8 * h;
           mma16(acc, load8(ds_s + r * DS_ROW + kk), load8(kt_s + (dtq * 32 + r) * KT_ROW + kk));
+        }
         }
         cstamp(c0, 4);
         if (MODE == MODE_A1 && a.dqkv) {
@@ -2382,7 +2480,7 @@ extern "C" int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void
     // ablation variants 11-19 (microbench only): 10 + VAR
     auto kern = NYS_VARIANT == 11 ? a1_fwd_bf16_kernel<1> : NYS_VARIANT == 12 ? a1_fwd_bf16_kernel<2>
               : NYS_VARIANT == 13 ? a1_fwd_bf16_kernel<3> : NYS_VARIANT == 19 ? a1_fwd_bf16_kernel<9>
-              : a1_fwd_bf16_kernel<0>;
+              : NYS_VARIANT == 16 ? a1_fwd_bf16_kernel<6> : a1_fwd_bf16_kernel<0>;
 #else
     auto kern = a1_fwd_bf16_kernel<0>;
 #endif
@@ -2526,6 +2624,9 @@ int a1_bwd_impl(int dtype, const void* q, const void* dmerged, const void* kl_t,
     } else if (NYS_VARIANT == 35) {   // diagnostic: the earlier cross-wave dQ form
       tm_allow_smem(attn_bwd_bf16_kernel<MODE_A1, 8, 0, 0>, BwdLay16::BYTES);
       attn_bwd_bf16_kernel<MODE_A1, 8, 0, 0><<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
+    } else if (NYS_VARIANT == 36) {   // diagnostic: the dQ chain with its reads just in time
+      tm_allow_smem(attn_bwd_bf16_kernel<MODE_A1, 8, 0, 2>, BwdLay16::BYTES);
+      attn_bwd_bf16_kernel<MODE_A1, 8, 0, 2><<<dim3(nqc, nbh), 512, BwdLay16::BYTES, st>>>(a);
     } else
 #endif
     {
@@ -2579,6 +2680,11 @@ void launch_a3_bwd_bf16(BwdArgs& a, int nbh, int n, hipStream_t st, int& slabs) 
     if (NYS_VARIANT == 35) {   // diagnostic: the earlier cross-wave dQ form
       tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9, 0, 0>, BwdLay9::BYTES);
       attn_bwd_bf16_kernel<MODE_A3, 9, 0, 0><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
+      return;
+    }
+    if (NYS_VARIANT == 36) {   // diagnostic: the dQ chain with its reads just in time
+      tm_allow_smem(attn_bwd_bf16_kernel<MODE_A3, 9, 0, 2>, BwdLay9::BYTES);
+      attn_bwd_bf16_kernel<MODE_A3, 9, 0, 2><<<dim3(sp.wpg, nbh), 576, BwdLay9::BYTES, st>>>(a);
       return;
     }
 #endif
