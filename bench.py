@@ -126,16 +126,45 @@ def roofline_model(site, n_patches, dtype_bytes):
 HBM_SITES = ("ln_fwd", "landmarks", "a3_fwd", "a1_fwd", "ppeg_fwd", "ppeg_bwd", "conv_bwd", "a1_bwd", "a3_bwd")
 
 # the dense d_model projections (code/models/TransMIL.py:26-34 to_qkv / to_out, :128-133 _fc1) and
-# their backward products: site -> (layers in call order, M, N, K as functions of (n', N patches))
+# their backward products, in bf16 mode: site -> (layers in call order, shape(n', N patches, layer) ->
+# (M, N, K, algorithmic HBM bytes), what).  The shapes are the ones the engine launches
+# (tests/test_interface.py::test_gemm_sites_match_the_engine_launches records them): layer 2's
+# backward (the class-row layer) runs the k / v part of to_qkv only (K = 2D; its q part goes through
+# tm_cls_q_rows' two small products, engine.CLS_Q_ROWS); layer 2 has no dense to_out GEMMs.
+# Bytes: every operand read once and every final output written once (bf16 T = 2 B operands, fp32
+# residual stream and weight gradients; split-K slabs are not algorithmic).
+_D, _T = 512, 2
+
+
+def _S(N):
+    import math
+    G = math.ceil(math.sqrt(N))
+    return G * G + 1
+
+
+def _qkv_k(layer):
+    from transmil_deepgraft_amd import engine
+    return 2 * _D if (layer == 2 and engine.CLS_Q_ROWS) else 3 * _D
+
+
 GEMM_SITES = {
-    "fc1_gemm": ((0,), lambda n, N: (N, 512, 512), "_fc1 Linear + GELU (+ grid-pad rows)"),
-    "qkv_gemm": ((1, 2), lambda n, N: (n, 1536, 512), "to_qkv (+ head-major scatter, q scale)"),
-    "out_gemm": ((1,), lambda n, N: (n, 512, 512), "to_out + bias + dropout + residual"),
-    "wgrad_out": ((1,), lambda n, N: (512, 512, n), "dW_out split-K (+ bias gradient)"),
-    "dmerged_gemm": ((1,), lambda n, N: (n, 512, 512), "dmerged = dout W_out"),
-    "wgrad_qkv": ((2, 1), lambda n, N: (1536, 512, n), "dW_qkv split-K"),
-    "dxn_gemm": ((2, 1), lambda n, N: (n, 512, 1536), "dxn = dqkv W_qkv"),
-    "wgrad_fc1": ((0,), lambda n, N: (512, 512, N), "dW_fc1 split-K (+ bias gradient)"),
+    "fc1_gemm": ((0,), lambda n, N, L: (N, _D, 512, N * 512 * _T + _D * 512 * _T + _D * 4 + (_S(N) - 1) * _D * 4
+                                        + N * _D * _T),
+                 "_fc1 Linear + GELU (+ grid-pad rows): x, W in; H0 (fp32), pre-activation out"),
+    "qkv_gemm": ((1, 2), lambda n, N, L: (n, 3 * _D, _D, n * _D * _T + 3 * _D * _D * _T + 3 * n * _D * _T),
+                 "to_qkv (+ head-major scatter, q scale): xn, W in; q, k, v out"),
+    "out_gemm": ((1,), lambda n, N, L: (n, _D, _D, n * _D * _T + _D * _D * _T + 2 * _S(N) * _D * 4),
+                 "to_out + bias + dropout + residual: merged, W, H in; H' (fp32) out"),
+    "wgrad_out": ((1,), lambda n, N, L: (_D, _D, n, 2 * n * _D * _T + (_D * _D + _D) * 4),
+                  "dW_out split-K (+ bias gradient): dout, merged in; dW, db (fp32) out"),
+    "dmerged_gemm": ((1,), lambda n, N, L: (n, _D, _D, 2 * n * _D * _T + _D * _D * _T),
+                     "dmerged = dout W_out"),
+    "wgrad_qkv": ((2, 1), lambda n, N, L: (_qkv_k(L), _D, n, n * _qkv_k(L) * _T + n * _D * _T + _qkv_k(L) * _D * 4),
+                  "dW_qkv split-K (layer 2: the k / v rows): dqkv, xn in; dW (fp32) out"),
+    "dxn_gemm": ((2, 1), lambda n, N, L: (n, _D, _qkv_k(L), n * _qkv_k(L) * _T + _qkv_k(L) * _D * _T + n * _D * _T),
+                 "dxn = dqkv W_qkv (layer 2: K = 2D)"),
+    "wgrad_fc1": ((0,), lambda n, N, L: (_D, 512, N, N * _D * _T + N * 512 * _T + (_D * 512 + _D) * 4),
+                  "dW_fc1 split-K (+ bias gradient): dpre, x in; dW, db (fp32) out"),
 }
 
 
@@ -207,9 +236,11 @@ def probe_site_times(engine, run_step, steps, sites):
 
 
 def gemm_roofline(per, n_patches):
-    """The dense projections against the dense bf16 MFMA peak: algorithmic flops (2 M N K) / the
-    probe's median event span per call site and layer (the split-K products' slab sums run in the
-    deferred flush, not in this span)."""
+    """The dense projections against their roofline: a site's time floor is
+    max(flops / dense bf16 peak, algorithmic bytes / HBM peak); ``frac`` = that floor / the probe's
+    median event span per call site and layer, ``bound`` says which term sets the floor (the
+    to_out and _fc1 epilogues move more bytes than their flops need).  The split-K products' slab
+    sums run in the deferred flush, not in this span."""
     import math
     G = math.ceil(math.sqrt(n_patches))
     n = (G * G + 1 + 255) // 256 * 256
@@ -218,14 +249,17 @@ def gemm_roofline(per, n_patches):
         xs = per.get(site, [])
         if not xs or len(xs) % len(layers):
             continue
-        M, N, K = shape(n, n_patches)
-        flops = 2 * M * N * K
         for k, layer in enumerate(layers):
+            M, N, K, byts = shape(n, n_patches, layer)
+            flops = 2 * M * N * K
             v = sorted(xs[k::len(layers)])
             ms = v[len(v) // 2]
-            tfs = flops / (ms / 1e3) / 1e12
-            out.append(dict(site=site, layer=layer, what=what, M=M, N=N, K=K, flops=flops, us=round(ms * 1e3, 2),
-                            achieved_tfs=round(tfs, 1), peak_tfs=BF16_PEAK_TFS, frac=round(tfs / BF16_PEAK_TFS, 4)))
+            sec = ms / 1e3
+            tf, tb = flops / (BF16_PEAK_TFS * 1e12), byts / (HBM_PEAK_GBS * 1e9)
+            out.append(dict(site=site, layer=layer, what=what, M=M, N=N, K=K, flops=flops, algorithmic_bytes=byts,
+                            us=round(ms * 1e3, 2), achieved_tfs=round(flops / sec / 1e12, 1),
+                            achieved_gbs=round(byts / sec / 1e9, 1), bound="mfma" if tf >= tb else "hbm",
+                            frac_mfma=round(tf / sec, 4), frac_hbm=round(tb / sec, 4), frac=round(max(tf, tb) / sec, 4)))
     return out
 
 
@@ -330,8 +364,10 @@ def make_step(task, opt, allreduce, bags, labels, K, warmup, eager=False):
     (accumulate_grad_batches, Lightning's semantics as TransMILTask.optimization_step): micro-batch
     i is "first" (i % K == 0: loss / K, gradients written), "mid" (added) or "last" ((i + 1) % K == 0:
     added, all-reduced, optimizer step), one captured graph per (bag, phase).  Warm-up: warmup * K
-    eager micro-batches (at least 2 K) on a side stream before the captures.  Returns a namespace
-    with ``step``, ``body(x, y, phase)``, ``load(i)`` and ``graph`` (None when eager)."""
+    eager micro-batches (at least 2 K) on a side stream before the captures, then every captured
+    graph replayed once (micro-batches 0 .. len(bags) * K - 1).  Returns a namespace with ``step``,
+    ``body(x, y, phase)``, ``load(i)``, ``graph`` (None when eager) and ``warm_micro`` = (eager
+    warm-up micro-batches, warm-up replays)."""
     static_x = torch.empty_like(bags[0])
     static_y = torch.empty_like(labels[0])
 
@@ -388,7 +424,16 @@ def make_step(task, opt, allreduce, bags, labels, K, warmup, eager=False):
 
         def step(i):
             graphs[i % len(bags), phase_of(i)].replay()
-    return types.SimpleNamespace(step=step, body=body, load=load, graph=graph, phase_of=phase_of)
+
+        # every captured graph replayed once before the timed region (untimed warm-up, real steps):
+        # a graph's first replay pays one-time work (the executable's upload, first-touch of its
+        # pool), which a short timed run (the driver's --steps 20) must not carry.  len(bags) * K
+        # micro-batches = every (bag, phase) graph, ending on an accumulation boundary.
+        for i in range(len(bags) * K):
+            step(i)
+        torch.cuda.synchronize()
+    return types.SimpleNamespace(step=step, body=body, load=load, graph=graph, phase_of=phase_of,
+                                 warm_micro=(max(warmup, 2) * K, 0 if eager else len(bags) * K))
 
 
 def main():

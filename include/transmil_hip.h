@@ -13,7 +13,11 @@
  *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream);
  *   - no host synchronisation, so every call is hipGraph-capturable -- with ONE documented
  *     exception, tm_conv1x1_tune (a host-timed algorithm search, refused during capture);
- *   - deterministic: no float atomics, fixed reduction orders;
+ *   - deterministic: no float atomics, fixed reduction orders -- every result is a function of
+ *     the inputs alone, with ONE documented exception: tm_conv1x1 after tm_conv1x1_tune runs the
+ *     algorithm the tune call timed fastest IN THIS PROCESS, so two processes that tuned may
+ *     round the C5 encoder features differently (the Python encoder skips the tune under
+ *     torch.use_deterministic_algorithms(True) or TM_CONV1X1_TUNE=0: heuristic first choice);
  *   - return 0 on success, 1 on a bad argument, 2 on a launch error;
  *     tm_last_error() returns the thread-local message.
  *   - dtype enum: TM_F32 = 0, TM_BF16 = 1 (activations / MFMA operands).

@@ -36,14 +36,48 @@ def bag(rank, micro, n=N_PATCHES):
     return x, torch.tensor([(rank + micro) % 2], device="cuda"), None   # (bags, labels, names)
 
 
-def main(out_path, k, steps, n=N_PATCHES):
+C5_TILES = 8
+
+
+def build_c5_model():
+    """The C5 image path (ImageBagModel: frozen RetCCL ResNet-50, eval-mode BN, bf16 channels-last
+    -> TransMIL(2, 2048) on its RCC-2048 _fc1 branch, bf16, train mode); model_interface.py:237-247,
+    300-316."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import deterministic_encoder_params_
+    from transmil_deepgraft_amd.encoder import ImageBagModel, retccl_resnet50
+    from transmil_deepgraft_amd.models import TransMIL
+    enc = retccl_resnet50()
+    deterministic_encoder_params_(enc, 2021)
+    enc = enc.set_compute_dtype(torch.bfloat16).eval().cuda()
+    torch.manual_seed(0)
+    mil = TransMIL(2, 2048).cuda().train().set_compute_dtype(torch.bfloat16)
+    return ImageBagModel(enc, mil)
+
+
+def c5_bag(rank, micro, n=C5_TILES):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from golden_util import encoder_tiles
+    x = torch.from_numpy(encoder_tiles(n, seed=500 + 100 * rank + micro)).cuda().view(1, n, 3, 224, 224)
+    return x, torch.tensor([(rank + micro) % 2], device="cuda"), None
+
+
+def main(out_path, k, steps, n=N_PATCHES, mode="feat"):
     import torch.distributed as dist
     from transmil_deepgraft_amd.interface import GradAllReduce, TransMILTask
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
     rank = dist.get_rank()
-    model = build_model()
-    ar = GradAllReduce(model.parameters(), model=model, overlap=True)
+    if mode == "c5":
+        model = build_c5_model()
+        # the frozen encoder has no trainable parameters: the bucket holds the MIL model's
+        ar = GradAllReduce(model.parameters(), model=model.model, overlap=True)
+        assert len(ar.bucket.ranges) == 3           # world > 1: layer1 cut from the _fc1 part
+        data = lambda micro: c5_bag(rank, micro, n)     # noqa: E731
+    else:
+        model = build_model()
+        ar = GradAllReduce(model.parameters(), model=model, overlap=True)
+        data = lambda micro: bag(rank, micro, n)        # noqa: E731
     issued = []      # parts whose all_reduce the backward's ready() hook issued (mid-backward)
 
     def spy(i, inner=ar._on_ready):
@@ -55,14 +89,18 @@ def main(out_path, k, steps, n=N_PATCHES):
     task = TransMILTask(model, accumulate_grad_batches=k)
     opt = task.configure_optimizers()[0][0]
     for micro in range(steps * k):
-        task.optimization_step(bag(rank, micro, n), opt, allreduce=ar)
+        task.optimization_step(data(micro), opt, allreduce=ar)
     torch.cuda.synchronize()
-    owned = all(ar.bucket.owns(p) for p in model.parameters()) or all(p.grad is None for p in model.parameters())
-    torch.save({"params": {n: p.detach().cpu() for n, p in model.named_parameters()},
-                "issued": issued, "owned": owned, "rank": rank}, out_path)
+    trainable = [p for p in model.parameters() if p.requires_grad]
+    owned = all(ar.bucket.owns(p) for p in trainable) or all(p.grad is None for p in trainable)
+    torch.save({"params": {n: p.detach().cpu() for n, p in model.named_parameters() if p.requires_grad},
+                "issued": issued, "owned": owned, "rank": rank, "parts": len(ar.bucket.ranges),
+                "exposed_bytes": ar.exposed_bytes()}, out_path)
+    ar.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else N_PATCHES)
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]) if len(sys.argv) > 4 else N_PATCHES,
+         sys.argv[5] if len(sys.argv) > 5 else "feat")

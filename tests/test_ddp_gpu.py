@@ -62,7 +62,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rccl_graph_body(overlap):
+def _rccl_graph_body(overlap, teardown="close"):
     """(Run in a child process by test_rccl_allreduce_inside_captured_graph.)  init_process_group("nccl") at world size 1 with the collective forced: the whole step
     (forward, CE, fused backward whose part-0 hook issues the RCCL all_reduce mid-backward when
     ``overlap``, the wait + 1/world scale, fused RAdam+Lookahead) captured as ONE hipGraph and
@@ -121,29 +121,36 @@ def _rccl_graph_body(overlap):
         for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
             torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6, msg=n)
     finally:
-        # the captured graph holds the communicator's kernels and the hook's work handles:
-        # release both (and drain the device) before the communicator is destroyed
+        # teardown order: the captured graph holds the communicator's kernels
+        # (and RCCL's registration of the buffers it captured), the model's bucket holds the
+        # all-reduce's hook: drop the graph, close the all-reduce, drain, THEN destroy the group
         torch.cuda.synchronize()
-        graph = ar = None
+        if teardown == "close":
+            if graph is not None:
+                graph.reset()
+            if ar is not None:
+                ar.close()
+        graph = ar = None       # teardown == "old": the round-5 order (scripts/dev/rccl_teardown.py)
         gc.collect()
         torch.cuda.synchronize()
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_rccl_allreduce_inside_captured_graph(overlap):
-    """_rccl_graph_body in a child process of its own: each parametrisation gets a fresh NCCL
-    process group (initialising and destroying one twice in a single process aborted the whole
-    pytest process once in a round-5 suite run -- a failure here now fails only this test)."""
+def test_rccl_allreduce_inside_captured_graph():
+    """_rccl_graph_body for overlap off, then on, in ONE child process: two NCCL process groups
+    initialised and destroyed back to back, each after a hipGraph captured over its all-reduce,
+    with the teardown order GradAllReduce.close() documents.  (The child process keeps a failure
+    from taking the pytest process with it; it is not needed for the two groups to coexist.)"""
     import os
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     code = (f"import sys; sys.path.insert(0, {here!r}); sys.path.insert(0, {os.path.dirname(here)!r}); "
-            f"import test_ddp_gpu as T; T._rccl_graph_body({overlap!r}); print('RCCL_GRAPH_OK')")
+            f"import test_ddp_gpu as T; T._rccl_graph_body(False); print('RCCL_GRAPH_OK 0', flush=True); "
+            f"T._rccl_graph_body(True); print('RCCL_GRAPH_OK 1', flush=True)")
     r = subprocess.run([sys.executable, "-c", code], cwd=os.path.dirname(here), capture_output=True, timeout=300)
     out = (r.stdout + r.stderr).decode(errors="replace")
-    assert r.returncode == 0 and "RCCL_GRAPH_OK" in out, f"rc={r.returncode}\n{out[-4000:]}"
+    assert r.returncode == 0 and "RCCL_GRAPH_OK 1" in out, f"rc={r.returncode}\n{out[-4000:]}"
 
 
 @pytest.mark.parametrize("k,npatch", [(1, 700), (3, 700), (1, 8192)])
@@ -185,7 +192,10 @@ def test_two_ranks_average_through_the_hip_engine(k, npatch, tmp_path):
         assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-3000:]}"
     res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     for r in range(world):
-        assert res[r]["issued"] == [0, 1] * steps, res[r]["issued"]
+        # world 2: three bucket parts, each issued by the backward's ready() hook (part 1 before the
+        # _fc1 backward, part 2 at its end)
+        assert res[r]["parts"] == 3
+        assert res[r]["issued"] == [0, 1, 2] * steps, res[r]["issued"]
     for n in res[0]["params"]:
         torch.testing.assert_close(res[0]["params"][n], res[1]["params"][n], rtol=0, atol=0, msg=n)
 
@@ -209,3 +219,67 @@ def test_two_ranks_average_through_the_hip_engine(k, npatch, tmp_path):
         torch.testing.assert_close(got, p.detach().cpu(), rtol=1e-5, atol=1e-7, msg=n)
         moved = max(moved, (p.detach() - start[n]).abs().max().item())
     assert moved > 1e-5      # the steps changed the parameters (the comparison is not vacuous)
+
+
+def test_two_ranks_average_the_c5_image_path(tmp_path):
+    """BASELINE config C5's image path under DDP: two processes on the one GPU (gloo), each
+    running ImageBagModel (frozen RetCCL ResNet-50, bf16, eval-mode BN -> TransMIL(2, 2048) RCC-2048
+    branch, bf16, train mode) on its own 8-tile bags through TransMILTask.optimization_step with
+    GradAllReduce over the MIL parameters (three bucket parts, each issued mid-backward).  After 2
+    optimizer steps both ranks hold the same parameters, equal (rtol 1e-5) to one process that
+    runs both ranks' bags with loss / 2 through the same kernels (reference: Lightning DDP,
+    code/train.py:178-201; ModelInterface.forward's image branch, model_interface.py:300-316)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    import ddp_two_rank_worker as W
+    from transmil_deepgraft_amd.interface import TransMILTask
+    steps, world, k = 2, 2, 1
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(here, "ddp_two_rank_worker.py"),
+                                       str(tmp_path / f"rank{r}.pt"), str(k), str(steps), str(W.C5_TILES), "c5"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=150)[0].decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{logs[r][-3000:]}"
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
+    for r in range(world):
+        assert res[r]["parts"] == 3 and res[r]["issued"] == [0, 1, 2] * steps, res[r]["issued"]
+        # only the class token + _fc1 part is reduced after the whole backward
+        assert res[r]["exposed_bytes"] < 0.5 * 4 * sum(v.numel() for v in res[r]["params"].values())
+    for n in res[0]["params"]:
+        torch.testing.assert_close(res[0]["params"][n], res[1]["params"][n], rtol=0, atol=0, msg=n)
+
+    model = W.build_c5_model()
+    mil = model.model
+    c0 = mil._dropout_counter.clone()
+    task = TransMILTask(model)
+    opt = task.configure_optimizers()[0][0]
+    start = {n: p.detach().clone() for n, p in model.named_parameters() if p.requires_grad}
+    for s in range(steps):
+        for r in range(world):
+            mil._dropout_counter.copy_(c0 + s)          # each rank's dropout stream at this step
+            task.backward(task.training_step(W.c5_bag(r, s)) / world)
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
+    moved = 0.0
+    for n, p in model.named_parameters():
+        if not p.requires_grad:
+            continue
+        torch.testing.assert_close(res[0]["params"][n], p.detach().cpu(), rtol=1e-5, atol=1e-7, msg=n)
+        moved = max(moved, (p.detach() - start[n]).abs().max().item())
+    assert moved > 1e-5

@@ -454,6 +454,20 @@ def _mixed_path_worker(rank, world, port, out):
             ar.bucket.ready(0)           # and the hook issues part 0 before layer1's backward
         ar()
         res.append([None if p.grad is None else p.grad.clone() for p in ps])
+    # then 200 steps with the roles fixed (rank 0 fused, rank 1 never uses parameter 2): the flags
+    # are reset every step, so the fused rank's flag does not decay (1, 0.5, 0.25, ... -> 0 after
+    # ~150 steps) into "unused" on both ranks
+    for step in range(200):
+        fused = rank == 0
+        for i, p in enumerate(ps):
+            p.grad = None if (not fused and i == 2) else torch.full((5,), float(4 * rank + i))
+        if fused:
+            ar.bucket.bind()
+            ar.bucket.ready(0)
+        ar()
+    res.append([None if p.grad is None else p.grad.clone() for p in ps])
+    res.append(ar.bucket.flags.clone())
+    ar.close()
     out[rank] = res
     dist.destroy_process_group()
 
@@ -476,6 +490,14 @@ def test_grad_allreduce_ranks_on_different_paths():
             expect = torch.full((5,), sum(vals) / 2.0)
             for r in range(2):
                 torch.testing.assert_close(res[r][step][i], expect)
+    # after 200 fixed-role steps: parameter 2 is still "used" (rank 1 adopts rank 0's half)
+    for i in range(4):
+        vals = [4 * r + i for r in range(2) if not (r == 1 and i == 2)]
+        for r in range(2):
+            assert res[r][2][i] is not None, (r, i)
+            torch.testing.assert_close(res[r][2][i], torch.full((5,), sum(vals) / 2.0))
+    for r in range(2):
+        assert torch.equal(res[r][3], torch.ones(4)), res[r][3]
 
 
 @pytest.mark.gpu

@@ -136,18 +136,25 @@ def test_golden_reference_d512_round2(name, dtype):
         assert (lo.argmax(1)[clear] == ref64.argmax(1)[clear]).all()
 
 
+# (N, model seed): fp64 oracle margins |logit1 - logit0| of 0.17 (2021: class 0), 0.25-0.26 (3002: class 0),
+# 0.29-0.37 (3004: class 1) at N = 1024 / 8192 on bag_input(N, 512, 5 + N) -- each at least 3x the 5e-2
+# logit tolerance, both classes represented
 @pytest.mark.parametrize("N", [1024, 8192])
-def test_bf16_mode_close_to_oracle(N):
-    ref, ours = _pair(2, dtype=torch.bfloat16)
+@pytest.mark.parametrize("seed", [2021, 3002, 3004])
+def test_bf16_mode_close_to_oracle(N, seed):
+    """The timed path's arithmetic (bf16 mode, eval) against the fp64 oracle at C1 / C2 sizes: logits
+    within 5e-2 and the class argmax equal, asserted unconditionally on bags whose oracle margin is
+    clear (checked first: a seed whose margin shrank below 0.15 fails here, it is not skipped)."""
+    ref, ours = _pair(2, dtype=torch.bfloat16, seed=seed)
     x = torch.from_numpy(bag_input(N, 512, 5 + N))
     with torch.no_grad():
         lr = _ref64(ref, x)
         lo = ours(x.to(DEV)).cpu()
-    np.testing.assert_allclose(lo.numpy(), lr.numpy(), rtol=0, atol=5e-2)
     lr_np = lr.numpy()
     top2 = np.sort(lr_np, axis=1)[:, -2:]
-    if (top2[:, 1] - top2[:, 0]).min() > 0.05:      # clear-margin bag: the class must not flip
-        assert (lo.numpy().argmax(1) == lr_np.argmax(1)).all()
+    assert (top2[:, 1] - top2[:, 0]).min() > 0.15, lr_np       # the bag's construction, not a skip
+    np.testing.assert_allclose(lo.numpy(), lr_np, rtol=0, atol=5e-2)
+    assert (lo.numpy().argmax(1) == lr_np.argmax(1)).all()
 
 
 @pytest.mark.parametrize("N,B,ncls", [(1, 1, 2), (2, 1, 2), (3, 1, 2), (255, 1, 2), (256, 1, 3), (257, 1, 2),

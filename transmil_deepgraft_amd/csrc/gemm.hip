@@ -983,6 +983,7 @@ __global__ __launch_bounds__(512) void gemm_persist_kernel(const bf16* __restric
   }
 }
 
+#ifdef TM_DIAG
 // ---------------------------------------------------------------------------
 // Persistent ring GEMM with the epilogue straight from the accumulator registers (gemm_pr_kernel):
 // two 512-thread workgroups per CU (64 KB of LDS each: the 2-stage LDS-DMA ring and nothing else),
@@ -1179,6 +1180,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
     }
   }
 }
+#endif  // TM_DIAG (gemm_pr_kernel: measured slower on every step shape, profiles/r05d_ab_gemm_pr_rejected.txt)
 
 // ---------------------------------------------------------------------------
 // Big-tile bf16 GEMM: 256 x TBN (256 or 128) per 512-thread workgroup.  A 128 x 128 tile moves
@@ -1421,15 +1423,15 @@ inline bool use_ring160(const tm_gemm_args& g) {
   return t128 > cu && t160 <= cu;
 }
 
-// the persistent register-epilogue kernel (k-contiguous A, no split).  Diagnostic build: variant 11
-// wherever valid, 12 never.
+#ifdef TM_DIAG
+// the persistent register-epilogue kernel (k-contiguous A, no split): diagnostic build only, variant
+// 11 wherever valid (the product library never selects it: slower on every step shape)
 inline bool use_pr(const tm_gemm_args& g) {
   if (g.a_trans || g.splits != 1 || g.K % 64 != 0 || g.mode == TM_EPI_SPLITK) return false;
   if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
-  if (GEMM_VARIANT == 11) return true;
-  if (GEMM_VARIANT != 0) return false;
-  return false;   // product selection: set from the measured A/B (scripts/dev/gemm_pr_ab.py)
+  return GEMM_VARIANT == 11;
 }
+#endif
 
 template <typename OutT>
 bool big_ok(const tm_gemm_args& g) {
@@ -1477,7 +1479,6 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
       TM_PERSIST_CASE(0, 0) TM_PERSIST_CASE(0, 1) TM_PERSIST_CASE(1, 0) TM_PERSIST_CASE(1, 1)
 #undef TM_PERSIST_CASE
     }
-#endif
     if (use_pr(g)) {
       const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
       const int ntiles = tiles_m * tiles_n, cap = 2 * tm_cu_count();
@@ -1498,6 +1499,7 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
       TM_CHECK_LAUNCH();
       return 0;
     }
+#endif
     if (use_ring160(g)) {
       constexpr size_t sm = 2 * R160_STAGE;
       const dim3 g160((g.N + BN - 1) / BN, (g.M + BM160 - 1) / BM160);

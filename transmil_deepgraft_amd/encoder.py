@@ -119,7 +119,13 @@ def _conv1x1_ws_bytes():
 
 
 def _tuning_enabled():
+    """The timed algorithm search picks hipBLASLt's fastest candidate per process from wall-clock
+    timings, so two processes (or ranks) may run different algorithms and their encoder features
+    differ by rounding.  Off with TM_CONV1X1_TUNE=0 or under torch.use_deterministic_algorithms(True)
+    (then every process runs the heuristic's first choice: run-to-run and rank-to-rank identical)."""
     import os
+    if torch.are_deterministic_algorithms_enabled():
+        return False
     return os.environ.get("TM_CONV1X1_TUNE", "1") != "0"
 
 

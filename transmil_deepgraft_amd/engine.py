@@ -860,14 +860,14 @@ class TransMILEngine:
                    inner=inner, ce=ce_out)
         return logits, ctx
 
-    def backward(self, dlogits, ctx, params, out=None, ready=None, gloss=None):
+    def backward(self, dlogits, ctx, params, out=None, ready=None, gloss=None, parts=2):
         """Returns a dict name -> fp32 gradient with the reference parameter names.  The deferred
         parameter-gradient sums go into a ReduceQueue owned by this call (reentrant across
         threads / streams)."""
         with reduce_scope():
-            return self._backward(dlogits, ctx, params, out, ready, gloss)
+            return self._backward(dlogits, ctx, params, out, ready, gloss, parts)
 
-    def _backward(self, dlogits, ctx, params, out=None, ready=None, gloss=None):
+    def _backward(self, dlogits, ctx, params, out=None, ready=None, gloss=None, parts=2):
         """Body of ``backward``.
 
         ``gloss``: the gradient of the forward's fused loss (``ce``; a 0-d device tensor); then
@@ -875,8 +875,11 @@ class TransMILEngine:
 
         ``out``: name -> preallocated fp32 tensor to write each gradient into (the views of a
         ``GradBucket``); ``ready(part)``: called once the head, norm, layer2 and PPEG gradients
-        are final (part 0, before layer1's backward is enqueued) and at the end (part 1), so
-        a bucketed all-reduce of part 0 overlaps layer1 / _fc1 backward."""
+        are final (part 0, before layer1's backward is enqueued) and at the end (the last part), so
+        a bucketed all-reduce of part 0 overlaps layer1 / _fc1 backward.  ``parts = 3`` (the bucket
+        of a world > 1 run, ``TransMIL.grad_bucket_parts(split_layer1=True)``): layer1's gradients
+        are flushed and ``ready(1)`` is called as soon as layer1's backward is enqueued, so their
+        all-reduce overlaps the _fc1 backward; ``ready(2)`` (class token, _fc1) at the end."""
         geo, prm = ctx["geo"], ctx["prm"]
         dev = ctx["H0"].device
         pool = Pool(dev)
@@ -933,6 +936,9 @@ class TransMILEngine:
                 flush_reductions()     # head, norm, layer2 and PPEG parameter gradients final
                 if ready is not None:
                     ready(0)
+            elif ready is not None and parts >= 3 and self.fc1["main"] is not None:
+                flush_reductions()     # layer1's parameter gradients final: part 1 goes now
+                ready(1)
         if self.fc1["main"] is None:
             # pre-embedded input: dL/dx = the token rows + the duplicated pad rows folded back
             dHv = dH.view(B, S, D)
@@ -972,7 +978,7 @@ class TransMILEngine:
                         work_pool=pool, bias_out=g[w0n + ".bias"])
         flush_reductions()
         if ready is not None:
-            ready(1)
+            ready(parts - 1 if parts >= 3 else 1)
         return g
 
 

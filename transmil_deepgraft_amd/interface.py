@@ -399,31 +399,68 @@ class GradAllReduce:
     so no unused-parameter search runs; on the module-by-module path the rank's has-gradient flags
     travel in the bucket's own all_reduce (a tail of the last part) and parameters used on another
     rank adopt the averaged gradient.  With ``model=`` (a TransMIL with
-    ``grad_bucket_parts``) the bucket has two parts: part 0 (head, norm, layer2, PPEG; 4.4 MB
-    fp32) is final before layer1's backward is enqueued and, with ``overlap``, its RCCL
-    all_reduce is issued right then on RCCL's stream, overlapping layer1 + _fc1 backward on
-    the compute stream; part 1 (layer1, class token, _fc1; 5.2 MB) follows at the end.  Two
-    messages of ~5 MB keep each xGMI ring step large (per-link bound) while hiding part 0.
+    ``grad_bucket_parts``) the bucket is cut where the fused backward finishes gradients: part 0
+    (head, norm, layer2, PPEG; 4.4 MB fp32) is final before layer1's backward is enqueued and, with
+    ``overlap``, its RCCL all_reduce is issued right then on RCCL's stream, overlapping layer1 +
+    _fc1 backward on the compute stream.  At world > 1 (``split_layer1``) part 1 is layer1 alone
+    (4.2 MB), issued before the _fc1 backward, and part 2 (class token, _fc1 + the flags; 1.05 MB)
+    is the only message after the whole backward (``exposed_bytes``); at world 1 (no collective)
+    layer1 and _fc1 stay one part (5.2 MB), which saves the extra flush launch.  Few ~1-5 MB
+    messages keep each xGMI ring step large (per-link bound).
 
     ``sync = False`` skips the reduction (Lightning's no-sync micro-batches under
     ``accumulate_grad_batches``, code/train.py:199); ``force`` runs the collective even at
     world size 1 (tests of the RCCL path inside a captured hipGraph)."""
 
-    def __init__(self, params, group=None, model=None, overlap=True, force=False):
+    def __init__(self, params, group=None, model=None, overlap=True, force=False, split_layer1=None):
         self.params = [p for p in params if p.requires_grad]
         self.group, self.overlap, self.force = group, overlap, force
+        if split_layer1 is None:
+            # a third part only where a collective runs: at world 1 its extra flush launch buys nothing
+            split_layer1 = self._world() > 1
         parts = [self.params]
         if model is not None and hasattr(model, "grad_bucket_parts"):
-            mp = model.grad_bucket_parts()
+            try:
+                mp = model.grad_bucket_parts(split_layer1=True) if split_layer1 else model.grad_bucket_parts()
+            except TypeError:       # a model whose bucket layout has no layer1 cut
+                mp = model.grad_bucket_parts()
             if {id(p) for part in mp for p in part} == {id(p) for p in self.params}:
                 parts = mp
         self.bucket = GradBucket(parts, self.params[0].device)
         self.flat = self.bucket.flat
+        self._model = model
         if model is not None and hasattr(model, "attach_grad_bucket"):
             model.attach_grad_bucket(self.bucket)
         self.bucket.hooks.append(self._on_ready)
         self.sync = True
         self._works = {}
+        self._closed = False
+
+    def exposed_bytes(self):
+        """fp32 bytes all-reduced after the whole backward (the last part: nothing left to hide it
+        behind); the earlier parts are issued from the backward and overlap what follows them."""
+        a, b = self.bucket.ranges[-1]
+        return 4 * (b - a) if self.overlap else 4 * self.flat.numel()
+
+    def close(self):
+        """Release everything that refers to the process group's communicator, BEFORE
+        ``dist.destroy_process_group()``: waits on and drops the outstanding async works, detaches
+        the bucket hook (the model's bucket keeps a bound method of this object alive) and the model's
+        bucket.  A hipGraph captured over this all-reduce holds the communicator's kernels and
+        its registered buffers: release it first (``GraphedOptimizationStep.close()`` or
+        ``graph.reset()``).  Idempotent; a closed instance raises when called."""
+        if self._closed:
+            return
+        for w in self._works.values():
+            w.wait()
+        self._works.clear()
+        if self._on_ready in self.bucket.hooks:
+            self.bucket.hooks.remove(self._on_ready)
+        m = self._model
+        if m is not None and getattr(m, "_grad_bucket", None) is self.bucket:
+            m.attach_grad_bucket(None)
+        self._model = None
+        self._closed = True
 
     def _world(self):
         if not (dist.is_available() and dist.is_initialized()):
@@ -442,6 +479,8 @@ class GradAllReduce:
                                          async_op=True)
 
     def __call__(self):
+        if self._closed:
+            raise RuntimeError("GradAllReduce: called after close()")
         if not self._active():
             self._works.clear()
             return
@@ -474,6 +513,11 @@ class GradAllReduce:
             for p, here, anywhere in zip(self.params, local, used):
                 if anywhere and not here:
                     p.grad = self.bucket.view(p)
+        # back to "used" for the next step on EVERY rank, whichever path it took: a fused rank never
+        # writes its flags, so it would otherwise carry the average forward and, beside a module-path
+        # rank that never uses a parameter, halve it each step until it underflows to 0.  (One tiny
+        # launch per reducing step; it runs only where a collective runs.)
+        self.bucket.flags.fill_(1.0)
 
 
 class _CrossEntropyOneHot(torch.autograd.Function):
@@ -686,7 +730,24 @@ class GraphedOptimizationStep:
             if "lookahead_step" in g:
                 g["lookahead_step"] += 1
 
+    def close(self):
+        """Release the captured graphs, then the all-reduce (``GradAllReduce.close``): a graph
+        captured over the RCCL all-reduce holds the communicator's kernels and registered
+        buffers, so it must be gone -- destroyed and drained -- before
+        ``dist.destroy_process_group()``.  Later calls raise."""
+        if self.graphs:
+            torch.cuda.synchronize()            # no replay in flight
+            for g in self.graphs.values():
+                g.reset()
+            torch.cuda.synchronize()
+        self.graphs, self.loss = None, {}
+        self._closed = True
+        if self.allreduce is not None:
+            self.allreduce.close()
+
     def __call__(self, batch):
+        if getattr(self, "_closed", False):
+            raise RuntimeError("GraphedOptimizationStep: called after close()")
         bags, label = batch[0], batch[1]
         task = self.task
         if self.graphs is None:

@@ -65,7 +65,7 @@ class CTMIL(TransMIL):
         named = [(n, p) for n, p in self.named_parameters() if not n.startswith(("conv1.", "conv2.", "_fc1."))]
         return (tuple(n.replace("pos_layer_0.", "pos_layer.", 1) for n, _ in named), tuple(p for _, p in named))
 
-    def grad_bucket_parts(self):
+    def grad_bucket_parts(self, split_layer1=False):
         return [[p for _, p in self.named_parameters()]]
 
     def forward_ce(self, x, label, class_stats=None):

@@ -101,7 +101,7 @@ class _TransMILFn(torch.autograd.Function):
                 # the parameters' .grad become its views (stable addresses: hipGraph-safe, no copy)
                 views = {n: bucket.view(p) for n, p in prm.items()}
                 dx = ctx.engine.backward(dl, ctx.c, prm, out=views, ready=bucket.ready,
-                                         gloss=gloss).pop("__dx__", None)
+                                         gloss=gloss, parts=len(bucket.ranges)).pop("__dx__", None)
                 ctx.c = None
                 with torch.no_grad():
                     for n, p in prm.items():
@@ -114,8 +114,8 @@ class _TransMILFn(torch.autograd.Function):
                 # gradient accumulation (accumulate_grad_batches > 1): add into the bucket views
                 with torch.no_grad():
                     torch._foreach_add_([p.grad for p in prm.values()], [g[n] for n in ctx.names])
-                bucket.ready(0)
-                bucket.ready(1)
+                for i in range(len(bucket.ranges)):
+                    bucket.ready(i)
                 return head[:8] + (dx,) + (None,) * len(ctx.names)
         return head[:8] + (dx,) + tuple(g[n] for n in ctx.names)
 
@@ -180,13 +180,18 @@ class TransMIL(nn.Module):
                  if not (layout is FC1_EMBED and n.startswith("_fc1."))]
         return tuple(n for n, _ in named), tuple(p for _, p in named)
 
-    def grad_bucket_parts(self):
+    def grad_bucket_parts(self, split_layer1=False):
         """Parameters in the order their gradients become final in the fused backward: part 0 =
         head, norm, layer2, PPEG (ready before layer1's backward starts), part 1 = layer1,
-        class token, _fc1."""
+        class token, _fc1.  ``split_layer1`` (world > 1): part 1 = layer1 alone (ready before the
+        _fc1 backward starts, so its all-reduce overlaps it) and part 2 = class token, _fc1."""
         first = (self._head + ".", "norm.", "layer2.", "pos_layer.")
         named = list(self.named_parameters())
-        return [[p for n, p in named if n.startswith(first)], [p for n, p in named if not n.startswith(first)]]
+        p0 = [p for n, p in named if n.startswith(first)]
+        rest = [(n, p) for n, p in named if not n.startswith(first)]
+        if not split_layer1:
+            return [p0, [p for _, p in rest]]
+        return [p0, [p for n, p in rest if n.startswith("layer1.")], [p for n, p in rest if not n.startswith("layer1.")]]
 
     def attach_grad_bucket(self, bucket):
         """Route the fused backward's parameter gradients into ``bucket`` (interface.GradBucket).
