@@ -221,7 +221,7 @@ def test_two_ranks_average_through_the_hip_engine(k, npatch, tmp_path):
     assert moved > 1e-5      # the steps changed the parameters (the comparison is not vacuous)
 
 
-def test_two_ranks_average_the_c5_image_path(tmp_path):
+def test_two_ranks_average_the_c5_image_path(tmp_path, monkeypatch):
     """BASELINE config C5's image path under DDP: two processes on the one GPU (gloo), each
     running ImageBagModel (frozen RetCCL ResNet-50, bf16, eval-mode BN -> TransMIL(2, 2048) RCC-2048
     branch, bf16, train mode) on its own 8-tile bags through TransMILTask.optimization_step with
@@ -237,6 +237,9 @@ def test_two_ranks_average_the_c5_image_path(tmp_path):
     import ddp_two_rank_worker as W
     from transmil_deepgraft_amd.interface import TransMILTask
     steps, world, k = 2, 2, 1
+    # the encoder's 1x1 convolutions on hipBLASLt's heuristic choice in every process: a per-process
+    # timed algorithm search (tm_conv1x1_tune) could round the features differently per process
+    monkeypatch.setenv("TM_CONV1X1_TUNE", "0")
     port = _free_port()
     procs = []
     for r in range(world):
@@ -258,8 +261,10 @@ def test_two_ranks_average_the_c5_image_path(tmp_path):
     res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     for r in range(world):
         assert res[r]["parts"] == 3 and res[r]["issued"] == [0, 1, 2] * steps, res[r]["issued"]
-        # only the class token + _fc1 part is reduced after the whole backward
-        assert res[r]["exposed_bytes"] < 0.5 * 4 * sum(v.numel() for v in res[r]["params"].values())
+        # only the class token + _fc1 part (+ the has-gradient flags, 64-B alignment) is reduced after
+        # the whole backward; layer1's part went out before the _fc1 backward
+        tail = 4 * sum(v.numel() for n, v in res[r]["params"].items() if n.startswith(("model._fc1.", "model.cls_token")))
+        assert tail <= res[r]["exposed_bytes"] < tail + 4096, (res[r]["exposed_bytes"], tail)
     for n in res[0]["params"]:
         torch.testing.assert_close(res[0]["params"][n], res[1]["params"][n], rtol=0, atol=0, msg=n)
 
@@ -280,6 +285,11 @@ def test_two_ranks_average_the_c5_image_path(tmp_path):
     for n, p in model.named_parameters():
         if not p.requires_grad:
             continue
-        torch.testing.assert_close(res[0]["params"][n], p.detach().cpu(), rtol=1e-5, atol=1e-7, msg=n)
+        got, want = res[0]["params"][n], p.detach().cpu()
+        # (the loss / world scale enters before the bf16 products here, after them on the ranks:
+        # a few weights of |w| ~ 1e-3 differ by ~1e-7)
+        torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6,
+                                   msg=lambda m, n=n, got=got, want=want: f"{n}: max |diff| "
+                                   f"{(got - want).abs().max().item():.3e}\n{m}")
         moved = max(moved, (p.detach() - start[n]).abs().max().item())
     assert moved > 1e-5

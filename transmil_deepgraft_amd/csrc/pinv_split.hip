@@ -230,23 +230,33 @@ TM_DEV void load_split8(const bf16* hi, long long plane, size_t off, float* v) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)l[e];
 }
-TM_DEV void store_split8(bf16* hi, long long plane, size_t off, const float* v) {
+// 16-B store; wt: write-through (buffer_store sc1: the line goes out now and leaves this XCD's L2,
+// so the launch-end L2 write-back has nothing of it to write)
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+TM_DEV void st16(void* base, size_t off_bytes, f32x4 v, bool wt) {
+  if (wt)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), tm_rsrc(base, 0x7FFFFFF0u),
+                                           (unsigned)off_bytes, 0, 16);
+  else
+    *(f32x4*)((char*)base + off_bytes) = v;
+}
+TM_DEV void store_split8(bf16* hi, long long plane, size_t off, const float* v, bool wt = false) {
   bf16x8 h, l;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     h[e] = (bf16)v[e];
     l[e] = (bf16)(v[e] - (float)h[e]);
   }
-  *(bf16x8*)(hi + off) = h;
-  *(bf16x8*)(hi + plane + off) = l;
+  st16(hi, off * 2, __builtin_bit_cast(f32x4, h), wt);
+  st16(hi, (plane + off) * 2, __builtin_bit_cast(f32x4, l), wt);
 }
 TM_DEV void load_f8(const float* p, size_t off, float* v) {
   const f32x4 a = *(const f32x4*)(p + off), b = *(const f32x4*)(p + off + 4);
   v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3]; v[4] = b[0]; v[5] = b[1]; v[6] = b[2]; v[7] = b[3];
 }
-TM_DEV void store_f8(float* p, size_t off, const float* v) {
-  *(f32x4*)(p + off) = (f32x4){v[0], v[1], v[2], v[3]};
-  *(f32x4*)(p + off + 4) = (f32x4){v[4], v[5], v[6], v[7]};
+TM_DEV void store_f8(float* p, size_t off, const float* v, bool wt = false) {
+  st16(p, off * 4, (f32x4){v[0], v[1], v[2], v[3]}, wt);
+  st16(p, (off + 4) * 4, (f32x4){v[4], v[5], v[6], v[7]}, wt);
 }
 
 // |X| row sums (which = 0) or column sums (which = 1) of one head, and their maximum
@@ -448,22 +458,26 @@ TM_DEV void stage_tile(const SJob& J, int nbh, long long plane, const float* max
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = s[e] + e1s * e1v[e] + e2s * e2v[e];
     if (dg) v[row - col] += diag;
-    if (J.c_f32) store_f8((float*)J.c, eoff, v); else store_split8((bf16*)J.c, plane, eoff, v);
-    if (!dotj && J.cf) store_f8(J.cf, eoff, v);
+    // write-through outputs: the launch-end L2 write-back would otherwise hold the next level's start
+    // (forward chain 91.4 -> 85.5 us, backward 170.8 -> 169.1 us in graph replay; diagnostic variant 6
+    // = plain stores for the A/B, scripts/dev/pinv_graph_stamps.py --ab 0,6)
+    const bool wt = SPLIT_DBG != 6;
+    if (J.c_f32) store_f8((float*)J.c, eoff, v, wt); else store_split8((bf16*)J.c, plane, eoff, v, wt);
+    if (!dotj && J.cf) store_f8(J.cf, eoff, v, wt);
     if (J.c2) {
       float w[8];
       const float c2a = J.c2_alpha, c2e = J.c2_e1;
 #pragma unroll
       for (int e = 0; e < 8; ++e) w[e] = c2a * s[e] + c2e * e1v[e];
       if (dg) w[row - col] += J.c2_diag;
-      store_split8(J.c2, plane, eoff, w);
+      store_split8(J.c2, plane, eoff, w, wt);
     }
     if (J.c3) {
       float w[8];
       const float c3e = J.c3_e1;
 #pragma unroll
       for (int e = 0; e < 8; ++e) w[e] = c3e * e1v[e];
-      store_split8(J.c3, plane, eoff, w);
+      store_split8(J.c3, plane, eoff, w, wt);
     }
     if (dotj) {
       float d = 0.f;
