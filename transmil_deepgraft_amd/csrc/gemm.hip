@@ -1433,9 +1433,15 @@ inline bool use_pr(const tm_gemm_args& g) {
 }
 #endif
 
+// the big-tile kernel's valid shapes; selected for every valid GEMM by diagnostic variant 7, and in the
+// product for the to_qkv projection (head-major scatter epilogue, N >= 1024, no split): 198 tiles of
+// 256 x 256 at n' = 8448 fill the chip in one round where the 128 x 128 ring needed 1.55 rounds of
+// 792 tiles (microbench 23.2 vs 27.6 us; scripts/microbench.py --gemm-ab)
 template <typename OutT>
 bool big_ok(const tm_gemm_args& g) {
-  if (GEMM_VARIANT != 7) return false;
+  const bool qkv_pick = GEMM_VARIANT == 0 && g.mode == TM_EPI_QKV && g.N >= 1024 && g.splits == 1 && g.M >= 2048 &&
+                        !g.a_trans && !g.b_kn;
+  if (GEMM_VARIANT != 7 && !qkv_pick) return false;
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if (g.a_trans && (g.M % 8 != 0 || g.M < 8)) return false;
   if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
@@ -1446,7 +1452,6 @@ template <typename T, typename OutT>
 int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.splits);
   if constexpr (sizeof(T) == 2) {
-#ifdef TM_DIAG
     if (big_ok<OutT>(g)) {
 #define TM_BIG_CASE(AT, BKN, TBN)                                                                  \
       if (g.a_trans == AT && g.b_kn == BKN) {                                                      \
@@ -1464,6 +1469,7 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
       }
 #undef TM_BIG_CASE
     }
+#ifdef TM_DIAG
     if (ring_ok<OutT>(g) && GEMM_VARIANT == 4) {
       const int tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
       const int ntiles = tiles_m * tiles_n * g.splits;
