@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--n", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--cpu-tiles", type=int, default=8, help="tiles of the CPU encoder sample (0: no cpu_baseline)")
+    ap.add_argument("--cpu-tiles", type=int, default=64, help="tiles of the CPU encoder sample (0: no cpu_baseline)")
     ap.add_argument("--encoder-mode", default="train", choices=["train", "eval"])
     # tiles per encoder piece: 1024 measured faster than 512 (eval 84.5 vs 89.0 ms per 4096 tiles;
     # smaller pieces slower: profiles/r04u_c5_chunks.txt); every piece tensor stays < 2 GiB (bf16: the

@@ -42,6 +42,9 @@ for w in (0, 4):
     st = a[:, w, :7]
     d = np.diff(st, axis=1)
     print(f"wave {w}: mean cycles per phase", [int(x) for x in d.mean(0)], " max", [int(x) for x in d.max(0)])
+    if os.environ.get("A3_SIM2", "0") == "1":
+        print(f"   A2 tail: key loop done -> k~ staged {int((a[:, w, 7] - a[:, w, 5]).mean())}, k~ staged -> end "
+              f"{int((a[:, w, 6] - a[:, w, 7]).mean())} cycles (means)")
     print(f"   total mean {int((st[:, 6] - st[:, 0]).mean())} cycles; start spread {int(st[:, 0].max() - st[:, 0].min())}"
           f"; end spread {int(st[:, 6].max() - st[:, 6].min())}; first start to last end {int(st[:, 6].max() - st[:, 0].min())}")
 _lib.lib().tm_debug_set_variant(1, 0)

@@ -707,3 +707,61 @@ def test_cls_q_rows_against_torch(B, n, nslabs):
         ex[b, NL] = xn[b, r].double().cpu()
     assert _rel(Aq.cpu(), ea) < 1e-6 and _rel(Xs.cpu(), ex) < 1e-6
     assert (Aq[:, NL + 1:] == 0).all() and (Xs[:, NL + 1:] == 0).all()
+
+
+@pytest.mark.parametrize("nbags,n", [(1, 1024), (2, 512)])
+def test_a1_bwd_dqkv_bf16_path_equals_the_fp32_dq_path(nbags, n):
+    """The bf16 layer-1 path (tm_nys_a1_bwd_dqkv: bf16(scale dq) straight into dqkv, then
+    tm_nys_assemble_q_slab_inplace adds the landmark term and rounds again) against the fp32 dq path
+    (tm_nys_a1_bwd + tm_nys_assemble_q_slab, one rounding): dk~ and dY bitwise equal, the q columns
+    within one bf16 ulp of the single-rounding result (the extra rounding), the k / v columns of dqkv
+    untouched (the double rounding had only end-to-end gradient tolerances)."""
+    L = _lib()
+    from transmil_deepgraft_amd._lib import BF16
+    from transmil_deepgraft_amd.engine import _p, _stream
+    nh, nbh, scale, slabs = 8, 8 * nbags, 0.125, 3
+    g = torch.Generator(device="cpu").manual_seed(11 + n)
+    q = (torch.randn(nbh, n, 64, generator=g) * 0.3).to(torch.bfloat16)
+    kl = (torch.randn(nbh, 256, 64, generator=g) * 0.3).to(torch.bfloat16)
+    y = torch.randn(nbh, 256, 64, generator=g).to(torch.bfloat16)
+    dm = (torch.randn(nbags, n, nh * 64, generator=g) * 0.1).to(torch.bfloat16)
+    lse = torch.logsumexp(q.float() @ kl.float().transpose(1, 2), -1)          # a consistent softmax
+    d1 = torch.randn(nbh, n, generator=g) * 0.05
+    dql = torch.randn(nbh, 256, 64, generator=g) * 0.1
+    slab = torch.randn(slabs, nbh, 256, 64, generator=g) * 0.1
+    qd, kd, yd, dmd, lsed, d1d, dqld, slabd = (t.to(DEV).contiguous() for t in (q, kl, y, dm, lse, d1, dql, slab))
+    ws = L.query("tm_nys_a1_bwd_workspace", nbh, n, 256) // 4
+    sentinel = 7.0
+    out = {}
+    for path in ("dqkv", "fp32"):
+        dqkv = torch.full((nbags, n, 3 * nh * 64), sentinel, dtype=torch.bfloat16, device=DEV)
+        work = torch.empty(ws, device=DEV)
+        dkl = torch.empty(nbh, 256, 64, device=DEV)
+        dy = torch.empty(nbh, 256, 64, device=DEV)
+        if path == "dqkv":
+            L.call("tm_nys_a1_bwd_dqkv", _p(qd), _p(dmd), _p(kd), _p(yd), _p(lsed), _p(d1d), nbh, nh, n, _p(dqkv),
+                   C.c_float(scale), _p(work), _p(dkl), _p(dy), None, _stream())
+            L.call("tm_nys_assemble_q_slab_inplace", _p(dqld), _p(slabd), slabs, nbags, nh, n, C.c_float(scale),
+                   _p(dqkv), _stream())
+        else:
+            dq = torch.empty(nbh, n, 64, device=DEV)
+            L.call("tm_nys_a1_bwd", BF16, _p(qd), _p(dmd), _p(kd), _p(yd), _p(lsed), _p(d1d), nbh, nh, n, 256,
+                   _p(dq), _p(work), _p(dkl), _p(dy), 0, None, _stream())
+            L.call("tm_nys_assemble_q_slab", BF16, _p(dq), -1, _p(dqld), _p(slabd), slabs, nbags, nh, n,
+                   C.c_float(scale), _p(dqkv), _stream())
+            # scale * dq in dqkv's q-column layout: the value the bf16 path rounds first
+            sdq = (scale * dq).view(nbags, nh, n, 64).permute(0, 2, 1, 3).reshape(nbags, n, nh * 64).cpu()
+        torch.cuda.synchronize()
+        out[path] = (dqkv.cpu().float(), dkl.cpu(), dy.cpu())
+    a, b = out["dqkv"], out["fp32"]
+    assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
+    qa, qb = a[0][..., :nh * 64], b[0][..., :nh * 64]
+    assert torch.isfinite(qb).all() and qb.abs().max() > 0
+    # the bf16 path rounds scale*dq to bf16 (half an ulp of that term) before the landmark term is
+    # added and the sum rounded (half an ulp of the result, as the fp32 path's single rounding):
+    # |a - b| <= ulp(scale dq) / 2 + ulp(b), ulp(x) = 2^(floor(log2 |x|) - 7)
+    def ulp(x):
+        return torch.exp2(torch.floor(torch.log2(x.abs().clamp_min(1e-30))) - 7)
+    bound = 0.5 * ulp(sdq) + ulp(qb)
+    assert ((qa - qb).abs() <= bound * 1.0001 + 1e-30).all(), ((qa - qb).abs() - bound).max()
+    assert (a[0][..., nh * 64:] == sentinel).all()

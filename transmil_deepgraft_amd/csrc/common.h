@@ -125,6 +125,34 @@ TM_DEV float wave_sum(float v) {
   return v;
 }
 
+// Whole-wave max / sum on DPP lane moves (no LDS round trip per step, as __shfl_xor's ds_bpermute
+// takes): quads, half rows, rows of 16, then the row broadcasts 15 / 31 fold the four rows into lane
+// 63, read back as a wave-uniform value.  A fixed combination order (deterministic sums).
+template <int CTRL, int ROW_MASK = 0xf>
+TM_DEV float dpp_mov(float old, float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, v),
+                                                               CTRL, ROW_MASK, 0xf, false));
+}
+TM_DEV float wave_max_dpp(float v) {
+  const float ninf = -INFINITY;
+  v = fmaxf(v, dpp_mov<0xB1>(ninf, v));         // quad_perm [1, 0, 3, 2]
+  v = fmaxf(v, dpp_mov<0x4E>(ninf, v));         // quad_perm [2, 3, 0, 1]
+  v = fmaxf(v, dpp_mov<0x141>(ninf, v));        // row_half_mirror
+  v = fmaxf(v, dpp_mov<0x140>(ninf, v));        // row_mirror: every lane holds its row's max
+  v = fmaxf(v, dpp_mov<0x142, 0xa>(ninf, v));   // row_bcast:15 into rows 1, 3
+  v = fmaxf(v, dpp_mov<0x143, 0xc>(ninf, v));   // row_bcast:31 into rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+TM_DEV float wave_sum_dpp(float v) {
+  v += dpp_mov<0xB1>(0.f, v);
+  v += dpp_mov<0x4E>(0.f, v);
+  v += dpp_mov<0x141>(0.f, v);
+  v += dpp_mov<0x140>(0.f, v);
+  v += dpp_mov<0x142, 0xa>(0.f, v);
+  v += dpp_mov<0x143, 0xc>(0.f, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 TM_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 TM_DEV float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));

@@ -111,62 +111,75 @@ __global__ __launch_bounds__(256) void landmarks_kernel(const T* __restrict__ q,
 // the q~ rows are LDS broadcasts.
 // a2s (optional): the same values as bf16 hi / lo planes (hi = bf16(a), lo = bf16(a - hi); lo plane at
 // a2s + nbh * 256 * 256), the operand format of the split pseudo-inverse chain (pinv_split.hip).
-constexpr int S2_ROWS = 8, S2_KT = NL + 1;   // k~^T rows of 257: the transposing writes spread over the banks
+constexpr int S2_ROWS = 8;
 
-// A2 rows o0 / NL .. + ROWS - 1 by one 256-thread group (thread j = column j), shared by
-// sim2_softmax_kernel and the fused A3 forward (a3_fwd_v2_kernel<.., S2R>): kt = k~^T [64][S2_KT]
-// and qs = the group's q~ rows [ROWS][64] in LDS, red = [4][ROWS] LDS scratch.  Every thread of the
-// workgroup calls it (its barriers are workgroup-wide); the arithmetic of a row does not depend on
-// ROWS, so both callers write the same bits.
-template <int ROWS>
-TM_DEV void sim2_rows(const float* kt, const float* qs, float* red, int j, float* __restrict__ a2,
-                      bf16* __restrict__ a2s, size_t o0, size_t plane) {
-  const int lane = j & 63, wave = j >> 6;
-  float s[ROWS];
+// A2 rows by ONE wave each (shared by sim2_softmax_kernel and the fused A3 forward, so both write
+// the same bits): the wave computes RW rows -- q~ rows qrow0, qrow0 + qstep, .. of `qs` ([rows][64]
+// fp32 in LDS) against the head's k~ in LDS as a row image [256][64] fp32 whose row j keeps its 16-B
+// chunk c at slot c ^ (j & 15) (kimg: filled by LDS-DMA, k2_stage_dma) -- lane l owning columns l,
+// l + 64, l + 128, l + 192 and reading each 4-d chunk of a row as one conflict-free 16-B read.  The
+// logits keep the sequential fmaf order over d; the row max and sum are in-wave reductions (no LDS
+// partials, no barrier: the 256-thread-per-row form spent ~9.7k of the A3 forward's cycles in its
+// three barriers and cross-wave exchanges).  Output row k at o0 + k ostep.
+constexpr int S2_KIMG = NL * DH;   // floats of the k~ row image
+
+// k~ of head bh (kl [nbh][256][64] fp32) into the swizzled row image kimg by LDS-DMA: 64 pieces of
+// 1 KB (4 rows), `nwaves` waves; lane L of a piece writes row 4 piece + L / 16, slot L % 16, i.e.
+// fetches the row's chunk (L % 16) ^ (row & 15).  Completion: the issuing waves' vmcnt + a barrier.
+TM_DEV void k2_stage_dma(float* kimg, const float* __restrict__ kl, int bh, int wave, int nwaves, int lane) {
+  typedef __attribute__((address_space(3))) void lds_t;
+  typedef __attribute__((address_space(1))) void glb_t;
+  const float* kb = kl + (size_t)bh * NL * DH;
+  for (int piece = wave; piece < 64; piece += nwaves) {
+    const int row = piece * 4 + (lane >> 4), slot = lane & 15;
+    __builtin_amdgcn_global_load_lds((glb_t*)(kb + (size_t)row * DH + (slot ^ (row & 15)) * 4),
+                                     (lds_t*)(kimg + piece * 256), 16, 0, 0);
+  }
+}
+
+template <int RW>
+TM_DEV void sim2_wave_rows(const float* kimg, const float* qs, int qrow0, int qstep, int lane, float* __restrict__ a2,
+                           bf16* __restrict__ a2s, size_t o0, size_t ostep, size_t plane) {
+  float s[RW][4];
 #pragma unroll
-  for (int r = 0; r < ROWS; ++r) s[r] = 0.f;
-#pragma unroll 2
-  for (int c = 0; c < DH; c += 4) {   // the q~ values as 16-B broadcasts; FMA order over c unchanged
-    const float kv0 = kt[c * S2_KT + j], kv1 = kt[(c + 1) * S2_KT + j];
-    const float kv2 = kt[(c + 2) * S2_KT + j], kv3 = kt[(c + 3) * S2_KT + j];
+  for (int k = 0; k < RW; ++k)
 #pragma unroll
-    for (int r = 0; r < ROWS; ++r) {
-      const f32x4 q4 = *(const f32x4*)(qs + r * DH + c);
-      s[r] = fmaf(q4[0], kv0, s[r]);
-      s[r] = fmaf(q4[1], kv1, s[r]);
-      s[r] = fmaf(q4[2], kv2, s[r]);
-      s[r] = fmaf(q4[3], kv3, s[r]);
+    for (int i = 0; i < 4; ++i) s[k][i] = 0.f;
+  const int sw = lane & 15;   // (lane + 64 i) & 15
+#pragma unroll 4
+  for (int c = 0; c < DH; c += 4) {
+    float kv[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 t = *(const f32x4*)(kimg + (lane + 64 * i) * DH + (((c >> 2) ^ sw) << 2));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) kv[i][e] = t[e];
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const f32x4 q4 = *(const f32x4*)(qs + (qrow0 + k * qstep) * DH + c);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[k][i] = fmaf(q4[e], kv[i][e], s[k][i]);
     }
   }
-  // row max
 #pragma unroll
-  for (int r = 0; r < ROWS; ++r) {
-    const float m = wave_max(s[r]);
-    if (lane == 0) red[wave * ROWS + r] = m;
-  }
-  __syncthreads();
-  float mx[ROWS];
+  for (int k = 0; k < RW; ++k) {
+    const float m = wave_max_dpp(fmaxf(fmaxf(s[k][0], s[k][1]), fmaxf(s[k][2], s[k][3])));
 #pragma unroll
-  for (int r = 0; r < ROWS; ++r)
-    mx[r] = fmaxf(fmaxf(red[0 * ROWS + r], red[1 * ROWS + r]), fmaxf(red[2 * ROWS + r], red[3 * ROWS + r]));
-  __syncthreads();
+    for (int i = 0; i < 4; ++i) s[k][i] = __expf(s[k][i] - m);
+    const float tot = wave_sum_dpp((s[k][0] + s[k][1]) + (s[k][2] + s[k][3]));
 #pragma unroll
-  for (int r = 0; r < ROWS; ++r) {
-    s[r] = __expf(s[r] - mx[r]);
-    const float t = wave_sum(s[r]);
-    if (lane == 0) red[wave * ROWS + r] = t;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < ROWS; ++r) {
-    const float tot = (red[0 * ROWS + r] + red[1 * ROWS + r]) + (red[2 * ROWS + r] + red[3 * ROWS + r]);
-    const size_t o = o0 + (size_t)r * NL + j;
-    const float v = s[r] / tot;
-    a2[o] = v;
-    if (a2s) {
-      const bf16 hi = (bf16)v;
-      a2s[o] = hi;
-      a2s[o + plane] = (bf16)(v - (float)hi);
+    for (int i = 0; i < 4; ++i) {
+      const size_t o = o0 + (size_t)k * ostep + lane + 64 * i;
+      const float v = s[k][i] / tot;
+      a2[o] = v;
+      if (a2s) {
+        const bf16 hi = (bf16)v;
+        a2s[o] = hi;
+        a2s[o + plane] = (bf16)(v - (float)hi);
+      }
     }
   }
 }
@@ -174,31 +187,27 @@ TM_DEV void sim2_rows(const float* kt, const float* qs, float* red, int j, float
 __global__ __launch_bounds__(256) void sim2_softmax_kernel(const float* __restrict__ ql, const float* __restrict__ kl,
                                                            float* __restrict__ a2, bf16* __restrict__ a2s) {
   const int bh = blockIdx.x, i0 = blockIdx.y * S2_ROWS, j = threadIdx.x;
-  __shared__ float kt[DH * S2_KT];   // k~^T
-  __shared__ __attribute__((aligned(16))) float qs[S2_ROWS * DH];
-  __shared__ float red[4 * S2_ROWS];
+  // one LDS array (the k~ row image, then the q~ rows): a second __shared__ object beside an LDS-DMA
+  // target can make hipcc drain the DMA early (cdna_hip_programming.md section 5, trap 4(a))
+  __shared__ __attribute__((aligned(16))) float lds[S2_KIMG + S2_ROWS * DH];
+  float* kimg = lds;
+  float* qs = lds + S2_KIMG;
+  const int w = j >> 6;
+  k2_stage_dma(kimg, kl, bh, w, 4, j & 63);
   {
-    // the q~ rows go out with the k~ loads (one memory round trip before the LDS writes)
     static_assert(S2_ROWS * DH % 256 == 0, "sim2: q~ rows per thread");
     constexpr int QE = S2_ROWS * DH / 256;
     float qv[QE];
 #pragma unroll
     for (int u = 0; u < QE; ++u) qv[u] = ql[((size_t)bh * NL + i0) * DH + u * 256 + j];
-    const float* kb = kl + (size_t)bh * NL * DH;
-    f32x4 v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = *(const f32x4*)(kb + (size_t)(u * 256 + j) * 4);  // piece p: row p/16, d 4 (p%16)
 #pragma unroll
     for (int u = 0; u < QE; ++u) qs[u * 256 + j] = qv[u];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int p = u * 256 + j, row = p >> 4, d0 = (p & 15) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) kt[(d0 + e) * S2_KT + row] = v[u][e];
-    }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's k~ pieces landed
   __syncthreads();
-  sim2_rows<S2_ROWS>(kt, qs, red, j, a2, a2s, ((size_t)bh * NL + i0) * NL, (size_t)gridDim.x * NL * NL);
+  // wave w: rows i0 + w and i0 + w + 4
+  sim2_wave_rows<S2_ROWS / 4>(kimg, qs, w, 4, j & 63, a2, a2s, ((size_t)bh * NL + i0 + w) * NL, (size_t)4 * NL,
+                              (size_t)gridDim.x * NL * NL);
 }
 
 // bench-mode A2 = softmax_j(ql_i . kl_j) on the MFMA: the logits as bf16x3 products (x = hi + lo,
@@ -969,7 +978,7 @@ constexpr int A3V_PIECES = (A3V_KEYS * 8 + 511) / 512;             // 16-B piece
 inline int a3v_splits(int nbh, int n) { return std::max(1, std::min(n / 32, tm_cu_count() / std::max(nbh, 1))); }
 
 // S2R > 0: the workgroup also writes A2 = softmax(q~ k~^T) rows p * 2 S2R .. + 2 S2R - 1 of its head
-// (sim2_rows, two 256-thread groups of S2R rows; host-checked 2 S2R P == 256) before its first key
+// (sim2_wave_rows, rows dealt over the 8 waves; host-checked 2 S2R P == 256) before its first key
 // chunk is staged: the k~ / q~ loads go out ahead of the chunk's, so the rows are computed while the
 // chunk is in flight, and the separate sim2 launch disappears from the step.
 struct Sim2Out { const float* kl; float* a2; bf16* a2s; };
@@ -1014,40 +1023,23 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
       }
     }
   };
-  // fused A2 rows: k~ of the head (16-B pieces, p = u 512 + tid: row p / 16, d 4 (p % 16)) and the
-  // group's q~ rows requested first
+  // fused A2 rows (S2R > 0): computed AFTER the key loop, from k~ loaded into registers during the
+  // first key chunk (so its L2 round trip hides under the chunk's MFMAs) and written into the LDS the
+  // chunk buffers leave free; the A2 rows then cost only the tail's LDS staging and arithmetic (the
+  // prologue form made the first key chunk wait for them: +5 us per call)
   constexpr int S2Q = S2R > 0 ? S2R * DH / 256 : 1;
-  f32x4 k2[S2R > 0 ? 8 : 1];
   float q2[S2Q];
+  f32x4 k2[S2R > 0 ? 8 : 1];
   const int g2 = tid >> 8, j2 = tid & 255, r2 = p * 2 * S2R + g2 * S2R;
+  fetch(sb0);
   if constexpr (S2R > 0) {
-    const float* kb = s2.kl + (size_t)bh * NL * DH;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) k2[u] = *(const f32x4*)(kb + (size_t)(u * 512 + tid) * 4);
 #pragma unroll
     for (int u = 0; u < S2Q; ++u) q2[u] = ql[((size_t)bh * NL + r2) * DH + u * 256 + j2];
   }
-  fetch(sb0);
   bf16x8 qf[4];
 #pragma unroll
   for (int st = 0; st < 4; ++st) qf[st] = cvt8<bf16>(ql + ((size_t)bh * NL + qi) * DH + st * 16 + 8 * h);
   stamp(1);
-  if constexpr (S2R > 0) {
-    float* kt = (float*)smem;                          // k~^T [64][S2_KT]; the chunk buffers come after
-    float* qs = kt + DH * S2_KT + g2 * S2R * DH;
-    float* red = kt + DH * S2_KT + 2 * S2R * DH + g2 * 4 * S2R;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int pc = u * 512 + tid, row = pc >> 4, d0 = (pc & 15) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) kt[(d0 + e) * S2_KT + row] = k2[u][e];
-    }
-#pragma unroll
-    for (int u = 0; u < S2Q; ++u) qs[u * 256 + j2] = q2[u];
-    __syncthreads();
-    sim2_rows<S2R>(kt, qs, red, j2, s2.a2, s2.a2s, ((size_t)bh * NL + r2) * NL, (size_t)nbh * NL * NL);
-    __syncthreads();   // the LDS goes to the key chunks
-  }
   stage(sb0, 0);
   __syncthreads();
   stamp(2);
@@ -1060,6 +1052,13 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
     const int ng = min(A3V_G, sb1 - c0);
     const bool more = c0 + A3V_G < sb1;
     if (more) fetch(c0 + A3V_G);   // in flight through this chunk's scores
+    if constexpr (S2R > 0) {
+      if (c0 == sb0) {   // k~ of the head for the A2 rows of the tail (16-B pieces: row p / 16, d 4 (p % 16))
+        const float* kb = s2.kl + (size_t)bh * NL * DH;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) k2[u] = *(const f32x4*)(kb + (size_t)(u * 512 + tid) * 4);
+      }
+    }
     const bf16* ks = (const bf16*)(smem + buf * A3V_BUF);
     const bf16* vs = (const bf16*)(smem + buf * A3V_BUF + A3V_KS);
     f32x16 s[A3V_G];   // S^T tiles (rows = keys, col = this lane's query)
@@ -1111,6 +1110,26 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
     if (c0 == sb0) stamp(4);
   }
   stamp(5);
+  if constexpr (S2R > 0) {
+    // (before the partial stores: a barrier behind them would wait for their write-back)
+    __syncthreads();   // every wave is done with the chunk buffers
+    float* kimg = (float*)smem;                        // k~ row image [256][64]: row j's chunk c at slot c ^ (j & 15)
+    float* qs = kimg + S2_KIMG + g2 * S2R * DH;        // [2 S2R rows][64]: group g2's rows at g2 S2R
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int pc = u * 512 + tid, row = pc >> 4, c = pc & 15;
+      *(f32x4*)(kimg + row * DH + ((c ^ (row & 15)) << 2)) = k2[u];
+    }
+#pragma unroll
+    for (int u = 0; u < S2Q; ++u) qs[u * 256 + j2] = q2[u];
+    __syncthreads();
+    stamp(7);          // (diagnostic: k~ staged)
+    // wave w: A2 rows p 2 S2R + w + 8 k, k < 2 S2R / 8 (the 8 waves split the 2 S2R rows evenly)
+    constexpr int RW = S2R > 0 ? 2 * S2R / 8 : 1;
+    static_assert(S2R == 0 || (2 * S2R) % 8 == 0, "fused A2 rows: a multiple of 8 rows per workgroup");
+    sim2_wave_rows<RW>(kimg, kimg + S2_KIMG, wave, 8, lane, s2.a2, s2.a2s,
+                       ((size_t)bh * NL + (size_t)p * 2 * S2R + wave) * NL, (size_t)8 * NL, (size_t)nbh * NL * NL);
+  }
   const size_t pidx = ((size_t)p * nbh + bh) * NL + qi;
   if (h == 0) { part_m[pidx] = m_run; part_l[pidx] = l_run; }
   float* po = part_o + pidx * DH;
