@@ -150,7 +150,7 @@ def _qkv_k(layer):
 GEMM_SITES = {
     "fc1_gemm": ((0,), lambda n, N, L: (N, _D, 512, N * 512 * _T + _D * 512 * _T + _D * 4 + (_S(N) - 1) * _D * 4
                                         + N * _D * _T),
-                 "_fc1 Linear + GELU (+ grid-pad rows): x, W in; H0 (fp32), pre-activation out"),
+                 "_fc1 Linear + GELU (+ grid-pad rows): x, W in; H0 (fp32), pre-activation (T) out"),
     "qkv_gemm": ((1, 2), lambda n, N, L: (n, 3 * _D, _D, n * _D * _T + 3 * _D * _D * _T + 3 * n * _D * _T),
                  "to_qkv (+ head-major scatter, q scale): xn, W in; q, k, v out"),
     "out_gemm": ((1,), lambda n, N, L: (n, _D, _D, n * _D * _T + _D * _D * _T + 2 * _S(N) * _D * 4),

@@ -72,6 +72,9 @@ typedef struct tm_gemm_args {
    * only, else NULL: colsum[z][m] = sum over split z's k of A[k][m] (the bias gradient of the same
    * dY, summed by the workgroups of the first column tile while they stage A) -- [splits][M] fp32 */
   float* colsum;
+  /* 1: the pre-activation store (pre) is bf16 whatever c_dtype (the bf16 step's _fc1: the GELU
+   * backward reads it back in bf16, tm_fc1_gelu_bwd with TM_BF16); 0: c_dtype */
+  int pre_bf16;
 } tm_gemm_args;
 
 int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* args, void* stream);
@@ -321,7 +324,9 @@ int tm_dropout_bwd_pad(int dtype, const float* dH, int B, int S, int n_pad, int 
                        uint64_t seed, const uint64_t* seed_ptr, void* out, void* stream);
 /* NystromAttention eq. 1 for a raw input: [B*S, D] fp32 -> front-padded [B, n_pad, D] T */
 int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, int pad, int D, void* y, void* stream);
-int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
+/* _fc1 GELU backward + grid-pad fold: dpre (dtype T) = (dH[token] + dH[dup]) * GELU'(pre); `pre` is the
+ * forward's pre-activation in the same T (fp32 for TM_F32, bf16 for TM_BF16: tm_gemm_args.pre_bf16) */
+int tm_fc1_gelu_bwd(int dtype, const float* dH, const void* pre, int B, int N, int S, int add, int D,
                     void* dpre, float* dcls, void* stream);
 /* dpre = dy * GELU'(pre) elementwise (fp32 dy / pre, dpre in dtype): the backward of the inner
  * Linear + GELU of the in_features = 2048 _fc1 branch (code/models/TransMIL.py:100-111) */

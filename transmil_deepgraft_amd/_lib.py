@@ -30,7 +30,7 @@ class GemmArgs(C.Structure):
                 ("drop_p", Fl), ("drop_scale", Fl), ("seed", U64), ("resid", P),
                 ("accumulate", I), ("grp_in", I), ("skip", I), ("grp_out", I),
                 ("out_off", I), ("dup_n", I), ("dup_off", I), ("nbags", I), ("nh", I),
-                ("dh", I), ("seq", I), ("qscale", Fl), ("seed_ptr", P), ("colsum", P)]
+                ("dh", I), ("seq", I), ("qscale", Fl), ("seed_ptr", P), ("colsum", P), ("pre_bf16", I)]
 
 
 class BmmJob(C.Structure):

@@ -24,6 +24,8 @@
 #include <new>
 
 #include "common.h"
+
+#include <cstdlib>
 #include "../../include/transmil_hip.h"
 
 namespace {
@@ -333,9 +335,15 @@ TM_DEV void gemm_epilogue_rows(const char* smem, OutT* __restrict__ C, const tm_
 #pragma unroll
       for (int e = 0; e < 8; ++e) x[e] = v[e] * g.alpha + bv[e];
       vec8<OutT> pre8, out8;
+      bf16x8 preb;
       if (g.pre) {
+        if (g.pre_bf16) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) pre8[e] = from_f<OutT>(x[e]);
+          for (int e = 0; e < 8; ++e) preb[e] = (bf16)x[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) pre8[e] = from_f<OutT>(x[e]);
+        }
       }
       if (g.gelu) {
 #pragma unroll
@@ -358,12 +366,16 @@ TM_DEV void gemm_epilogue_rows(const char* smem, OutT* __restrict__ C, const tm_
 #pragma unroll
       for (int e = 0; e < 8; ++e) out8[e] = from_f<OutT>(x[e]);
       if (vec) {
-        if (g.pre) store8<OutT>((OutT*)g.pre + (size_t)m * g.ld_pre + n, pre8);
+        if (g.pre) {
+          if (g.pre_bf16) store8<bf16>((bf16*)g.pre + (size_t)m * g.ld_pre + n, preb);
+          else store8<OutT>((OutT*)g.pre + (size_t)m * g.ld_pre + n, pre8);
+        }
         store8<OutT>(C + off, out8);
         if (dup >= 0) store8<OutT>(C + (size_t)dup * g.ldc + n, out8);
       } else {
         for (int e = 0; e < ne; ++e) {
-          if (g.pre) ((OutT*)g.pre)[(size_t)m * g.ld_pre + n + e] = pre8[e];
+          if (g.pre && g.pre_bf16) ((bf16*)g.pre)[(size_t)m * g.ld_pre + n + e] = preb[e];
+          else if (g.pre) ((OutT*)g.pre)[(size_t)m * g.ld_pre + n + e] = pre8[e];
           C[off + e] = out8[e];
           if (dup >= 0) C[(size_t)dup * g.ldc + n + e] = out8[e];
         }
@@ -1427,7 +1439,7 @@ inline bool use_ring160(const tm_gemm_args& g) {
 // the persistent register-epilogue kernel (k-contiguous A, no split): diagnostic build only, variant
 // 11 wherever valid (the product library never selects it: slower on every step shape)
 inline bool use_pr(const tm_gemm_args& g) {
-  if (g.a_trans || g.splits != 1 || g.K % 64 != 0 || g.mode == TM_EPI_SPLITK) return false;
+  if (g.a_trans || g.splits != 1 || g.K % 64 != 0 || g.mode == TM_EPI_SPLITK || g.pre_bf16) return false;
   if (g.b_kn && (g.N % 8 != 0 || g.N < 8)) return false;
   return GEMM_VARIANT == 11;
 }
@@ -1437,10 +1449,14 @@ inline bool use_pr(const tm_gemm_args& g) {
 // product for the to_qkv projection (head-major scatter epilogue, N >= 1024, no split): 198 tiles of
 // 256 x 256 at n' = 8448 fill the chip in one round where the 128 x 128 ring needed 1.55 rounds of
 // 792 tiles (microbench 23.2 vs 27.6 us; scripts/microbench.py --gemm-ab)
+inline bool qkv_big_enabled() {   // TM_GEMM_QKV_BIG=0: the 128 x 128 ring for to_qkv (A/B runs only)
+  static const bool on = [] { const char* e = std::getenv("TM_GEMM_QKV_BIG"); return !(e && e[0] == '0'); }();
+  return on;
+}
 template <typename OutT>
 bool big_ok(const tm_gemm_args& g) {
   const bool qkv_pick = GEMM_VARIANT == 0 && g.mode == TM_EPI_QKV && g.N >= 1024 && g.splits == 1 && g.M >= 2048 &&
-                        !g.a_trans && !g.b_kn;
+                        !g.a_trans && !g.b_kn && qkv_big_enabled();
   if (GEMM_VARIANT != 7 && !qkv_pick) return false;
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
   if (g.a_trans && (g.M % 8 != 0 || g.M < 8)) return false;

@@ -132,7 +132,7 @@ __global__ void dropout_bwd_pad_kernel(const float* __restrict__ dH, int S, int 
 // columns per thread (16-B loads, one 16-B T store), 4 rows per 256-thread block; block (0, 0) also
 // writes the class-token gradient dcls = sum_b dH[b, 0, :] (one launch for both).
 template <typename T>
-__global__ __launch_bounds__(256) void fc1_gelu_bwd_kernel(const float* __restrict__ dH, const float* __restrict__ pre,
+__global__ __launch_bounds__(256) void fc1_gelu_bwd_kernel(const float* __restrict__ dH, const T* __restrict__ pre,
                                                            int B, int N, int S, int add, int D, T* __restrict__ dpre,
                                                            float* __restrict__ dcls) {
   const int b = blockIdx.y, i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -149,7 +149,9 @@ __global__ __launch_bounds__(256) void fc1_gelu_bwd_kernel(const float* __restri
   const size_t o = ((size_t)b * N + i) * D;
   for (int c = lane * 8; c < D; c += 64 * 8) {
     const f32x4 a0 = *(const f32x4*)(g0 + c), a1 = *(const f32x4*)(g0 + c + 4);
-    const f32x4 p0 = *(const f32x4*)(pre + o + c), p1 = *(const f32x4*)(pre + o + c + 4);
+    const vec8<T> pv = load8<T>(pre + o + c);   // the pre-activation in T (bf16 step: bf16)
+    const f32x4 p0 = {to_f(pv[0]), to_f(pv[1]), to_f(pv[2]), to_f(pv[3])};
+    const f32x4 p1 = {to_f(pv[4]), to_f(pv[5]), to_f(pv[6]), to_f(pv[7])};
     f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
     if (i < add) { d0 = *(const f32x4*)(g1 + c); d1 = *(const f32x4*)(g1 + c + 4); }
     vec8<T> out;
@@ -322,13 +324,13 @@ extern "C" int tm_pad_rows(int dtype, const float* x, int B, int S, int n_pad, i
   return 0;
 }
 
-extern "C" int tm_fc1_gelu_bwd(int dtype, const float* dH, const float* pre, int B, int N, int S, int add, int D,
+extern "C" int tm_fc1_gelu_bwd(int dtype, const float* dH, const void* pre, int B, int N, int S, int add, int D,
                                void* dpre, float* dcls, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   TM_REQUIRE(D % 8 == 0 && ((uintptr_t)dH % 16) == 0 && ((uintptr_t)pre % 16) == 0 && ((uintptr_t)dpre % 16) == 0,
              "fc1_gelu_bwd: D % 8 == 0 and 16-B aligned rows");
-  TM_DTYPE_DISPATCH(dtype, (fc1_gelu_bwd_kernel<T><<<dim3((N + 3) / 4, B), 256, 0, st>>>(dH, pre, B, N, S, add, D,
-                                                                                         (T*)dpre, dcls)));
+  TM_DTYPE_DISPATCH(dtype, (fc1_gelu_bwd_kernel<T><<<dim3((N + 3) / 4, B), 256, 0, st>>>(dH, (const T*)pre, B, N, S,
+                                                                                         add, D, (T*)dpre, dcls)));
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -131,7 +131,7 @@ class Geometry:
 # ----------------------------------------------------------------------------- GEMM helpers
 def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c_dtype=None,
          alpha=1.0, bias=None, gelu=False, pre=None, ld_pre=0, drop_p=0.0, seed=0, seed_ptr=None, resid=None,
-         accumulate=False, rowmap=None, qkv=None, splits=1, k_per_split=None):
+         accumulate=False, rowmap=None, qkv=None, splits=1, k_per_split=None, pre_bf16=False):
     g = GemmArgs()
     g.M, g.N, g.K = M, N, K
     g.lda, g.ldb, g.ldc = lda, ldb, ldc
@@ -149,6 +149,7 @@ def gemm(A, B, Cout, M, N, K, *, lda, ldb, ldc, a_trans=0, b_kn=0, dtype=BF16, c
     g.gelu = int(gelu)
     g.pre = _p(pre)
     g.ld_pre = ld_pre
+    g.pre_bf16 = int(pre_bf16)
     g.drop_p = drop_p
     g.drop_scale = 1.0 / (1.0 - drop_p) if drop_p > 0 else 1.0
     g.seed = seed
@@ -828,10 +829,14 @@ class TransMILEngine:
             if geo.add:
                 H0v[:, N + 1:].copy_(xe[:, :geo.add])
         else:
-            pre = pool(B * N * D).view(B * N, D)   # fp32 pre-activation for the GELU backward
+            # the pre-activation for the GELU backward, in T: bf16 in the bf16 step (half the bytes of the
+            # fp32 store and of its read-back; the GELU derivative's input then carries bf16 precision,
+            # as the _fc1 operands themselves do), fp32 in the parity mode
+            pre = pool(B * N * D, self.tdtype).view(B * N, D)
             with probe("fc1_gemm"):
                 gemm(xt, prm["w1"], H0, B * N, D, F, lda=F, ldb=F, ldc=D, dtype=self.dt_code, c_dtype=F32,
-                     bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N))
+                     bias=prm["b1"], gelu=True, pre=pre, ld_pre=D, rowmap=(N, 0, geo.S, 1, geo.add, 1 + N),
+                     pre_bf16=self.dt_code == BF16)
         H1, s1 = translayer_forward(H0, geo, prm[1], self.tdtype, self.dt_code, pool, drop_p, seeds[0], seed_dev)
         H2 = pool(B * geo.S * D).view(B * geo.S, D)
         with probe("ppeg_fwd"):
