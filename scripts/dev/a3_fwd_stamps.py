@@ -1,7 +1,7 @@
 """Per-phase s_memtime stamps of the bf16 A3 forward (a3_fwd_v2_kernel) at the bench shape
 (diagnostic build, variant 32): slots 0 start, 1 chunk-0 loads + query fragments issued, 2 chunk 0
 staged, 3 chunk 0 computed, 4 chunk 1 staged, 5 key loop done, 6 partials stored (waitcnt 0).
-Prints mean / max cycle deltas over workgroups for waves 0 and 4."""
+Prints mean / max cycle deltas over workgroups for each wave."""
 import ctypes as C, os, sys, time
 sys.path.insert(0, os.getcwd())
 os.environ.setdefault("TRANSMIL_HIP_LIB", os.path.join(os.getcwd(), "transmil_deepgraft_amd", "libtransmil_hip_diag.so"))
@@ -38,7 +38,7 @@ nblk = P * nbh
 buf = (C.c_ulonglong * (512 * 8 * 8))()
 _lib.call("tm_debug_a1_stamps", buf, 512 * 8 * 8)
 a = np.frombuffer(buf, dtype=np.uint64).reshape(512, 8, 8)[:nblk].astype(np.int64)
-for w in (0, 4):
+for w in range(8):
     st = a[:, w, :7]
     d = np.diff(st, axis=1)
     print(f"wave {w}: mean cycles per phase", [int(x) for x in d.mean(0)], " max", [int(x) for x in d.max(0)])

@@ -33,6 +33,7 @@ qkv_out = torch.empty(3, 8, n, 64, device=dev, dtype=torch.bfloat16)
 out32 = torch.empty(S, 512, device=dev)
 fc1_out = torch.empty(S, 512, device=dev)
 pre = torch.empty(N, 512, device=dev)
+pre_b = torch.empty(N, 512, device=dev, dtype=torch.bfloat16)
 X8192 = (torch.randn(N, 512, device=dev) * 0.1).to(torch.bfloat16)
 dm = torch.empty(n, 512, device=dev, dtype=torch.bfloat16)
 
@@ -46,6 +47,15 @@ cases = {
                                      c_dtype=F32, bias=bias, resid=resid, rowmap=(n, pad, S, 0, 0, 0)), n, 512),
     "fc1": (lambda: E.gemm(X8192, W512, fc1_out, N, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16, c_dtype=F32,
                            bias=bias, gelu=True, pre=pre, ld_pre=512, rowmap=(N, 0, S, 1, 89, 1 + N)), N, 512),
+    "fc1_prebf16": (lambda: E.gemm(X8192, W512, fc1_out, N, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16,
+                                   c_dtype=F32, bias=bias, gelu=True, pre=pre_b, ld_pre=512, pre_bf16=True,
+                                   rowmap=(N, 0, S, 1, 89, 1 + N)), N, 512),
+    "fc1_nogelu":(lambda: E.gemm(X8192, W512, fc1_out, N, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16,
+                                  c_dtype=F32, bias=bias, pre=pre, ld_pre=512, rowmap=(N, 0, S, 1, 89, 1 + N)), N, 512),
+    "fc1_nopre": (lambda: E.gemm(X8192, W512, fc1_out, N, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16,
+                                 c_dtype=F32, bias=bias, gelu=True, rowmap=(N, 0, S, 1, 89, 1 + N)), N, 512),
+    "fc1_plain": (lambda: E.gemm(X8192, W512, fc1_out, N, 512, 512, lda=512, ldb=512, ldc=512, dtype=BF16,
+                                 c_dtype=F32, bias=bias, rowmap=(N, 0, S, 1, 89, 1 + N)), N, 512),
     "dmerged_128": (lambda: E.gemm(A512, W512, dm, n, 512, 512, lda=512, ldb=512, ldc=512, b_kn=1, dtype=BF16),
                     n, 512),
 }
