@@ -265,6 +265,35 @@ def test_fused_radam_lookahead_matches_torch(k):
         torch.testing.assert_close(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=2e-5, atol=1e-10)
 
 
+@pytest.mark.gpu
+def test_fused_radam_lookahead_grid_stride_matches_torch():
+    """The optimizer launch walks the flat state grid-strided (at most 1024 workgroups of 256 x 4
+    elements per pass): ~2.9 M elements over odd-sized tensors take three passes, with tensor
+    boundaries and padding tails inside a wave; 8 steps incl. two Lookahead syncs (k = 3)."""
+    from transmil_deepgraft_amd.interface import FusedRAdamLookahead
+    torch.manual_seed(5)
+    sizes = [(1000, 1003), (7,), (1299, 1001), (513, 511), (3,), (101,)]
+    a = [nn.Parameter(torch.randn(s, device="cuda") * 0.1) for s in sizes]
+    b = [nn.Parameter(p.detach().clone()) for p in a]
+    groups = lambda ps: [{"params": ps[:3], "weight_decay": 0.05}, {"params": ps[3:], "weight_decay": 0.0}]
+    opt_a = FusedRAdamLookahead(groups(a), lr=3e-3, lookahead_k=3)
+    base = torch.optim.RAdam(groups(b), lr=3e-3)
+    opt_b = RefLookahead(base, k=3)
+    for step in range(8):
+        g = torch.Generator().manual_seed(200 + step)
+        for pa, pb in zip(a, b):
+            pa.grad = (torch.randn(pa.shape, generator=g) * 0.1).cuda()
+            pb.grad = pa.grad.clone()
+        opt_a.step()
+        opt_b.step()
+    torch.cuda.synchronize()
+    assert sum(p.numel() for p in a) > 2 * 1024 * 1024
+    for pa, pb in zip(a, b):
+        torch.testing.assert_close(pa, pb, rtol=2e-5, atol=2e-6)
+    c = opt_a._counters.cpu()
+    assert (c[:c.numel() // 2 * 2].view(-1, 2) == 8).all()
+
+
 def test_fc1_branches_and_mdmil_state_dict_keys():
     """Host logic of the model entry points (no GPU): the 2048 branch selects the RCC engine
     layout, the reference-broken 1024 branch raises, and MDMIL / TransMIL(2048) expose exactly
