@@ -782,7 +782,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void g
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ring_stamp<STAMP>(ts, 6);
     ring_stamp<STAMP>(ts, 7, true);
-    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;   // split-K grids too
     if (tid < 8 && blk < 2048) {
       unsigned long long v = ts[0];
 #pragma unroll
