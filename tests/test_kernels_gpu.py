@@ -709,6 +709,62 @@ def test_cls_q_rows_against_torch(B, n, nslabs):
     assert (Aq[:, NL + 1:] == 0).all() and (Xs[:, NL + 1:] == 0).all()
 
 
+@pytest.mark.parametrize("deferred", [False, True])
+@pytest.mark.parametrize("nbags,n", [(1, 8448), (2, 1024)])
+def test_a1_bwd_bf16_landmark_and_y_grads_vs_fp64(nbags, n, deferred):
+    """The bf16 A1 backward's key-side sums against fp64: dk~ = dS^T q and dY = P^T dO with
+    P = exp(q k~^T - lse), dS = P o (dO Y^T - D).  Its per-workgroup partials are bf16 slabs
+    (rounded once each, summed in fp32 in index order by the flush); checked through the immediate
+    reduce and through a caller-owned queue flushed afterwards (the engine's deferred form), which
+    must give the same bits."""
+    L = _lib()
+    import ctypes as C_
+    from transmil_deepgraft_amd.engine import _p, _stream
+    nh, nbh = 8, 8 * nbags
+    g = torch.Generator(device="cpu").manual_seed(29 + n)
+    q = (torch.randn(nbh, n, 64, generator=g) * 0.3).to(torch.bfloat16)
+    kl = (torch.randn(nbh, 256, 64, generator=g) * 0.3).to(torch.bfloat16)
+    y = torch.randn(nbh, 256, 64, generator=g).to(torch.bfloat16)
+    dm = (torch.randn(nbags, n, nh * 64, generator=g) * 0.1).to(torch.bfloat16)
+    lse = torch.logsumexp(q.float() @ kl.float().transpose(1, 2), -1)
+    d1 = torch.randn(nbh, n, generator=g) * 0.05
+    qd, kd, yd, dmd, lsed, d1d = (t.to(DEV).contiguous() for t in (q, kl, y, dm, lse, d1))
+    ws = L.query("tm_nys_a1_bwd_workspace", nbh, n, 256) // 4
+    work = torch.empty(ws, device=DEV)
+    dkl = torch.full((nbh, 256, 64), 3.0, device=DEV)
+    dy = torch.full((nbh, 256, 64), 3.0, device=DEV)
+    dq = torch.empty(nbh, n, 64, device=DEV)
+    rq = C_.c_void_p(L.lib().tm_reduce_queue_create()) if deferred else None
+    try:
+        L.call("tm_nys_a1_bwd", 1, _p(qd), _p(dmd), _p(kd), _p(yd), _p(lsed), _p(d1d), nbh, nh, n, 256,
+               _p(dq), _p(work), _p(dkl), _p(dy), 0, rq, _stream())
+        if deferred:
+            assert L.lib().tm_reduce_queue_pending(rq) == 2
+            L.call("tm_reduce_flush", rq, _stream())
+        torch.cuda.synchronize()
+    finally:
+        if deferred:
+            L.lib().tm_reduce_queue_destroy(rq)
+    # fp64 reference per head
+    dO = dm.double().view(nbags, n, nh, 64).permute(0, 2, 1, 3).reshape(nbh, n, 64)
+    qf, kf, yf = q.double(), kl.double(), y.double()
+    P = torch.exp(qf @ kf.transpose(1, 2) - lse.double()[..., None])
+    dS = P * (dO @ yf.transpose(1, 2) - d1.double()[..., None])
+    ek = dS.transpose(1, 2) @ qf
+    ey = P.transpose(1, 2) @ dO
+    ak, ay = dkl.cpu(), dy.cpu()
+    rk, ry = _rel(ak, ek), _rel(ay, ey)
+    # bf16 partials (2^-9 each) over fp32 sums of bf16 products: well inside 4e-3 of the max
+    assert rk < 4e-3 and ry < 4e-3, (rk, ry)
+    test_a1_bwd_bf16_landmark_and_y_grads_vs_fp64.last = getattr(test_a1_bwd_bf16_landmark_and_y_grads_vs_fp64,
+                                                                 "last", {})
+    key = (nbags, n)
+    prev = test_a1_bwd_bf16_landmark_and_y_grads_vs_fp64.last.get(key)
+    if prev is not None:                       # the other reduce path: identical bits
+        assert torch.equal(prev[0], ak) and torch.equal(prev[1], ay)
+    test_a1_bwd_bf16_landmark_and_y_grads_vs_fp64.last[key] = (ak, ay)
+
+
 @pytest.mark.parametrize("nbags,n", [(1, 1024), (2, 512)])
 def test_a1_bwd_dqkv_bf16_path_equals_the_fp32_dq_path(nbags, n):
     """The bf16 layer-1 path (tm_nys_a1_bwd_dqkv: bf16(scale dq) straight into dqkv, then

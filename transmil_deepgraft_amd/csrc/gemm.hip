@@ -1728,7 +1728,7 @@ extern "C" int tm_debug_gemm_stamps(unsigned long long* host, int count) {
 namespace {
 constexpr int DEFER_MAX = 48;
 struct ReduceEntry {
-  const float* slab;
+  const void* slab;  // fp32, or bf16 (bf16 != 0: the bf16-mode attention partial slabs)
   float* out;
   long long count;
   int splits;
@@ -1738,6 +1738,7 @@ struct ReduceEntry {
   int par;   // threads per output unit (power of 2 <= 64): each sums every par-th split, then a
              // fixed xor-shuffle tree (entries with many splits and few outputs, e.g. LayerNorm
              // weight partials of every 32-row block, would otherwise be one long serial loop)
+  int bf16;  // slab elements are bf16 (summed in fp32 like the fp32 ones, same order)
 };
 struct ReduceTable {
   ReduceEntry e[DEFER_MAX];
@@ -1775,8 +1776,17 @@ __global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     for (int z0 = sub; z0 < r.splits; z0 += U * par) {
       f32x4 v[U];
+      if (r.bf16) {
 #pragma unroll
-      for (int k = 0; k < U; ++k) v[k] = *(const f32x4*)(r.slab + (size_t)min(z0 + k * par, r.splits - 1) * r.count + j);
+        for (int k = 0; k < U; ++k) {
+          const bf16x4 b = *(const bf16x4*)((const bf16*)r.slab + (size_t)min(z0 + k * par, r.splits - 1) * r.count + j);
+          v[k] = (f32x4){(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+          v[k] = *(const f32x4*)((const float*)r.slab + (size_t)min(z0 + k * par, r.splits - 1) * r.count + j);
+      }
 #pragma unroll
       for (int k = 0; k < U; ++k) s += (z0 + k * par < r.splits) ? v[k] : (f32x4){0.f, 0.f, 0.f, 0.f};
     }
@@ -1793,7 +1803,10 @@ __global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
   for (int z0 = sub; z0 < r.splits; z0 += U * par) {
     float v[U];
 #pragma unroll
-    for (int k = 0; k < U; ++k) v[k] = r.slab[(size_t)min(z0 + k * par, r.splits - 1) * r.count + u];
+    for (int k = 0; k < U; ++k) {
+      const size_t idx = (size_t)min(z0 + k * par, r.splits - 1) * r.count + u;
+      v[k] = r.bf16 ? (float)((const bf16*)r.slab)[idx] : ((const float*)r.slab)[idx];
+    }
 #pragma unroll
     for (int k = 0; k < U; ++k) s += (z0 + k * par < r.splits) ? v[k] : 0.f;
   }
@@ -1840,25 +1853,54 @@ extern "C" int tm_reduce_flush(tm_reduce_queue* q, void* stream) {
   return 0;
 }
 
+namespace {
+// one multi_reduce entry appended to t (the caller has made room)
+void push_reduce_entry(ReduceTable& t, const void* slab, int slab_bf16, float* out, int splits, long long count,
+                       float alpha, int accumulate) {
+  const int vec = count % 4 == 0 && ((uintptr_t)slab % (slab_bf16 ? 8 : 16)) == 0 && ((uintptr_t)out % 16) == 0;
+  const long long units = vec ? count / 4 : count;
+  // threads per unit: enough that each sums <= 2 bursts of 12 splits, while the entry keeps
+  // to <= ~64 K threads
+  int par = 1;
+  while (par < 64 && (splits + par - 1) / par > 24 && units * par * 2 <= 65536) par <<= 1;
+  t.e[t.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha, vec, par, slab_bf16};
+  // offsets count threads: par per 16-B unit (or element)
+  t.off[t.n + 1] = t.off[t.n] + units * par;
+  ++t.n;
+}
+}  // namespace
+
+// Library-internal (not in the ABI header): the split-K sum of a slab of fp32 or bf16 partials
+// (slab_dtype TM_F32 / TM_BF16), deferred into q when given.  The bf16 form serves the bf16-mode
+// attention backward's partial slabs; both forms add the splits in index order in fp32.
+int tm_splitk_reduce_typed(const void* slab, int slab_dtype, float* out, int splits, long long count, float alpha,
+                           int accumulate, tm_reduce_queue* q, void* stream) {
+  if (slab_dtype == TM_F32)
+    return tm_splitk_reduce((const float*)slab, out, splits, count, alpha, accumulate, q, stream);
+  TM_REQUIRE(slab && out && splits >= 1 && count >= 0, "splitk_reduce: bad args");
+  TM_REQUIRE(!q || q->magic == RQ_MAGIC, "splitk_reduce: not a tm_reduce_queue");
+  if (count == 0) return 0;
+  if (q) {
+    if (q->t.n == DEFER_MAX)
+      if (int rc = tm_reduce_flush(q, stream)) return rc;
+    push_reduce_entry(q->t, slab, 1, out, splits, count, alpha, accumulate);
+    return 0;
+  }
+  tm_reduce_queue local{};   // not deferred: a one-entry table launched now
+  local.magic = RQ_MAGIC;
+  push_reduce_entry(local.t, slab, 1, out, splits, count, alpha, accumulate);
+  return tm_reduce_flush(&local, stream);
+}
+
 extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
                                 int accumulate, tm_reduce_queue* q, void* stream) {
   TM_REQUIRE(slab && out && splits >= 1 && count >= 0, "splitk_reduce: bad args");
   TM_REQUIRE(!q || q->magic == RQ_MAGIC, "splitk_reduce: not a tm_reduce_queue");
   if (count == 0) return 0;
   if (q) {
-    ReduceTable& t = q->t;
-    if (t.n == DEFER_MAX)
+    if (q->t.n == DEFER_MAX)
       if (int rc = tm_reduce_flush(q, stream)) return rc;
-    const int vec = count % 4 == 0 && ((uintptr_t)slab % 16) == 0 && ((uintptr_t)out % 16) == 0;
-    const long long units = vec ? count / 4 : count;
-    // threads per unit: enough that each sums <= 2 bursts of 12 splits, while the entry keeps
-    // to <= ~64 K threads
-    int par = 1;
-    while (par < 64 && (splits + par - 1) / par > 24 && units * par * 2 <= 65536) par <<= 1;
-    t.e[t.n] = ReduceEntry{slab, out, count, splits, accumulate, alpha, vec, par};
-    // offsets count threads: par per 16-B unit (or element)
-    t.off[t.n + 1] = t.off[t.n] + units * par;
-    ++t.n;
+    push_reduce_entry(q->t, slab, 0, out, splits, count, alpha, accumulate);
     return 0;
   }
   hipStream_t st = (hipStream_t)stream;

@@ -1567,9 +1567,18 @@ struct BwdArgs {
   // bf16 A1 kernel: dqkv non-null = dq written as bf16(dq_scale * dq) into the q part of dqkv
   // ([bag][q_total][3 nh 64], the columns of head bh % nh) instead of fp32 rows at dq
   float dq_scale;
+  // bf16 A1 kernel: 1 = the dk~ / dY partial slabs written as bf16 (half the slab bytes out and back
+  // through the deferred flush, which sums them in fp32); slab_stride / dk_bh / dv_bh then count
+  // bf16 elements
+  int slab_bf16;
 };
 
 enum { MODE_A3 = 0, MODE_A1 = 1 };
+}  // namespace
+// gemm.hip (library-internal): split-K sum of fp32 or bf16 partial slabs, deferred into q when given
+int tm_splitk_reduce_typed(const void* slab, int slab_dtype, float* out, int splits, long long count, float alpha,
+                           int accumulate, tm_reduce_queue* q, void* stream);
+namespace {
 #ifdef TM_DIAG
 int g_nys_variant = 0;
 #endif
@@ -2165,6 +2174,16 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
             (f32x4){accv[4 * g4], accv[4 * g4 + 1], accv[4 * g4 + 2], accv[4 * g4 + 3]};
     }
     __syncthreads();
+    if (MODE == MODE_A1 && a.slab_bf16) {
+      bf16* dstb = (bf16*)(which == 0 ? a.dv : a.dk) + (size_t)blk * a.slab_stride + bh * (which == 0 ? a.dv_bh : a.dk_bh);
+      for (int i = tid; i < nk * DH / 4; i += NT) {
+        const int key = i >> 4, d4 = (i & 15) * 4;
+        const f32x4 val = *(const f32x4*)(stage + key * 68 + d4);
+        *(bf16x4*)(dstb + (size_t)key * DH + d4) = (bf16x4){(bf16)val[0], (bf16)val[1], (bf16)val[2], (bf16)val[3]};
+      }
+      __syncthreads();
+      continue;
+    }
     float* dst;
     bool add = false;
     if (MODE == MODE_A3) {
@@ -2635,6 +2654,8 @@ int a1_bwd_impl(int dtype, const void* q, const void* dmerged, const void* kl_t,
   hipStream_t st = (hipStream_t)stream;
   if (split) {
     a.q_total = n;
+    // the dk~ / dY partials as bf16 (diagnostic variant 37: fp32, the earlier form)
+    a.slab_bf16 = NYS_VARIANT != 37;
 #ifdef TM_DIAG
     if (NYS_VARIANT == 33 || NYS_VARIANT == 34) {   // diagnostic: stamps per wave (33 phases, 34 inside chunk 2)
       auto kern = NYS_VARIANT == 33 ? attn_bwd_bf16_kernel<MODE_A1, 8, 1> : attn_bwd_bf16_kernel<MODE_A1, 8, 2>;
@@ -2658,9 +2679,10 @@ int a1_bwd_impl(int dtype, const void* q, const void* dmerged, const void* kl_t,
   }
   TM_CHECK_LAUNCH();
   const long long cnt = (long long)nbh * NL * DH;
-  int rc = tm_splitk_reduce(slab_k, dkl, nqc, cnt, 1.0f, accumulate, rq, stream);
+  const int sdt = a.slab_bf16 ? TM_BF16 : TM_F32;
+  int rc = tm_splitk_reduce_typed(slab_k, sdt, dkl, nqc, cnt, 1.0f, accumulate, rq, stream);
   if (rc) return rc;
-  return tm_splitk_reduce(slab_v, dy, nqc, cnt, 1.0f, 0, rq, stream);
+  return tm_splitk_reduce_typed(slab_v, sdt, dy, nqc, cnt, 1.0f, 0, rq, stream);
 }
 }  // namespace
 
