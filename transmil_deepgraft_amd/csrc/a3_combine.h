@@ -11,7 +11,7 @@
 #include "common.h"
 
 struct A3Combine {
-  const float* part_o;   // [P][nbh][256][64]  sum_keys exp(s - m) v
+  const bf16* part_o;    // [P][nbh][256][64]  sum_keys exp(s - m) v  (bf16; merged in fp32)
   const float* part_m;   // [P][nbh][256]      m
   const float* part_l;   // [P][nbh][256]      sum_keys exp(s - m)
   int P, nbh;
@@ -46,7 +46,8 @@ TM_DEV A3CombineState a3_combine_phase1(const A3Combine& c, int bh, int qy, int 
         const size_t pidx = (size_t)min(p0 + 2 * u, c.P - 1) * pstride + q0;
         mv[u] = c.part_m[pidx];
         lv[u] = c.part_l[pidx];
-        ov[u] = *(const f32x4*)(c.part_o + pidx * 64 + d4);
+        const bf16x4 b = *(const bf16x4*)(c.part_o + pidx * 64 + d4);
+        ov[u] = (f32x4){(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
       }
       float mb = s.M;
 #pragma unroll

@@ -985,7 +985,7 @@ struct Sim2Out { const float* kl; float* a2; bf16* a2s; };
 template <int ST = 0, int S2R = 0>   // ST: diagnostic s_memtime stamps (g_a1_stamps)
 __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict__ ql, const bf16* __restrict__ k,
                                                         const bf16* __restrict__ v, int n, int P,
-                                                        float* __restrict__ part_o, float* __restrict__ part_m,
+                                                        bf16* __restrict__ part_o, float* __restrict__ part_m,
                                                         float* __restrict__ part_l, Sim2Out s2) {
   constexpr int KROW = Lay<bf16>::KROW, VROW = Lay<bf16>::VROW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1132,15 +1132,15 @@ __global__ __launch_bounds__(512) void a3_fwd_v2_kernel(const float* __restrict_
   }
   const size_t pidx = ((size_t)p * nbh + bh) * NL + qi;
   if (h == 0) { part_m[pidx] = m_run; part_l[pidx] = l_run; }
-  float* po = part_o + pidx * DH;
+  // the unnormalised partial sum in bf16 (half the slab bytes out and through the combine, which
+  // merges the partials in fp32); m / l stay fp32
+  bf16* po = part_o + pidx * DH;
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      f32x4 val;
-      val[0] = o[dt][4 * g4]; val[1] = o[dt][4 * g4 + 1]; val[2] = o[dt][4 * g4 + 2]; val[3] = o[dt][4 * g4 + 3];
-      *(f32x4*)(po + dt * 32 + 8 * g4 + 4 * h) = val;
-    }
+    for (int g4 = 0; g4 < 4; ++g4)
+      *(bf16x4*)(po + dt * 32 + 8 * g4 + 4 * h) =
+          (bf16x4){(bf16)o[dt][4 * g4], (bf16)o[dt][4 * g4 + 1], (bf16)o[dt][4 * g4 + 2], (bf16)o[dt][4 * g4 + 3]};
   if (ST) {
     __builtin_amdgcn_s_waitcnt(0);
     stamp(6);
@@ -2432,8 +2432,8 @@ namespace {
 void launch_a3_fwd_v2(const float* ql, const void* k, const void* v, int nbh, int n, float* work, Sim2Out s2,
                       hipStream_t st) {
   const int P = a3v_splits(nbh, n);
-  float* po = work;
-  float* pm = po + (size_t)P * nbh * NL * DH;
+  bf16* po = (bf16*)work;                          // bf16 partial sums in the first half of an fp32-sized region
+  float* pm = work + (size_t)P * nbh * NL * DH;
   float* pl = pm + (size_t)P * nbh * NL;
   const dim3 grid(P, nbh);
   const bf16* kb = (const bf16*)k;
@@ -2475,8 +2475,8 @@ extern "C" int tm_nys_a3_fwd(int dtype, const float* ql, const void* k, const vo
     TM_CHECK_LAUNCH();
     if (!w) return 0;   // deferred: the combine runs in the pseudo-inverse chain (tm_pinv_fwd_split_a3)
     const int P = a3v_splits(nbh, n);
-    float* po = work;
-    float* pm = po + (size_t)P * nbh * NL * DH;
+    const bf16* po = (const bf16*)work;
+    float* pm = work + (size_t)P * nbh * NL * DH;
     float* pl = pm + (size_t)P * nbh * NL;
     a3_combine_v2_kernel<<<dim3(nbh, NL / 8), 256, 0, st>>>(A3Combine{po, pm, pl, P, nbh, w, lse3});
     TM_CHECK_LAUNCH();

@@ -992,13 +992,14 @@ extern "C" int tm_pinv_fwd_split(const float* X, const void* Xs, int nbh, int it
 }
 
 // as tm_pinv_fwd_split, and the A3 forward's partial combine (tm_nys_a3_fwd with w = null left the
-// partials in a3_work: part_o [P][nbh][256][64], then part_m, part_l [P][nbh][256]) runs beside the
+// partials in a3_work: part_o [P][nbh][256][64] bf16 in an fp32-sized region, then part_m, part_l
+// [P][nbh][256] fp32) runs beside the
 // chain's last product: W and lse3 are written by the same launch that writes Z_iters.
 extern "C" int tm_pinv_fwd_split_a3(const float* X, const void* Xs, int nbh, int iters, float* saved,
                                     const float* a3_work, int a3_parts, float* w, float* lse3, void* stream) {
   TM_REQUIRE(a3_work && w && lse3 && a3_parts >= 1, "pinv_fwd_split_a3: bad A3 args");
-  const float* po = a3_work;
-  const float* pm = po + (size_t)a3_parts * nbh * NL * 64;
+  const bf16* po = (const bf16*)a3_work;   // bf16 partial sums in the first half of their fp32-sized region
+  const float* pm = a3_work + (size_t)a3_parts * nbh * NL * 64;
   const float* pl = pm + (size_t)a3_parts * nbh * NL;
   const A3Combine a3{po, pm, pl, a3_parts, nbh, w, lse3};
   return pinv_fwd_split(X, Xs, nbh, iters, saved, &a3, stream);
