@@ -199,8 +199,9 @@ int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const flo
  * (k = dK + dk~[t/l]/l, v = dv_conv + dV) and dql (=) from its slabs; then tm_nys_assemble_q
  * writes the q part, scale * (dq + (dql_a + dql_b)[t/l]/l).  dv_conv is read only for rows
  * [dv_lo, dv_hi) (zero elsewhere; 0, n = dense); dq_row >= 0: dq is zero outside that row.
- * dql = NULL: the dq~ partial slab is left in work ([tm_nys_a3_bwd_slabs][B*h][256][64] fp32) for
- * tm_nys_assemble_q_slab, which reduces it while writing the q part (one launch fewer). */
+ * dql = NULL: the dq~ partial slab is left in work ([tm_nys_a3_bwd_slabs][B*h][256][64] bf16, each
+ * partial rounded once; the consumers sum them in fp32) for tm_nys_assemble_q_slab, which reduces it
+ * while writing the q part (one launch fewer). */
 int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v, const float* lse3,
                         const float* d3, int nbh, int nh, int n, const float* dv_conv, int dv_lo, int dv_hi,
                         const float* dkl, float* work, float* dql, void* dqkv, tm_reduce_queue* rq,
@@ -210,11 +211,11 @@ int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a
 /* partial slabs the bf16 A3 backward writes (tm_nys_a3_bwd_fused's work) */
 int tm_nys_a3_bwd_slabs(int nbh, int n);
 /* q part of dqkv, scale * (dq + (dql + sum_p slab[p])[t/l]/l), the slab sum in the same launch
- * (nh <= 8; slab [slabs][nbags*nh][256][64] fp32 as tm_nys_a3_bwd_fused(dql = NULL) leaves it) */
-int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, const float* dql, const float* slab, int slabs,
+ * (nh <= 8; slab [slabs][nbags*nh][256][64] bf16 as tm_nys_a3_bwd_fused(dql = NULL) leaves it) */
+int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, const float* dql, const void* slab, int slabs,
                            int nbags, int nh, int n, float scale, void* dqkv, void* stream);
 /* bf16, after tm_nys_a1_bwd_dqkv: q += scale * (dql + sum_p slab[p])[t/l]/l in place in dqkv */
-int tm_nys_assemble_q_slab_inplace(const float* dql, const float* slab, int slabs, int nbags, int nh, int n,
+int tm_nys_assemble_q_slab_inplace(const float* dql, const void* slab, int slabs, int nbags, int nh, int n,
                                    float scale, void* dqkv, void* stream);
 
 /* ---- pseudo-inverse + small fp32 batched products (pinv.hip) -------------
@@ -443,7 +444,7 @@ int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, const void*
  *   nslabs [B*nh][256][64] partials tm_nys_a3_bwd_fused leaves in its work), row 256: dq[b*nh+h][r][d];
  *   Xs rows j < 256: sum over the segment's rows of xn[b] (bf16 [B][n][nh*64], pad rows zero),
  *   row 256: xn[b][r]; rows 257..287 of both: zeros (operand rows to a multiple of 32). */
-int tm_cls_q_rows(const float* dql, const float* slab, int nslabs, const float* dq, const void* xn, int B, int nh,
+int tm_cls_q_rows(const float* dql, const void* slab, int nslabs, const float* dq, const void* xn, int B, int nh,
                   int n, int r, float* Aq, float* Xs, void* stream);
 
 /* fp32 -> dtype copies of up to 8 tensors (per-step bf16 GEMM weight operands) in one launch;

@@ -651,7 +651,8 @@ def test_colsum_bf16_matches_fp64(rows, cols, ld, acc):
 @pytest.mark.parametrize("B,n", [(2, 768), (1, 8448), (1, 33280)])   # l = 3, 33 (C2), 130 (C3)
 def test_assemble_q_slab_reduces_the_a3_partials(dtype, dq_row, B, n):
     """tm_nys_assemble_q_slab: q part of dqkv = scale * (dq + (dql + sum_p slab[p])[t / l] / l)
-    against fp64, the other two thirds of dqkv untouched (the fused A3 backward wrote them)."""
+    against fp64 (the slab's bf16 partials summed in fp32), the other two thirds of dqkv untouched
+    (the fused A3 backward wrote them)."""
     from transmil_deepgraft_amd._lib import BF16, F32
     from transmil_deepgraft_amd.engine import _p, _stream
     lib = _lib()
@@ -660,7 +661,7 @@ def test_assemble_q_slab_reduces_the_a3_partials(dtype, dq_row, B, n):
     g = torch.Generator(device=DEV).manual_seed(11)
     dq = torch.randn(nbh, n, 64, device=DEV, generator=g)
     dql = torch.randn(nbh, 256, 64, device=DEV, generator=g)
-    slab = torch.randn(slabs, nbh, 256, 64, device=DEV, generator=g)
+    slab = torch.randn(slabs, nbh, 256, 64, device=DEV, generator=g).to(torch.bfloat16)   # as the fused A3 backward leaves it
     dqkv = torch.full((B, n, 3 * nh * 64), 7.0, device=DEV).to(dtype)
     lib.call("tm_nys_assemble_q_slab", BF16 if dtype == torch.bfloat16 else F32, _p(dq), dq_row, _p(dql), _p(slab),
              slabs, B, nh, n, C.c_float(scale), _p(dqkv), _stream())
@@ -690,7 +691,7 @@ def test_cls_q_rows_against_torch(B, n, nslabs):
     nbh, l, r = B * nh, n // 256, n // 3
     g = torch.Generator(device="cpu").manual_seed(n + nslabs)
     dql = torch.randn(nbh, NL, 64, generator=g).to(DEV)
-    slab = torch.randn(max(nslabs, 1), nbh, NL, 64, generator=g).to(DEV)
+    slab = torch.randn(max(nslabs, 1), nbh, NL, 64, generator=g).to(torch.bfloat16).to(DEV)   # bf16 partials
     dq = torch.randn(nbh, n, 64, generator=g).to(DEV)
     xn = torch.randn(B, n, D, generator=g).to(torch.bfloat16).to(DEV)
     Aq = torch.full((B, QROWS, D), float("nan"), device=DEV)
@@ -784,7 +785,7 @@ def test_a1_bwd_dqkv_bf16_path_equals_the_fp32_dq_path(nbags, n):
     lse = torch.logsumexp(q.float() @ kl.float().transpose(1, 2), -1)          # a consistent softmax
     d1 = torch.randn(nbh, n, generator=g) * 0.05
     dql = torch.randn(nbh, 256, 64, generator=g) * 0.1
-    slab = torch.randn(slabs, nbh, 256, 64, generator=g) * 0.1
+    slab = (torch.randn(slabs, nbh, 256, 64, generator=g) * 0.1).to(torch.bfloat16)
     qd, kd, yd, dmd, lsed, d1d, dqld, slabd = (t.to(DEV).contiguous() for t in (q, kl, y, dm, lse, d1, dql, slab))
     ws = L.query("tm_nys_a1_bwd_workspace", nbh, n, 256) // 4
     sentinel = 7.0

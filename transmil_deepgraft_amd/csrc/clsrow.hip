@@ -358,7 +358,7 @@ constexpr int QROWS = NL + 32;   // rows per bag: NL landmark rows, the class ro
 // 8 row groups x 64 threads x 8 columns; the groups' partial sums are combined through LDS in a
 // fixed order.
 constexpr int QR_SLABS = 64;     // slabs per burst: 16 pieces per thread
-__global__ __launch_bounds__(512) void cls_q_rows_kernel(const float* __restrict__ dql, const float* __restrict__ slab,
+__global__ __launch_bounds__(512) void cls_q_rows_kernel(const float* __restrict__ dql, const bf16* __restrict__ slab,
                                                          int nslabs, const float* __restrict__ dq,
                                                          const bf16* __restrict__ xn, int nh, int n, int r,
                                                          float* __restrict__ Aq, float* __restrict__ Xs) {
@@ -397,7 +397,12 @@ __global__ __launch_bounds__(512) void cls_q_rows_kernel(const float* __restrict
 #pragma unroll
     for (int i = 0; i < QR_SLABS / 4; ++i) {
       const int p = p0 + g + 4 * i;
-      sp[i] = p < nslabs ? *(const f32x4*)(slab + p * ss + o) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      if (p < nslabs) {   // bf16 partials (tm_nys_a3_bwd_fused), summed in fp32
+        const bf16x4 v = *(const bf16x4*)(slab + p * ss + o);
+        sp[i] = (f32x4){(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+      } else {
+        sp[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
     }
     bf16x8 xp[XR];
 #pragma unroll
@@ -505,12 +510,12 @@ extern "C" int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, 
   return 0;
 }
 
-extern "C" int tm_cls_q_rows(const float* dql, const float* slab, int nslabs, const float* dq, const void* xn, int B,
+extern "C" int tm_cls_q_rows(const float* dql, const void* slab, int nslabs, const float* dq, const void* xn, int B,
                              int nh, int n, int r, float* Aq, float* Xs, void* stream) {
   TM_REQUIRE(dql && dq && xn && Aq && Xs && B > 0 && nh * DH == 512 && (nslabs == 0 || slab),
              "cls_q_rows: bad args (nh * 64 must be 512)");
   TM_REQUIRE(n % NL == 0 && r >= 0 && r < n && nslabs >= 0, "cls_q_rows: bad row / n / slab count");
-  cls_q_rows_kernel<<<dim3(QROWS, B), 512, 0, (hipStream_t)stream>>>(dql, slab, nslabs, dq, (const bf16*)xn, nh, n, r,
+  cls_q_rows_kernel<<<dim3(QROWS, B), 512, 0, (hipStream_t)stream>>>(dql, (const bf16*)slab, nslabs, dq, (const bf16*)xn, nh, n, r,
                                                                      Aq, Xs);
   TM_CHECK_LAUNCH();
   return 0;

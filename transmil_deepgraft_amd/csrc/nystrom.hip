@@ -1567,9 +1567,9 @@ struct BwdArgs {
   // bf16 A1 kernel: dqkv non-null = dq written as bf16(dq_scale * dq) into the q part of dqkv
   // ([bag][q_total][3 nh 64], the columns of head bh % nh) instead of fp32 rows at dq
   float dq_scale;
-  // bf16 A1 kernel: 1 = the dk~ / dY partial slabs written as bf16 (half the slab bytes out and back
-  // through the deferred flush, which sums them in fp32); slab_stride / dk_bh / dv_bh then count
-  // bf16 elements
+  // 1 = partial slabs written as bf16 (half the slab bytes out and back; their consumers sum them in
+  // fp32): the bf16 A1 kernel's dk~ / dY slabs (through the deferred flush), the fused A3 backward's
+  // dq~ slab (through assemble_q_slab / cls_q_rows); the slab strides then count bf16 elements
   int slab_bf16;
 };
 
@@ -2039,6 +2039,10 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
           bf16* qo = (bf16*)a.dqkv + ((size_t)bag * a.q_total + q_begin + c0) * ld + hh * DH + dtq * 32 + r;
 #pragma unroll
           for (int i = 0; i < 16; ++i) qo[(size_t)acc_row(i, h) * ld] = (bf16)(a.dq_scale * acc[i]);
+        } else if (MODE == MODE_A3 && a.slab_bf16) {   // the fused A3 backward's dq~ partials as bf16
+          bf16* dst = (bf16*)a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh + (size_t)(q_begin + c0) * DH + dtq * 32 + r;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) dst[(size_t)acc_row(i, h) * DH] = (bf16)acc[i];
         } else {
           float* dst = MODE == MODE_A1 ? a.dq + bh * a.dq_bh : a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh;
           dst += (size_t)(q_begin + c0) * DH + dtq * 32 + r;
@@ -2074,7 +2078,11 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
           const int q = tid >> 4, d4 = (tid & 15) * 4;
           const f32x4 v = (*(const f32x4*)(xch + q * 64 + d4) + *(const f32x4*)(xch + 2048 + q * 64 + d4)) +
                           *(const f32x4*)(xch + 4096 + q * 64 + d4);
-          *(f32x4*)(dst + (size_t)q * DH + d4) = v;
+          if (MODE == MODE_A3 && a.slab_bf16)
+            *(bf16x4*)((bf16*)a.dq + (size_t)blk * a.slab_stride + bh * a.dq_bh + (size_t)(q_begin + c0 + q) * DH + d4) =
+                (bf16x4){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          else
+            *(f32x4*)(dst + (size_t)q * DH + d4) = v;
         }
       } else if (kq == 0) {
         if (MODE == MODE_A1 && a.dqkv) {
@@ -2283,7 +2291,7 @@ constexpr int AQ_THREADS = 512, AQ_GROUPS = AQ_THREADS / 64, AQ_QP = 5;
 template <typename T, bool INPLACE = false>
 __global__ __launch_bounds__(AQ_THREADS) void assemble_q_slab_kernel(const float* __restrict__ dq, int dq_row,
                                                                      const float* __restrict__ dql,
-                                                                     const float* __restrict__ slab, int slabs,
+                                                                     const bf16* __restrict__ slab, int slabs,
                                                                      long long slab_count, int n, int l, int nh,
                                                                      float scale, T* __restrict__ dqkv) {
   __shared__ __attribute__((aligned(16))) float part[AQ_GROUPS][8 * DH];   // [group][nh <= 8 heads x 64 d]
@@ -2322,18 +2330,18 @@ __global__ __launch_bounds__(AQ_THREADS) void assemble_q_slab_kernel(const float
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       int p = g;
       for (; p + 3 * AQ_GROUPS < slabs; p += 4 * AQ_GROUPS) {   // four partials in flight per thread
-        f32x8 v[4];
+        bf16x8 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = load8<float>(slab + (size_t)(p + AQ_GROUPS * u) * slab_count + off);
+        for (int u = 0; u < 4; ++u) v[u] = load8<bf16>(slab + (size_t)(p + AQ_GROUPS * u) * slab_count + off);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[e] += v[u][e];
+          for (int e = 0; e < 8; ++e) acc[e] += (float)v[u][e];
       }
       for (; p < slabs; p += AQ_GROUPS) {
-        const f32x8 v = load8<float>(slab + (size_t)p * slab_count + off);
+        const bf16x8 v = load8<bf16>(slab + (size_t)p * slab_count + off);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+        for (int e = 0; e < 8; ++e) acc[e] += (float)v[e];
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) part[g][c + e] = acc[e];
@@ -2795,31 +2803,32 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   a.dv_lo = dv_lo; a.dv_hi = dv_hi;
   hipStream_t st = (hipStream_t)stream;
   int slabs = nkb;
+  a.slab_bf16 = 1;      // the dq~ partials as bf16 ([slabs][B*h][256][64], summed in fp32 by the consumer)
   launch_a3_bwd_bf16(a, nbh, n, st, slabs);
   TM_CHECK_LAUNCH();
   if (!dql) return 0;   // the slab stays for tm_nys_assemble_q_slab
-  return tm_splitk_reduce(work, dql, slabs, (long long)nbh * NL * DH, 1.0f, 0, rq, stream);
+  return tm_splitk_reduce_typed(work, TM_BF16, dql, slabs, (long long)nbh * NL * DH, 1.0f, 0, rq, stream);
 }
 
 extern "C" int tm_nys_a3_bwd_slabs(int nbh, int n) { return a3_bwd_split(nbh, n).wpg; }
 
-extern "C" int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, const float* dql, const float* slab,
+extern "C" int tm_nys_assemble_q_slab(int dtype, const float* dq, int dq_row, const float* dql, const void* slab,
                                       int slabs, int nbags, int nh, int n, float scale, void* dqkv, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0 && nh > 0 && nh <= 8 && slabs > 0, "assemble_q_slab: bad shape");
   TM_REQUIRE(dq && dql && slab && dqkv, "assemble_q_slab: null operand");
   TM_DTYPE_DISPATCH(dtype, (assemble_q_slab_kernel<T><<<dim3(NL, nbags), AQ_THREADS, 0, (hipStream_t)stream>>>(
-                               dq, dq_row, dql, slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL, nh, scale,
-                               (T*)dqkv)));
+                               dq, dq_row, dql, (const bf16*)slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL,
+                               nh, scale, (T*)dqkv)));
   TM_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int tm_nys_assemble_q_slab_inplace(const float* dql, const float* slab, int slabs, int nbags, int nh, int n,
+extern "C" int tm_nys_assemble_q_slab_inplace(const float* dql, const void* slab, int slabs, int nbags, int nh, int n,
                                               float scale, void* dqkv, void* stream) {
   TM_REQUIRE(n > 0 && n % NL == 0 && nh > 0 && nh <= 8 && slabs > 0, "assemble_q_slab_inplace: bad shape");
   TM_REQUIRE(dql && slab && dqkv && ((uintptr_t)dqkv % 16) == 0, "assemble_q_slab_inplace: null / misaligned operand");
   assemble_q_slab_kernel<bf16, true><<<dim3(NL, nbags), AQ_THREADS, 0, (hipStream_t)stream>>>(
-      nullptr, -1, dql, slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL, nh, scale, (bf16*)dqkv);
+      nullptr, -1, dql, (const bf16*)slab, slabs, (long long)nbags * nh * NL * DH, n, n / NL, nh, scale, (bf16*)dqkv);
   TM_CHECK_LAUNCH();
   return 0;
 }
