@@ -75,6 +75,9 @@ typedef struct tm_gemm_args {
   /* 1: the pre-activation store (pre) is bf16 whatever c_dtype (the bf16 step's _fc1: the GELU
    * backward reads it back in bf16, tm_fc1_gelu_bwd with TM_BF16); 0: c_dtype */
   int pre_bf16;
+  /* TM_EPI_SPLITK with bf16 operands: 1 = the split slabs are written bf16 (each split's partial
+   * rounded once; tm_splitk_reduce_bf16 sums them in fp32); 0: fp32 slabs (c_dtype TM_F32) */
+  int slab_bf16;
 } tm_gemm_args;
 
 int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* args, void* stream);
@@ -94,6 +97,9 @@ int tm_reduce_queue_pending(const tm_reduce_queue* rq); /* queued entries, -1 if
 int tm_reduce_flush(tm_reduce_queue* rq, void* stream);
 int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,
                      int accumulate, tm_reduce_queue* rq, void* stream);
+/* the same over bf16 slabs (tm_gemm_args.slab_bf16): the splits summed in fp32 in index order */
+int tm_splitk_reduce_bf16(const void* slab, float* out, int splits, long long count, float alpha,
+                          int accumulate, tm_reduce_queue* rq, void* stream);
 long long tm_colsum_workspace(int rows, int cols, int rows_per_chunk);
 int tm_colsum(const void* X, int dtype, int rows, int cols, int ld, int rows_per_chunk,
               float* work, float* out, int accumulate, tm_reduce_queue* rq, void* stream);

@@ -30,7 +30,7 @@ class GemmArgs(C.Structure):
                 ("drop_p", Fl), ("drop_scale", Fl), ("seed", U64), ("resid", P),
                 ("accumulate", I), ("grp_in", I), ("skip", I), ("grp_out", I),
                 ("out_off", I), ("dup_n", I), ("dup_off", I), ("nbags", I), ("nh", I),
-                ("dh", I), ("seq", I), ("qscale", Fl), ("seed_ptr", P), ("colsum", P), ("pre_bf16", I)]
+                ("dh", I), ("seq", I), ("qscale", Fl), ("seed_ptr", P), ("colsum", P), ("pre_bf16", I), ("slab_bf16", I)]
 
 
 class BmmJob(C.Structure):
@@ -68,6 +68,7 @@ _SIGS = {
     "tm_build_info": (C.c_char_p, []),
     "tm_gemm": (I, [P, P, P, C.POINTER(GemmArgs), P]),
     "tm_splitk_reduce": (I, [P, P, I, L, Fl, I, P, P]),
+    "tm_splitk_reduce_bf16": (I, [P, P, I, L, Fl, I, P, P]),
     "tm_colsum_workspace": (L, [I, I, I]),
     "tm_colsum": (I, [P, I, I, I, I, I, P, P, I, P, P]),
     "tm_layernorm_fwd": (I, [P, P, P, Fl, I, I, I, I, I, I, P, P, P, P]),

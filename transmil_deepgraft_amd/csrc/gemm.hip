@@ -221,6 +221,21 @@ TM_DEV void gemm_epilogue_rows(const char* smem, OutT* __restrict__ C, const tm_
   };
   if (KIND == EK_SPLITK || (KIND == EK_ANY && g.mode == TM_EPI_SPLITK)) {
     const size_t slab = (size_t)(split < 0 ? (int)blockIdx.z : split) * g.M * g.N;
+    if (g.slab_bf16) {   // bf16 slabs: each split's partial rounded once (summed in fp32 by the flush)
+      const bool vb = ne == 8 && g.N % 8 == 0;
+#pragma unroll 1
+      for (int it = 0; it < IT; ++it) {
+        const int m = m0 + lr0 + it * LRS;
+        if (m >= g.M) break;
+        float v[8];
+        chunk(it, v);
+        bf16* dst = (bf16*)C + slab + (size_t)m * g.N + n;
+        if (vb) store8<bf16>(dst, (bf16x8){(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3], (bf16)v[4], (bf16)v[5],
+                                           (bf16)v[6], (bf16)v[7]});
+        else { for (int e = 0; e < ne; ++e) dst[e] = (bf16)v[e]; }
+      }
+      return;
+    }
     const bool vec = ne == 8 && g.N % 4 == 0;
 #pragma unroll 1
     for (int it = 0; it < IT; ++it) {
@@ -1682,7 +1697,9 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, int rows, int col
 extern "C" int tm_gemm(const void* A, const void* B, void* C, const tm_gemm_args* g, void* stream) {
   TM_REQUIRE(g && A && B && C, "gemm: null argument");
   TM_REQUIRE(g->M >= 0 && g->N >= 0 && g->K >= 0 && g->splits >= 1, "gemm: bad shape");
-  TM_REQUIRE(g->mode != TM_EPI_SPLITK || g->c_dtype == TM_F32, "gemm: split-K slabs are fp32");
+  TM_REQUIRE(g->mode != TM_EPI_SPLITK || g->c_dtype == TM_F32, "gemm: split-K slabs are fp32 (or bf16 via slab_bf16)");
+  TM_REQUIRE(!g->slab_bf16 || (g->mode == TM_EPI_SPLITK && g->ab_dtype == TM_BF16),
+             "gemm: slab_bf16 is for bf16 split-K weight gradients");
   TM_REQUIRE(g->k_per_split > 0, "gemm: k_per_split must be > 0");
   TM_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0, "gemm: operands must be 16-B aligned");
   const int E = g->ab_dtype == TM_BF16 ? 8 : 4;
@@ -1890,6 +1907,11 @@ int tm_splitk_reduce_typed(const void* slab, int slab_dtype, float* out, int spl
   local.magic = RQ_MAGIC;
   push_reduce_entry(local.t, slab, 1, out, splits, count, alpha, accumulate);
   return tm_reduce_flush(&local, stream);
+}
+
+extern "C" int tm_splitk_reduce_bf16(const void* slab, float* out, int splits, long long count, float alpha,
+                                     int accumulate, tm_reduce_queue* q, void* stream) {
+  return tm_splitk_reduce_typed(slab, TM_BF16, out, splits, count, alpha, accumulate, q, stream);
 }
 
 extern "C" int tm_splitk_reduce(const float* slab, float* out, int splits, long long count, float alpha,

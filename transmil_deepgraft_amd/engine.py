@@ -176,10 +176,12 @@ def cu_count():
     return _CU[dev]
 
 
-def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=None):
+def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=None, slab_bf16=None):
     """out[M,N] (fp32) = sum_k dY[k, m] X[k, n]  (split-K, deterministic).  ``bias_out`` [M]: also
     the bias gradient sum_k dY[k, m] -- in bf16 mode summed by the weight-gradient kernel itself
-    while it stages dY (tm_gemm_args.colsum), else one tm_colsum pass."""
+    while it stages dY (tm_gemm_args.colsum), else one tm_colsum pass.  ``slab_bf16`` (default: the
+    bf16 mode): the split partials are stored bf16 (half the slab bytes written and read back by the
+    flush, which sums them in fp32 in split order); False keeps fp32 slabs."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     splits = max(1, min(16, cu_count() // max(tiles, 1), (K + 255) // 256))   # <= one workgroup per CU
     if splits == 1:
@@ -190,7 +192,9 @@ def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=Non
     bk = 64 if dtype == BF16 else 32
     kps = ((K + splits - 1) // splits + bk - 1) // bk * bk
     splits = (K + kps - 1) // kps
-    slab = work_pool(splits * M * N)
+    # bf16 mode: bf16 split slabs (each split's partial rounded once, summed in fp32 by the flush)
+    sb16 = dtype == BF16 if slab_bf16 is None else bool(slab_bf16) and dtype == BF16
+    slab = work_pool(splits * M * N, torch.bfloat16) if sb16 else work_pool(splits * M * N)
     g = GemmArgs()
     g.M, g.N, g.K = M, N, K
     g.lda, g.ldb, g.ldc = ldy, ldx, N
@@ -199,12 +203,14 @@ def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=Non
     g.splits, g.k_per_split = splits, kps
     g.mode = EPI_SPLITK
     g.alpha = 1.0
+    g.slab_bf16 = int(sb16)
     fuse = bias_out is not None and dtype == BF16 and K % 64 == 0 and M % 8 == 0 and N % 8 == 0
     cs = work_pool(splits * M) if fuse else None
     if fuse:
         g.colsum = cs.data_ptr()
     _lib.call("tm_gemm", _p(dY), _p(X), _p(slab), C.byref(g), _stream())
-    _lib.call("tm_splitk_reduce", _p(slab), _p(out), splits, M * N, C.c_float(1.0), 0, _rq(), _stream())
+    _lib.call("tm_splitk_reduce_bf16" if sb16 else "tm_splitk_reduce", _p(slab), _p(out), splits, M * N,
+              C.c_float(1.0), 0, _rq(), _stream())
     if fuse:
         _lib.call("tm_splitk_reduce", _p(cs), _p(bias_out), splits, M, C.c_float(1.0), 0, _rq(), _stream())
     elif bias_out is not None:
