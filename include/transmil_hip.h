@@ -173,8 +173,9 @@ int tm_nys_a1_fwd(int dtype, const void* q, const void* v, const void* kl_t, con
 int tm_nys_rowdot_cast(int dtype, const float* dw, const float* w, int rows, float* dd, void* dw_t, void* stream);
 int tm_cast_f32(int dtype, const float* x, void* y, long long count, void* stream);
 long long tm_nys_conv_bwd_workspace(int nbags, int nh, int n);
+/* dv [B*h, n, 64] in the step's dtype T (bf16 in the bf16 mode: the fused A3 backward reads it once) */
 int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merged, const void* v, const float* wconv,
-                    int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv,
+                    int nbh, int nh, int n, void* dv, float* d1, float* work, float* dwconv,
                     tm_reduce_queue* rq, void* stream);
 long long tm_nys_a1_bwd_workspace(int nbh, int n, int queries_per_wg);
 int tm_nys_a1_bwd(int dtype, const void* q, const void* dmerged, const void* kl_t, const void* y_t,
@@ -203,13 +204,14 @@ int tm_nys_assemble_dqkv(int dtype, const float* dq, const float* dql, const flo
                          const float* dv, int nbags, int nh, int n, float scale, void* dqkv, void* stream);
 /* bf16 mode, fused key side: the A3 backward writes the final bf16 k / v parts of dqkv
  * (k = dK + dk~[t/l]/l, v = dv_conv + dV) and dql (=) from its slabs; then tm_nys_assemble_q
- * writes the q part, scale * (dq + (dql_a + dql_b)[t/l]/l).  dv_conv is read only for rows
+ * writes the q part, scale * (dq + (dql_a + dql_b)[t/l]/l).  dv_conv (bf16, as tm_nys_conv_bwd /
+ * tm_cls_a1_row_bwd write it in the bf16 mode) is read only for rows
  * [dv_lo, dv_hi) (zero elsewhere; 0, n = dense); dq_row >= 0: dq is zero outside that row.
  * dql = NULL: the dq~ partial slab is left in work ([tm_nys_a3_bwd_slabs][B*h][256][64] bf16, each
  * partial rounded once; the consumers sum them in fp32) for tm_nys_assemble_q_slab, which reduces it
  * while writing the q part (one launch fewer). */
 int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v, const float* lse3,
-                        const float* d3, int nbh, int nh, int n, const float* dv_conv, int dv_lo, int dv_hi,
+                        const float* d3, int nbh, int nh, int n, const void* dv_conv, int dv_lo, int dv_hi,
                         const float* dkl, float* work, float* dql, void* dqkv, tm_reduce_queue* rq,
                         void* stream);
 int tm_nys_assemble_q(int dtype, const float* dq, int dq_row, const float* dql_a, const float* dql_b, int nbags,
@@ -440,7 +442,7 @@ int tm_cls_head_out_bwd(int dtype, const float* prob, const long long* label, co
                         float* dwo, float* dbo, void* dmerged, void* stream);
 int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, const void* v, const void* kl_t, const void* y_t,
                       const float* lse1, const float* wconv, int B, int nh, int n, int r, float* dq, float* dkl,
-                      float* dy, float* dv, float* dwconv, void* stream);
+                      float* dy, void* dv, float* dwconv, void* stream);   /* dv: the 33-row window, in T */
 /* bf16 mode: layer 2's q enters the loss only through its landmark means q~ (App. A eq. 4) and the
  * class row r, so dL/dq = dq~[t / l] / l on every row t plus the class row's own term, and the q
  * part of to_qkv's backward is two small products instead of a dense q block in dqkv:

@@ -485,7 +485,8 @@ def _conv_bwd_ref(dO, O, v, wconv, nh):
 @pytest.mark.gpu
 @pytest.mark.parametrize("nbags,n", [(1, 100), (1, 8448), (2, 1000), (4, 300)])
 def test_conv_bwd_bf16_mfma(nbags, n):
-    """The MFMA conv33 backward (bf16 mode) against fp64."""
+    """The MFMA conv33 backward (bf16 mode) against fp64; dv is written bf16 (the fused A3 backward
+    reads it once), d1 and the weight gradient fp32."""
     L = _lib()
     from transmil_deepgraft_amd._lib import BF16
     from transmil_deepgraft_amd.engine import _p, _stream
@@ -497,7 +498,7 @@ def test_conv_bwd_bf16_mfma(nbags, n):
     v = torch.randn(nbh, n, 64, generator=g).to(torch.bfloat16)
     wconv = torch.randn(nh, 33, generator=g) * 0.1
     ref_dv, ref_d1, ref_dw = _conv_bwd_ref(dO, O, v, wconv, nh)
-    dv = torch.full((nbh, n, 64), float("nan"), device=DEV)
+    dv = torch.full((nbh, n, 64), float("nan"), device=DEV, dtype=torch.bfloat16)   # dv in the step's dtype
     d1 = torch.full((nbh, n), float("nan"), device=DEV)
     dw = torch.full((nh * 33,), float("nan"), device=DEV)
     work = torch.empty(L.query("tm_nys_conv_bwd_workspace", nbags, nh, n) // 4 + 16, device=DEV)
@@ -506,7 +507,8 @@ def test_conv_bwd_bf16_mfma(nbags, n):
            _p(dw), None, _stream())
     torch.cuda.synchronize()
     assert torch.isfinite(dv).all() and torch.isfinite(d1).all() and torch.isfinite(dw).all()
-    assert _rel(dv.cpu(), ref_dv) < 1e-5
+    assert _rel(dv.cpu(), ref_dv) < 4e-3          # fp32 sums, one bf16 rounding (half an ulp: 2^-9)
+    assert _rel(dv.cpu(), ref_dv.to(torch.bfloat16)) < 4e-3
     assert (d1.cpu().double() - ref_d1).abs().max().item() < 1e-3 * ref_d1.abs().max().item()
     assert _rel(dw.cpu().view(nh, 33), ref_dw) < 1e-5
 

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(256) void a1_row_bwd_kernel(const T* __restrict__ d
                                                          const T* __restrict__ y_t, const float* __restrict__ lse1,
                                                          const float* __restrict__ wconv, int B, int nh, int n, int r,
                                                          float* __restrict__ dq, float* __restrict__ dkl,
-                                                         float* __restrict__ dy, float* __restrict__ dv,
+                                                         float* __restrict__ dy, T* __restrict__ dv,
                                                          float* __restrict__ dwconv) {
   __shared__ float red[4];
   __shared__ float gs[DH], qs[DH], dss[NL];
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void a1_row_bwd_kernel(const T* __restrict__ d
     // conv33 backward window
     for (int i = tid; i < TAPS * DH; i += 256) {
       const int tau = i / DH, dd = i % DH, t = r + tau - HALF;
-      if (t >= 0 && t < n) dv[((size_t)bh * n + t) * DH + dd] = wconv[h * TAPS + tau] * gs[dd];
+      if (t >= 0 && t < n) dv[((size_t)bh * n + t) * DH + dd] = from_f<T>(wconv[h * TAPS + tau] * gs[dd]);   // dv in T
     }
     return;
   }
@@ -499,13 +499,13 @@ extern "C" int tm_cls_head_out_bwd(int dtype, const float* prob, const long long
 
 extern "C" int tm_cls_a1_row_bwd(int dtype, const void* dmerged, const void* q, const void* v, const void* kl_t,
                                  const void* y_t, const float* lse1, const float* wconv, int B, int nh, int n, int r,
-                                 float* dq, float* dkl, float* dy, float* dv, float* dwconv, void* stream) {
+                                 float* dq, float* dkl, float* dy, void* dv, float* dwconv, void* stream) {
   TM_REQUIRE(dmerged && q && v && kl_t && y_t && lse1 && wconv && dq && dkl && dy && dv && dwconv && B > 0 && nh > 0,
              "cls_a1_row_bwd: bad args");
   TM_REQUIRE(n % NL == 0 && r >= 0 && r < n, "cls_a1_row_bwd: bad row / n");
   TM_CLS_DISPATCH(dtype, (a1_row_bwd_kernel<T><<<dim3(B * nh, 4), 256, 0, (hipStream_t)stream>>>(
                              (const T*)dmerged, (const T*)q, (const T*)v, (const T*)kl_t, (const T*)y_t, lse1, wconv,
-                             B, nh, n, r, dq, dkl, dy, dv, dwconv)));
+                             B, nh, n, r, dq, dkl, dy, (T*)dv, dwconv)));
   TM_CHECK_LAUNCH();
   return 0;
 }

@@ -1233,7 +1233,7 @@ __global__ void cast_rows_kernel(const float* __restrict__ x, T* __restrict__ y,
 template <typename T>
 __global__ __launch_bounds__(256, 2) void conv_bwd_kernel(const T* __restrict__ dmerged, const T* __restrict__ merged,
                                                        const T* __restrict__ v, const float* __restrict__ wconv,
-                                                       int n, int nh, float* __restrict__ dv, float* __restrict__ d1,
+                                                       int n, int nh, T* __restrict__ dv, float* __restrict__ d1,
                                                        float* __restrict__ dw_part) {
   constexpr int R = 64, HR = R + 2 * HALF, RW = DH + 4;  // 96 staged rows, 68-float rows
   constexpr int NTQ = (TAPS + 3) / 4;                    // taps per thread (9)
@@ -1349,9 +1349,9 @@ __global__ __launch_bounds__(256, 2) void conv_bwd_kernel(const T* __restrict__ 
           acc[e + 2] = fmaf(wt, x4[2], acc[e + 2]); acc[e + 3] = fmaf(wt, x4[3], acc[e + 3]);
         }
       }
-      float* dst = dv + ((size_t)bh * n + t) * DH + d0;
+      T* dst = dv + ((size_t)bh * n + t) * DH + d0;   // dv in the step's dtype
 #pragma unroll
-      for (int e = 0; e < 16; e += 4) *(f32x4*)(dst + e) = (f32x4){acc[e], acc[e + 1], acc[e + 2], acc[e + 3]};
+      for (int e = 0; e < 16; ++e) dst[e] = from_f<T>(acc[e]);
     }
   }
 }
@@ -1399,7 +1399,7 @@ __global__ __launch_bounds__(512) void conv_bwd_mfma_kernel(const bf16* __restri
                                                             const bf16* __restrict__ merged,
                                                             const bf16* __restrict__ v,
                                                             const float* __restrict__ wconv, int n, int nh, int R,
-                                                            float* __restrict__ dv, float* __restrict__ d1,
+                                                            bf16* __restrict__ dv, float* __restrict__ d1,
                                                             float* __restrict__ dw_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16* dos = (bf16*)(smem + CbLay::DO_OFF);
@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(512) void conv_bwd_mfma_kernel(const bf16* __restri
 #pragma unroll
       for (int reg = 0; reg < 16; ++reg) {
         const int l2 = 32 * i + acc_row(reg, h);
-        if (l2 < rows) dv[((size_t)bh * n + t0 + l2) * DH + dt * 32 + r32] = acc[reg];
+        if (l2 < rows) dv[((size_t)bh * n + t0 + l2) * DH + dt * 32 + r32] = (bf16)acc[reg];   // bf16: read once by the fused A3 backward
       }
     }
     __builtin_amdgcn_wave_barrier();   // the stage is rewritten by the wave's next tile
@@ -2124,7 +2124,7 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
     const int bag = bh / nh, hh = bh % nh, inner = nh * DH;
     bf16* outk = (bf16*)a.dqkv + ((size_t)bag * a.n_key_rows + key0) * 3 * inner + inner + hh * DH;
     bf16* outv = outk + inner;
-    const float* dvc = a.dv + bh * a.dv_bh + (size_t)key0 * DH;
+    const bf16* dvc = (const bf16*)a.dv + bh * a.dv_bh + (size_t)key0 * DH;   // the conv backward's dv (bf16)
     const float* dkl = a.dkl + (size_t)bh * NL * DH;
     f32x4 av[IT][2], ak[IT][2];
 #pragma unroll
@@ -2132,9 +2132,9 @@ __global__ __launch_bounds__(64 * NW) void attn_bwd_bf16_kernel(BwdArgs a) {
       const int i = tid + NT * it, key = i >> 3, d8 = (i & 7) * 8;
       const bool valid = key < nk;
       const bool vw = valid && key0 + key >= a.dv_lo && key0 + key < a.dv_hi;
-      const float* pv = dvc + (size_t)min(key, nk - 1) * DH + d8;
-      av[it][0] = vw ? *(const f32x4*)pv : (f32x4){0.f, 0.f, 0.f, 0.f};
-      av[it][1] = vw ? *(const f32x4*)(pv + 4) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      const bf16x8 pv = vw ? *(const bf16x8*)(dvc + (size_t)min(key, nk - 1) * DH + d8) : (bf16x8){};
+      av[it][0] = (f32x4){(float)pv[0], (float)pv[1], (float)pv[2], (float)pv[3]};
+      av[it][1] = (f32x4){(float)pv[4], (float)pv[5], (float)pv[6], (float)pv[7]};
     }
     float* stage_k = stage + LY::NK * 68;
 #pragma unroll
@@ -2577,7 +2577,7 @@ extern "C" long long tm_nys_conv_bwd_workspace(int nbags, int nh, int n) {
 }
 
 extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merged, const void* v, const float* wconv,
-                               int nbh, int nh, int n, float* dv, float* d1, float* work, float* dwconv,
+                               int nbh, int nh, int n, void* dv, float* d1, float* work, float* dwconv,
                                tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(nbh % nh == 0 && n > 0, "conv_bwd: bad shape");
   hipStream_t st = (hipStream_t)stream;
@@ -2585,13 +2585,13 @@ extern "C" int tm_nys_conv_bwd(int dtype, const void* dmerged, const void* merge
     const int r = conv_bwd_rows(nbh, n), nblk = (n + r - 1) / r;
     tm_allow_smem(conv_bwd_mfma_kernel, CbLay::BYTES);
     conv_bwd_mfma_kernel<<<dim3(nblk, nbh), 512, CbLay::BYTES, st>>>(
-        (const bf16*)dmerged, (const bf16*)merged, (const bf16*)v, wconv, n, nh, r, dv, d1, work);
+        (const bf16*)dmerged, (const bf16*)merged, (const bf16*)v, wconv, n, nh, r, (bf16*)dv, d1, work);
     TM_CHECK_LAUNCH();
     return tm_splitk_reduce(work, dwconv, (nbh / nh) * nblk, (long long)nh * TAPS, 1.0f, 0, rq, stream);
   }
   const int ntb = (n + 63) / 64;
   TM_DTYPE_DISPATCH(dtype, (conv_bwd_kernel<T><<<dim3(ntb, nbh), 256, 0, st>>>(
-                               (const T*)dmerged, (const T*)merged, (const T*)v, wconv, n, nh, dv, d1, work)));
+                               (const T*)dmerged, (const T*)merged, (const T*)v, wconv, n, nh, (T*)dv, d1, work)));
   TM_CHECK_LAUNCH();
   return tm_splitk_reduce(work, dwconv, (nbh / nh) * ntb, (long long)nh * TAPS, 1.0f, 0, rq, stream);
 }
@@ -2783,7 +2783,7 @@ extern "C" int tm_nys_a3_bwd(int dtype, const void* ql_t, const void* dw_t, cons
 // the conv backward's dv (fp32, read) and dk~ (fp32 [bh][256][64], after the pseudo-inverse
 // backward); dql3 (=) from the per-key-block slabs.
 extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const void* k, const void* v,
-                                   const float* lse3, const float* d3, int nbh, int nh, int n, const float* dv_conv,
+                                   const float* lse3, const float* d3, int nbh, int nh, int n, const void* dv_conv,
                                    int dv_lo, int dv_hi, const float* dkl, float* work, float* dql, void* dqkv,
                                    tm_reduce_queue* rq, void* stream) {
   TM_REQUIRE(n % NL == 0 && nbh % nh == 0, "a3_bwd_fused: n must be a multiple of 256");
@@ -2797,7 +2797,7 @@ extern "C" int tm_nys_a3_bwd_fused(const void* ql_t, const void* dw_t, const voi
   a.lse = lse3; a.lse_bh = NL; a.dd = d3; a.dd2 = d3 + (size_t)nbh * NL; a.dd_bh = NL;   // [2][nbh][256] partials
   a.dq = work; a.dq_bh = (long long)NL * DH;
   a.slab_stride = (long long)nbh * NL * DH;
-  a.dv = (float*)dv_conv; a.dv_bh = (long long)n * DH;
+  a.dv = (float*)dv_conv; a.dv_bh = (long long)n * DH;   // bf16 rows (the kernel reads them as bf16)
   a.nh = nh; a.n_queries_per_wg = NL; a.n_key_rows = n;
   a.dqkv = dqkv; a.dkl = dkl; a.l = n / NL; a.inv_l = 1.0f / (float)(n / NL);
   a.dv_lo = dv_lo; a.dv_hi = dv_hi;

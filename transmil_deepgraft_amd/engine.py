@@ -439,7 +439,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         # bf16 consumers read only that row / window, the fp32 path reads dense zero-filled buffers
         alloc = pool if fused else (lambda numel: torch.zeros(numel, dtype=torch.float32, device=q.device))
         dq = alloc(nbh * n * DH)
-        dv = alloc(nbh * n * DH)
+        dv = pool(nbh * n * DH, tdtype) if fused else alloc(nbh * n * DH)   # dv in T (the fused A3 reads bf16)
         _lib.call("tm_cls_a1_row_bwd", dt_code, _p(dmerged), _p(q), _p(v), _p(state["kl_t"]), _p(y_t),
                   _p(state["lse1"]), _p(wconv), geo.B, nh, n, cls_row, _p(dq), _p(dkl), _p(dy), _p(dv),
                   _p(dwconv_out), st)
@@ -449,7 +449,7 @@ def nystrom_core_backward(dmerged, merged, qkv, state, geo: Geometry, wconv, tdt
         # landmark term is added there in place at the end (tm_nys_assemble_q_slab_inplace)
         dqkv_early = pool(geo.B * n * 3 * nh * DH, tdtype).view(geo.B, n, 3 * nh * DH) if fused else None
         dq = None if fused else pool(nbh * n * DH)
-        dv = pool(nbh * n * DH)
+        dv = pool(nbh * n * DH, tdtype)      # the conv backward's dv in T (bf16 mode: read once by the fused A3)
         d1 = pool(nbh * n)
         with defer_reductions(), probe("conv_bwd"):
             work = pool(_lib.query("tm_nys_conv_bwd_workspace", geo.B, nh, n) // 4)
