@@ -186,7 +186,7 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
     a1f = 2 * n * d * t + 2 * lm * t + n * d * t + heads * n * f4   # q, v, k~, Y in; merged, lse1 out
     ppf = 2 * S * d * f4                             # H1 in, H2 out (fp32 residual stream)
     ppb = 3 * S * d * f4 + n * d * t                 # H1, dH in; dH1 out; layer 1's padded dropout gradient out
-    cvb = 3 * n * d * t + n * d * f4 + heads * n * f4   # dmerged, merged, v in; dv (fp32), D1 out
+    cvb = 4 * n * d * t + heads * n * f4   # dmerged, merged, v in; dv (in T, round 6), D1 out
     # q, dO in (T); lse1, D1 in; k~, Y (T) in; dq out (T: the precision dqkv carries); dk~, dY out (fp32)
     a1b = 2 * n * d * t + 2 * heads * n * f4 + 2 * lm * t + n * d * t + 2 * lm * f4
     a3b_small = 2 * lm * t + 2 * heads * m * f4 + lm * f4 + lm * f4   # q~, dW in, lse3, D3, dk~ in, dq~3 out

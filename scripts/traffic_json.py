@@ -25,6 +25,12 @@ def short(name):
     name = name.replace("(anonymous namespace)::", "")
     if name.startswith("void "):
         name = name[5:]
+    # names the profiler left mangled (a __bf16 parameter defeats its demangler):
+    # _ZN12_GLOBAL__N_1<len><identifier>I<template args>... -> the identifier
+    m = re.match(r"_ZN12_GLOBAL__N_1(\d+)", name)
+    if m:
+        i = m.end()
+        return name[i:i + int(m.group(1))]
     return re.sub(r"\(.*$", "", name).strip()
 
 
