@@ -176,6 +176,13 @@ def cu_count():
     return _CU[dev]
 
 
+# A/B knobs (scripts/dev/ab_env.sh only; defaults are the measured choices): workgroup slots the
+# split-K weight gradients size their splits for (0: one per CU), and the LayerNorm backward's rows
+# per block
+_WGRAD_SLOTS = int(os.environ.get("TM_WGRAD_SLOTS", "0"))
+_LN_BWD_RPB = int(os.environ.get("TM_LN_BWD_RPB", "8"))
+
+
 def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=None, slab_bf16=None):
     """out[M,N] (fp32) = sum_k dY[k, m] X[k, n]  (split-K, deterministic).  ``bias_out`` [M]: also
     the bias gradient sum_k dY[k, m] -- in bf16 mode summed by the weight-gradient kernel itself
@@ -183,7 +190,8 @@ def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=Non
     bf16 mode): the split partials are stored bf16 (half the slab bytes written and read back by the
     flush, which sums them in fp32 in split order); False keeps fp32 slabs."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
-    splits = max(1, min(16, cu_count() // max(tiles, 1), (K + 255) // 256))   # <= one workgroup per CU
+    slots = _WGRAD_SLOTS or cu_count()
+    splits = max(1, min(16, slots // max(tiles, 1), (K + 255) // 256))   # <= one workgroup per CU
     if splits == 1:
         gemm(dY, X, out, M, N, K, lda=ldy, ldb=ldx, ldc=N, a_trans=1, b_kn=1, dtype=dtype, c_dtype=F32)
         if bias_out is not None:
@@ -620,7 +628,7 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
                                         cls_row=pad if saved["cls_only"] else None,
                                         xn=saved["xn"] if qrows_on else None)
     dxn = pool(B * n * D, tdtype).view(B, n, D)
-    rpb = 8     # LN backward: 2 rows per wave, both requested up front (the partials go through the deferred reduce)
+    rpb = _LN_BWD_RPB   # LN backward: 8 = 2 rows per wave, both requested up front (partials via the deferred reduce)
     if qrows is None:
         # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
         with defer_reductions(), probe("wgrad_qkv"):
