@@ -180,7 +180,7 @@ def cu_count():
 # split-K weight gradients size their splits for (0: one per CU), and the LayerNorm backward's rows
 # per block
 _WGRAD_SLOTS = int(os.environ.get("TM_WGRAD_SLOTS", "0"))
-_LN_BWD_RPB = int(os.environ.get("TM_LN_BWD_RPB", "8"))
+_LN_BWD_RPB = int(os.environ.get("TM_LN_BWD_RPB", "16"))
 
 
 def weight_grad(dY, X, out, M, N, K, *, ldy, ldx, dtype, work_pool, bias_out=None, slab_bf16=None):
@@ -628,7 +628,8 @@ def translayer_backward(dH, H_in, saved, geo: Geometry, prm, grads, tdtype, dt_c
                                         cls_row=pad if saved["cls_only"] else None,
                                         xn=saved["xn"] if qrows_on else None)
     dxn = pool(B * n * D, tdtype).view(B, n, D)
-    rpb = _LN_BWD_RPB   # LN backward: 8 = 2 rows per wave, both requested up front (partials via the deferred reduce)
+    rpb = _LN_BWD_RPB   # LN backward rows per block: 16 = 4 rows per wave, one ahead in flight (partials via the
+                        # deferred reduce; 4 / 8 / 32 measured slower or level, profiles/r06w_*, r06x_*)
     if qrows is None:
         # to_qkv: dWqkv = dqkv^T xn ; dxn = dqkv Wqkv
         with defer_reductions(), probe("wgrad_qkv"):
