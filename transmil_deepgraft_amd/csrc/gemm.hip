@@ -1751,7 +1751,7 @@ struct ReduceEntry {
   int splits;
   int accumulate;
   float alpha;
-  int vec;   // 1: 16-B units (count % 4 == 0, both pointers 16-B aligned)
+  int vec;   // 1: 4-element units (count % 4 == 0, aligned); 2: bf16 slabs in 8-element units (16-B loads)
   int par;   // threads per output unit (power of 2 <= 64): each sums every par-th split, then a
              // fixed xor-shuffle tree (entries with many splits and few outputs, e.g. LayerNorm
              // weight partials of every 32-row block, would otherwise be one long serial loop)
@@ -1788,6 +1788,38 @@ __global__ __launch_bounds__(256) void multi_reduce_kernel(ReduceTable t) {
   const int par = r.par, sub = (int)(tt & (par - 1));
   const long long u = tt / par;
   constexpr int U = 12;
+  if (r.vec == 2) {   // bf16 slabs, 8 elements (one 16-B load) per unit: as many bytes in flight as fp32
+    const size_t j = (size_t)u * 8;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+    for (int z0 = sub; z0 < r.splits; z0 += U * par) {
+      bf16x8 v[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        v[k] = *(const bf16x8*)((const bf16*)r.slab + (size_t)min(z0 + k * par, r.splits - 1) * r.count + j);
+#pragma unroll
+      for (int k = 0; k < U; ++k)
+        if (z0 + k * par < r.splits) {
+          s0 += (f32x4){(float)v[k][0], (float)v[k][1], (float)v[k][2], (float)v[k][3]};
+          s1 += (f32x4){(float)v[k][4], (float)v[k][5], (float)v[k][6], (float)v[k][7]};
+        }
+    }
+    for (int o = 1; o < par; o <<= 1)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        s0[c] += __shfl_xor(s0[c], o, 64);
+        s1[c] += __shfl_xor(s1[c], o, 64);
+      }
+    if (sub) return;
+    s0 *= r.alpha;
+    s1 *= r.alpha;
+    if (r.accumulate) {
+      s0 += *(const f32x4*)(r.out + j);
+      s1 += *(const f32x4*)(r.out + j + 4);
+    }
+    *(f32x4*)(r.out + j) = s0;
+    *(f32x4*)(r.out + j + 4) = s1;
+    return;
+  }
   if (r.vec) {
     const size_t j = (size_t)u * 4;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
@@ -1874,8 +1906,11 @@ namespace {
 // one multi_reduce entry appended to t (the caller has made room)
 void push_reduce_entry(ReduceTable& t, const void* slab, int slab_bf16, float* out, int splits, long long count,
                        float alpha, int accumulate) {
-  const int vec = count % 4 == 0 && ((uintptr_t)slab % (slab_bf16 ? 8 : 16)) == 0 && ((uintptr_t)out % 16) == 0;
-  const long long units = vec ? count / 4 : count;
+  // vec 2: bf16 slabs in 8-element units (16-B loads); 1: 4-element units; 0: element by element
+  const int vec = slab_bf16 && count % 8 == 0 && ((uintptr_t)slab % 16) == 0 && ((uintptr_t)out % 16) == 0
+                      ? 2
+                      : (count % 4 == 0 && ((uintptr_t)slab % (slab_bf16 ? 8 : 16)) == 0 && ((uintptr_t)out % 16) == 0);
+  const long long units = vec == 2 ? count / 8 : vec ? count / 4 : count;
   // threads per unit: enough that each sums <= 2 bursts of 12 splits, while the entry keeps
   // to <= ~64 K threads
   int par = 1;
