@@ -653,6 +653,37 @@ def test_colsum_bf16_matches_fp64(rows, cols, ld, acc):
     assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=2e-3)   # fp32 sums of ~8 K terms of size ~1
 
 
+# ----------------------------------------------------------------------------- _fc1 GELU backward
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,N", [(1, 8192), (2, 300)])
+def test_fc1_gelu_bwd_against_fp64(dtype, B, N):
+    """tm_fc1_gelu_bwd: dpre[b, i] = (dH[b, 1 + i] + [i < add] dH[b, 1 + N + i]) * GELU'(pre[b, i]) and
+    dcls = sum_b dH[b, 0], against fp64 on the same (T-rounded) pre-activation: fp32 within 1e-6,
+    the bf16 result (one rounding) within 4e-3 of the max."""
+    from transmil_deepgraft_amd._lib import BF16, F32
+    from transmil_deepgraft_amd.engine import _p, _stream
+    L = _lib()
+    D = 512
+    G = math.ceil(math.sqrt(N))
+    add, S = G * G - N, G * G + 1
+    g = torch.Generator(device="cpu").manual_seed(N + B)
+    dH = torch.randn(B, S, D, generator=g)
+    pre = (torch.randn(B, N, D, generator=g) * 2.0).to(dtype)
+    dpre = torch.full((B, N, D), float("nan"), dtype=dtype, device=DEV)
+    dcls = torch.full((D,), float("nan"), device=DEV)
+    dHd, pred = dH.to(DEV).contiguous(), pre.to(DEV).contiguous()
+    L.call("tm_fc1_gelu_bwd", BF16 if dtype == torch.bfloat16 else F32, _p(dHd), _p(pred), B, N, S, add, D,
+           _p(dpre), _p(dcls), _stream())
+    torch.cuda.synchronize()
+    x = pre.double()
+    gd = 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+    up = dH[:, 1:1 + N].double().clone()
+    up[:, :add] += dH[:, 1 + N:1 + N + add].double()
+    ref = up * gd
+    assert _rel(dpre.cpu(), ref) < (1e-6 if dtype == torch.float32 else 4e-3)
+    assert _rel(dcls.cpu(), dH[:, 0].double().sum(0)) < 1e-6
+
+
 # ----------------------------------------------------------------------------- assemble_q_slab
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("dq_row", [-1, 300])
