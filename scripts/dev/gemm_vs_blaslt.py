@@ -29,7 +29,7 @@ dev = "cuda"
 M = 8448
 for name, N, K, bkn, cd in (("qkv", 1536, 512, 0, BF16), ("to_out", 512, 512, 0, F32),
                             ("dmerged", 512, 512, 1, BF16), ("dxn", 512, 1536, 1, BF16),
-                            ("fc1", 512, 1024, 0, F32)):
+                            ("fc1", 512, 512, 0, F32)):
     A = (torch.randn(M, K, device=dev) * 0.1).to(torch.bfloat16)
     Bm = ((torch.randn(K, N, device=dev) if bkn else torch.randn(N, K, device=dev)) * 0.1).to(torch.bfloat16)
     odt = torch.float32 if cd == F32 else torch.bfloat16
@@ -45,7 +45,7 @@ for name, N, K, bkn, cd in (("qkv", 1536, 512, 0, BF16), ("to_out", 512, 512, 0,
     fl = 2.0 * M * N * K
     print(f"{name:8s} M{M} N{N} K{K}: ours {t_ours:6.1f} us ({fl / t_ours / 1e6:5.0f} TF/s) | "
           f"hipBLASLt {t_lt:6.1f} us ({fl / t_lt / 1e6:5.0f} TF/s)", flush=True)
-for Mw, Nw in ((1536, 512), (512, 512), (512, 1024)):
+for Mw, Nw in ((1536, 512), (1024, 512), (512, 512)):
     dY = (torch.randn(M, Mw, device=dev) * 0.1).to(torch.bfloat16)
     X = (torch.randn(M, Nw, device=dev) * 0.1).to(torch.bfloat16)
     out = torch.empty(Mw, Nw, device=dev)
