@@ -167,6 +167,27 @@ def test_gemm_qkv_scatter(dtype):
     assert _rel(out.cpu(), ref) < tol
 
 
+@pytest.mark.parametrize("Bg,n", [(1, 8448), (2, 2304)])
+def test_gemm_qkv_scatter_big_tile(Bg, n):
+    """to_qkv at the step's sizes takes the 256 x 256 big-tile kernel (M >= 2048, N = 1536): the
+    head-major scatter + q scale against fp64, every output element written (two 128-row epilogue
+    passes per tile; n = 8448: 33 row tiles, the last one full; 2 x 2304: tiles straddle bags)."""
+    from transmil_deepgraft_amd.engine import gemm
+    from transmil_deepgraft_amd._lib import BF16
+    D, nh = 512, 8
+    g = torch.Generator().manual_seed(14)
+    x = (torch.randn(Bg * n, D, generator=g) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(3 * D, D, generator=g) * 0.05).to(torch.bfloat16)
+    out = torch.full((3, Bg * nh, n, 64), float("nan"), dtype=torch.bfloat16, device=DEV)
+    gemm(x.to(DEV), w.to(DEV), out, Bg * n, 3 * D, D, lda=D, ldb=D, ldc=0, dtype=BF16, qkv=(Bg, nh, 64, n, 0.125))
+    torch.cuda.synchronize()
+    ref = (x.double() @ w.double().t()).view(Bg, n, 3, nh, 64).permute(2, 0, 3, 1, 4).reshape(3, Bg * nh, n, 64)
+    ref[0] *= 0.125
+    got = out.cpu()
+    assert torch.isfinite(got).all()
+    assert _rel(got, ref) < 8e-3
+
+
 @pytest.mark.parametrize("N,K,b_kn,mode", [(512, 1536, 1, "plain"), (512, 512, 1, "plain"),
                                           (512, 512, 0, "to_out"), (1536, 512, 0, "qkv")])
 def test_gemm_160_row_tiles_at_bench_rows(N, K, b_kn, mode):

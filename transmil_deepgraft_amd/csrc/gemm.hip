@@ -264,11 +264,14 @@ TM_DEV void gemm_epilogue_rows(const char* smem, OutT* __restrict__ C, const tm_
     const int which = n / inner, hh = (n % inner) / g.dh, d = n % g.dh;
     const float qs = which == 0 ? g.qscale : 1.f;
     OutT* base = C + (((long long)which * g.nbags) * g.nh + hh) * g.seq * g.dh + d;
+    // (bag, t) of the thread's first row once; later rows step by LRS (< seq) -- no integer
+    // division per chunk (it cost ~30 VALU each in the 8-chunk big-tile passes)
+    int bag = (m0 + lr0) / g.seq, t = m0 + lr0 - bag * g.seq;
 #pragma unroll 1
-    for (int it = 0; it < IT; ++it) {
+    for (int it = 0; it < IT; ++it, t += LRS) {
       const int m = m0 + lr0 + it * LRS;
       if (m >= g.M) break;
-      const int bag = m / g.seq, t = m - bag * g.seq;
+      while (t >= g.seq) { t -= g.seq; ++bag; }
       OutT* dst = base + (long long)bag * g.nh * g.seq * g.dh + (long long)t * g.dh;
       float v[8];
       chunk(it, v);
@@ -1268,9 +1271,13 @@ TM_DEV void rd_big(bf16x8& f, unsigned base, unsigned kc_s) {
   }
 }
 
-template <typename OutT, bool A_T, bool B_KN, int TBN>
+constexpr int BIG_EROWS = 128;   // rows per epilogue pass of the big-tile kernel
+template <typename OutT, bool A_T, bool B_KN, int TBN, bool STAMP = false>   // STAMP: diagnostic variant 12
 __global__ __launch_bounds__(512) void gemm_big_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                        OutT* __restrict__ C, tm_gemm_args g) {
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  ring_stamp<STAMP>(ts, 0, true);
+  ring_stamp<STAMP>(ts, 1);
   constexpr int WM = TBN == 256 ? 2 : 4, WN = 8 / WM;
   constexpr int FM = GBM / WM / 32, FN = TBN / WN / 32;      // 32x32 MFMA tiles per wave
   constexpr int A_BYTES = GBM * 128, B_BYTES = TBN * 128, STG = A_BYTES + B_BYTES;
@@ -1335,6 +1342,7 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(const bf16* __restrict__ 
     if (ahead >= 1) wait_vm<LPW>(); else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (STAMP && kt == 0) ring_stamp<STAMP>(ts, 2);
     if (kt + NS - 1 < nk) issue(kt + NS - 1);
     const unsigned sb = ring + (kt % NS) * STG;
     bf16x8 af[2][FM], bf[2][FN];
@@ -1359,35 +1367,54 @@ __global__ __launch_bounds__(512) void gemm_big_kernel(const bf16* __restrict__ 
 #undef TM_BIG_READ
 #undef TM_BIG_MMA
   }
+  ring_stamp<STAMP>(ts, 3);
   __syncthreads();   // every fragment read done: the ring becomes the epilogue image
+  ring_stamp<STAMP>(ts, 4);
   float* ep = (float*)smem;
   constexpr int ROWF = TBN + 8;
+  // two passes of BIG_EROWS = 128 rows (the fp32 image, 135 KB at TBN = 256, fits beside nothing
+  // else; four 64-row passes took 17.6 k cycles of a 45 k-cycle workgroup: twice the barriers and
+  // staging phases, scripts/dev/qkv_big_stamps.py)
 #pragma unroll
-  for (int qtr = 0; qtr < GBM / 64; ++qtr) {
-    // rows 64 qtr .. +63: wave row wm covers rows wm * GBM/WM .. ; its frags i with 32-row blocks inside
+  for (int ph = 0; ph < GBM / BIG_EROWS; ++ph) {
+    // rows BIG_EROWS ph ..: wave row wm covers rows wm * GBM/WM .. ; its frags i with 32-row blocks inside
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int rb = wm * (GBM / WM) + i * 32;
-      if (rb / 64 == qtr) {
+      if (rb / BIG_EROWS == ph) {
         const int h = lane >> 5, l32 = lane & 31;
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int cb = wn * (TBN / WN) + j * 32;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) ep[(rb - 64 * qtr + acc_row(r, h)) * ROWF + cb + l32] = acc[i][j][r];
+          for (int r = 0; r < 16; ++r) ep[(rb - BIG_EROWS * ph + acc_row(r, h)) * ROWF + cb + l32] = acc[i][j][r];
         }
       }
     }
     __syncthreads();
-    gemm_epilogue_rows<OutT, TBN, 64, 512>((char*)smem, C, g, m0 + qtr * 64, n0);
+    gemm_epilogue_rows<OutT, TBN, BIG_EROWS, 512>((char*)smem, C, g, m0 + ph * BIG_EROWS, n0);
     __syncthreads();
+  }
+  if constexpr (STAMP) {   // (slots as the ring kernel's; 4 = staged is the k-loop barrier here)
+    ring_stamp<STAMP>(ts, 5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ring_stamp<STAMP>(ts, 6);
+    ring_stamp<STAMP>(ts, 7, true);
+    const int blk = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (tid < 8 && blk < 2048) {
+      unsigned long long v = ts[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) v = tid == i ? ts[i] : v;
+      g_gemm_stamps[blk * 8 + tid] = v;
+    }
   }
 }
 
 template <typename OutT, int TBN>
 constexpr int big_lds() {
   constexpr int ring = (TBN == 256 ? 2 : 3) * (GBM + TBN) * 128;
-  constexpr int epi = 64 * (TBN + 8) * 4;
+  constexpr int epi = BIG_EROWS * (TBN + 8) * 4;
+  static_assert(epi <= 160 * 1024, "big-tile epilogue image exceeds the LDS");
   return ring > epi ? ring : epi;
 }
 
@@ -1470,7 +1497,7 @@ inline bool qkv_big_enabled() {   // TM_GEMM_QKV_BIG=0: the 128 x 128 ring for t
 }
 template <typename OutT>
 bool big_ok(const tm_gemm_args& g) {
-  const bool qkv_pick = GEMM_VARIANT == 0 && g.mode == TM_EPI_QKV && g.N >= 1024 && g.splits == 1 && g.M >= 2048 &&
+  const bool qkv_pick = (GEMM_VARIANT == 0 || GEMM_VARIANT == 12) && g.mode == TM_EPI_QKV && g.N >= 1024 && g.splits == 1 && g.M >= 2048 &&
                         !g.a_trans && !g.b_kn && qkv_big_enabled();
   if (GEMM_VARIANT != 7 && !qkv_pick) return false;
   if (g.K % 64 != 0 || (g.splits > 1 && g.k_per_split % 64 != 0)) return false;
@@ -1484,11 +1511,21 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, g.splits);
   if constexpr (sizeof(T) == 2) {
     if (big_ok<OutT>(g)) {
+#ifdef TM_DIAG
+#define TM_BIG_STAMP(AT, BKN, TBN)                                                                   \
+      if (GEMM_VARIANT == 12) {   /* diagnostic: the QKV pick with per-workgroup stamps */         \
+        tm_allow_smem(gemm_big_kernel<OutT, AT, BKN, TBN, true>, sm);                                \
+        gemm_big_kernel<OutT, AT, BKN, TBN, true><<<gb, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
+      } else
+#else
+#define TM_BIG_STAMP(AT, BKN, TBN)
+#endif
 #define TM_BIG_CASE(AT, BKN, TBN)                                                                  \
       if (g.a_trans == AT && g.b_kn == BKN) {                                                      \
         constexpr int sm = big_lds<OutT, TBN>();                                                   \
         tm_allow_smem(gemm_big_kernel<OutT, AT, BKN, TBN>, sm);                                   \
         const dim3 gb((g.N + TBN - 1) / TBN, (g.M + GBM - 1) / GBM, g.splits);                      \
+        TM_BIG_STAMP(AT, BKN, TBN)                                                                 \
         gemm_big_kernel<OutT, AT, BKN, TBN><<<gb, 512, sm, st>>>((const bf16*)A, (const bf16*)B, (OutT*)C, g); \
         TM_CHECK_LAUNCH();                                                                         \
         return 0;                                                                                  \
@@ -1498,6 +1535,7 @@ int launch_t(const void* A, const void* B, void* C, const tm_gemm_args& g, hipSt
       } else {
         TM_BIG_CASE(0, 0, 128) TM_BIG_CASE(0, 1, 128) TM_BIG_CASE(1, 0, 128) TM_BIG_CASE(1, 1, 128)
       }
+#undef TM_BIG_STAMP
 #undef TM_BIG_CASE
     }
 #ifdef TM_DIAG
