@@ -120,15 +120,14 @@ TM_DEV void droppad_store4(const DropPad& dp, uint64_t seed, int b, int S, int D
 
 // grid (nchunk * ntiles, B), block 256
 template <bool BWD>
-__global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ src, int S, int G, int D,
-                                                          const float* __restrict__ wf, const float* __restrict__ bf,
-                                                          float* __restrict__ y, DropPad dp) {
+TM_DEV void ppeg_stencil_body(const float* __restrict__ src, int S, int G, int D, const float* __restrict__ wf,
+                              const float* __restrict__ bf, float* __restrict__ y, const DropPad& dp, int bx, int by) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* win = lds;                  // [WIN][CS]: x (forward) / dy (backward)
   float* wl = lds + WIN * CS;        // [49][CW] taps (flipped for the backward)
   const int nchunk = D / CW;
   const int tid = threadIdx.x, cq = tid & (NQ - 1), cp = (tid / NQ) & 3, orow = tid >> 5;
-  const int chunk = blockIdx.x % nchunk, t = blockIdx.x / nchunk, b = blockIdx.y;
+  const int chunk = bx % nchunk, t = bx / nchunk, b = by;
   const int ntc = (G + TC - 1) / TC, r0 = (t / ntc) * TR, c0 = (t % ntc) * TC;
   const int ch0 = chunk * CW + 4 * cq;
   const float* sb = src + (size_t)b * S * D + D + chunk * CW;
@@ -183,17 +182,23 @@ __global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restri
     }
   }
 }
+template <bool BWD>
+__global__ __launch_bounds__(256) void ppeg_stencil_kernel(const float* __restrict__ src, int S, int G, int D,
+                                                          const float* __restrict__ wf, const float* __restrict__ bf,
+                                                          float* __restrict__ y, DropPad dp) {
+  ppeg_stencil_body<BWD>(src, S, G, D, wf, bf, y, dp, blockIdx.x, blockIdx.y);
+}
 
 // grid (nchunk * ntr * ceil(ntc / WT), B), block 256; part: Z = B * ntr * ceil(ntc / WT) slabs in four
 // regions [Z][D][49], [Z][D][25], [Z][D][9], [Z][D] (see the store loop)
-__global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy_,
-                                                        int S, int G, int D, float* __restrict__ part) {
+TM_DEV void ppeg_wgrad_body(const float* __restrict__ x, const float* __restrict__ dy_, int S, int G, int D,
+                            float* __restrict__ part, int bx, int by, int gx, int gy) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* win = lds;                  // [WIN][CS] x window
   float* dyt = lds + WIN * CS;       // [TR * TC][CS] dy tile
   const int nchunk = D / CW;
   const int tid = threadIdx.x, cq = tid & (NQ - 1), g = tid / NQ;   // g < 28: tap row g >> 2, tile rows 2 (g & 3) ..
-  const int chunk = blockIdx.x % nchunk, grp = blockIdx.x / nchunk, b = blockIdx.y;
+  const int chunk = bx % nchunk, grp = bx / nchunk, b = by;
   const int ntc = (G + TC - 1) / TC, ngc = (ntc + WT - 1) / WT;
   const int tr = grp / ngc, tc0 = (grp % ngc) * WT;
   const float* xb = x + (size_t)b * S * D + D + chunk * CW;
@@ -255,7 +260,7 @@ __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict
   // four slab regions, each [Z][count] with Z = B * groups slabs (the deferred reduce sums a
   // region's slabs straight into one gradient): the folded 7x7 taps (= dw7), their 5x5 and 3x3
   // centres (the fold is a sum, so these are dw5 / dw3), and the bias sums (db7 = db5 = db3)
-  const size_t Z = (size_t)gridDim.y * (gridDim.x / nchunk), z = (size_t)b * (gridDim.x / nchunk) + grp;
+  const size_t Z = (size_t)gy * (gx / nchunk), z = (size_t)b * (gx / nchunk) + grp;
   float* p7 = part + z * D * NT;
   float* p5 = part + Z * D * NT + z * D * 25;
   float* p3 = part + Z * D * (NT + 25) + z * D * 9;
@@ -276,6 +281,18 @@ __global__ __launch_bounds__(256) void ppeg_wgrad_kernel(const float* __restrict
     if (trow >= 2 && trow <= 4 && dx >= 2 && dx <= 4) p3[(size_t)ch * 9 + (trow - 2) * 3 + dx - 2] = s;
   }
 }
+
+// The backward's two independent parts as ONE launch (grid (nwg + nst, B), LDS of the larger):
+// blocks [0, nwg) the weight gradient (three tiles each, so first), the rest the dx stencil.  One
+// launch boundary fewer, and each part's tail runs under the other's blocks.
+__global__ __launch_bounds__(256) void ppeg_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                      int S, int G, int D, const float* __restrict__ wf,
+                                                      float* __restrict__ dx, DropPad dp, float* __restrict__ part,
+                                                      int nwg) {
+  if ((int)blockIdx.x < nwg) ppeg_wgrad_body(x, dy, S, G, D, part, blockIdx.x, blockIdx.y, nwg, gridDim.y);
+  else ppeg_stencil_body<true>(dy, S, G, D, wf, nullptr, dx, dp, blockIdx.x - nwg, blockIdx.y);
+}
+constexpr int BWD_LDS = ST_LDS > WG_LDS ? ST_LDS : WG_LDS;
 
 }  // namespace
 
@@ -324,9 +341,8 @@ extern "C" int tm_ppeg_bwd(const float* x, const float* dy, int B, int G, int D,
   const int S = 1 + G * G;
   const DropPad dp{dout, dtype, n_pad, pad, p, p > 0.f ? 1.f / (1.f - p) : 1.f, seed, seed_ptr};
   const int ntiles = ((G + TR - 1) / TR) * ((G + TC - 1) / TC);
-  ppeg_stencil_kernel<true><<<dim3(ntiles * (D / CW), B), 256, ST_LDS, st>>>(dy, S, G, D, wfold, nullptr, dx, dp);
-  TM_CHECK_LAUNCH();
-  ppeg_wgrad_kernel<<<dim3(wgrad_groups(G) * (D / CW), B), 256, WG_LDS, st>>>(x, dy, S, G, D, work);
+  const int nwg = wgrad_groups(G) * (D / CW), nst = ntiles * (D / CW);
+  ppeg_bwd_kernel<<<dim3(nwg + nst, B), 256, BWD_LDS, st>>>(x, dy, S, G, D, wfold, dx, dp, work, nwg);
   TM_CHECK_LAUNCH();
   // the weight-gradient slabs summed in slab order into the unfolded gradients (deferred into the
   // caller's queue when it has one: the flush that finalises the PPEG gradients is one launch)
