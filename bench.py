@@ -201,7 +201,7 @@ def hbm_model(n_patches, dtype_bytes, d=512, heads=8, m=256, dh=64):
         ("a1_fwd", 1): ("a1_fwd_bf16_kernel", a1f),
         ("ppeg_fwd", 0): ("ppeg_stencil_kernel<false>", ppf),
         # (the weight-gradient slab sums ride in the deferred multi_reduce flush that follows)
-        ("ppeg_bwd", 0): ("ppeg_stencil_kernel<true> + ppeg_wgrad_kernel", ppb),
+        ("ppeg_bwd", 0): ("ppeg_bwd_kernel (weight gradient + dx stencil, one launch)", ppb),
         ("conv_bwd", 1): ("conv_bwd_mfma_kernel", cvb),
         # the kernel alone; its dk~ / dY partial slabs are summed in the deferred flush that follows
         ("a1_bwd", 1): ("attn_bwd_bf16_kernel<1, 8> (dk~ / dY slab sums in the deferred flush)", a1b),

@@ -89,7 +89,7 @@ def main():
             pats = {"ln_fwd": [r"ln_fwd_kernel"], "landmarks": [r"landmarks_kernel"],
                     "a3_fwd": [r"^a3_fwd_v2_kernel"], "a1_fwd": [r"^a1_fwd_bf16_kernel"],
                     "ppeg_fwd": [r"^ppeg_stencil_kernel<false>"],
-                    "ppeg_bwd": [r"^ppeg_stencil_kernel<true>", r"^ppeg_wgrad_kernel"],
+                    "ppeg_bwd": [r"^ppeg_bwd_kernel"],
                     "conv_bwd": [r"^conv_bwd_mfma_kernel"], "a1_bwd": [r"^attn_bwd_bf16_kernel<1, 8"],
                     "a3_bwd": [r"^attn_bwd_bf16_kernel<0, 9"]}[site]
             key = site if len(layers) == 1 else f"{site}:{layer}"
